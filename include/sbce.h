@@ -1,0 +1,146 @@
+/*
+ * sbce.h — C-ABI of libsbce.so, the MI355X-native EM semi-blind channel
+ * estimator for the MIMO-RIS cascaded channel.
+ *
+ * Drop-in boundary.  The reference has no native code: its
+ * operator is the Python function
+ *     em(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn,
+ *        itera, h_initial) -> theta (K,1) complex128
+ * ("Proposed method/Proposed_method_NMSEvsTp.py":50-83, called at :165; same
+ * contract at "Proposed method/Proposed_method_NMSEvsTd.py":44/150 and
+ * "Proposed method/SNR/all_Detectors.py":242/377).  The build's Python shim
+ * (package em.py) keeps that signature, stacks the per-symbol lists into
+ * batch-major device buffers and calls sbce_em() through ctypes.  Every entry
+ * point below is what that ctypes binding declares.
+ *
+ * Conventions
+ *   - complex numbers are interleaved float64 pairs (re, im), i.e. numpy
+ *     complex128 / torch.complex128 memory;
+ *   - every pointer in sbce_ptrs is a DEVICE pointer owned by the caller
+ *     (e.g. torch.empty(..., device="cuda").data_ptr()); the library never
+ *     allocates, keeps no global state and never synchronises the stream;
+ *   - all work is stream-ordered on `hip_stream` (a hipStream_t, 0 = default);
+ *   - return value 0 on success, a negative SBCE_E* code otherwise; nothing
+ *     throws across the ABI.  Per-trial numerical status goes to ptrs->status.
+ *
+ * Batch-major layouts (B = dims.batch, P = dims.n_psi = N+1 with the direct
+ * path, L = P*n_tx, K = L*n_rx):
+ *   y_d      [B][T_d][n_rx]          data observations   (reference Y_d list)
+ *   y_p      [B][T_p][n_rx]          pilot observations  (reference Y_p list)
+ *   psi_d    [B][T_d][P]             RIS phases, TRANSPOSED reference
+ *                                    PsiTilde_td ((N+1) x T_d, row 0 = direct)
+ *   u_p      [B][T_p][L]             pilot regressors u_p = psi_p (x) x_p, i.e.
+ *                                    Z_p[t] = u_p^T (x) I_{n_rx}
+ *   cons     [M]                     constellation, table order of
+ *                                    all_possibleSymbols' last column
+ *   theta    [B][K]                  in: h_initial, out: estimate; reference
+ *                                    vec order theta[(p*n_tx+a)*n_rx + r]
+ *   x_d_true [B][T_d][n_tx]          optional (LLF genie term)
+ *   llf      [B][iters] float64      optional output (IterationsvsLLF.py:76)
+ *   h_true   [B][K]                  optional: enables the reference's oracle
+ *                                    early stop (PM.py:110-112)
+ *   iters_done [B] int32             optional output: iterations performed
+ *   status   [B] int32               per-trial flags (bit 0: non-HPD pivot)
+ */
+#ifndef SBCE_H_
+#define SBCE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SBCE_ABI_VERSION 1
+
+/* return codes */
+#define SBCE_OK 0
+#define SBCE_EINVAL (-1)        /* bad dims / null pointer / misaligned */
+#define SBCE_EUNSUPPORTED (-2)  /* shape outside the compiled kernel set */
+#define SBCE_EHIP (-3)          /* a HIP launch failed */
+#define SBCE_EWORKSPACE (-4)    /* workspace too small */
+
+/* E-step modes */
+#define SBCE_ESTEP_SOFT 0       /* exact posterior over all M^n_tx hypotheses:
+                                   Proposed_method_NMSEvsTp.py:61-71 */
+#define SBCE_ESTEP_HARD 1       /* argmax posterior ("log-max"):
+                                   ML_detecctor.py:65-77 */
+
+/* M-step solve modes (SURVEY.md §7 hard part 3) */
+#define SBCE_SOLVE_CHOL 0       /* Hermitian Cholesky of the reduced L x L system
+                                   (== LU of the K x K reference system,
+                                   Proposed_method_NMSEvsTp.py:80, on HPD R) */
+#define SBCE_SOLVE_CHOL_DROP 1  /* non-HPD pivots dropped (solution restricted to
+                                   the well-posed subspace; lstsq-like, PM.py:108) */
+
+/* per-trial status bits */
+#define SBCE_STATUS_NONHPD 1
+
+typedef struct sbce_dims {
+    int32_t batch;      /* B: independent Monte-Carlo trials */
+    int32_t n_tx;       /* streams (1..4 for the exact E-step) */
+    int32_t n_rx;       /* receive antennas (1..8) */
+    int32_t n_psi;      /* P = rows of PsiTilde_td (N+1 with the direct path) */
+    int32_t t_p;        /* pilot symbols */
+    int32_t t_d;        /* data symbols */
+    int32_t m;          /* constellation size (power of two, 2..64) */
+    int32_t reserved;   /* must be 0 */
+    double varn;        /* noise variance parameter; posterior uses varn^2 */
+} sbce_dims;
+
+typedef struct sbce_ptrs {
+    const void* y_d;
+    const void* y_p;
+    const void* psi_d;
+    const void* u_p;
+    const void* cons;
+    void* theta;
+    const void* x_d_true;   /* may be NULL */
+    double* llf;            /* may be NULL (requires x_d_true) */
+    const void* h_true;     /* may be NULL */
+    int32_t* iters_done;    /* may be NULL */
+    int32_t* status;        /* may be NULL */
+    void* workspace;
+    size_t workspace_bytes;
+} sbce_ptrs;
+
+/* ABI version (SBCE_ABI_VERSION). */
+int sbce_abi_version(void);
+
+/* Static description of an error code. */
+const char* sbce_strerror(int code);
+
+/* Device workspace needed by sbce_em / sbce_estep / sbce_mstep for `d`. */
+int sbce_workspace_bytes(const sbce_dims* d, size_t* bytes);
+
+/* Full EM: `iters` iterations of E-step + M-step on every trial of the batch.
+ * Replaces em() at Proposed_method_NMSEvsTp.py:50-83 (estep_mode SOFT) and the
+ * hard-ML em() at ML_detecctor.py:51-86 (estep_mode HARD, llf != NULL). */
+int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode,
+            int solve_mode, void* hip_stream);
+
+/* One E-step: theta -> per-symbol posterior moments, written to `moments`
+ * [B][T_d][n_tx + n_tx*n_tx] complex (m_t, then S_t row-major,
+ * S_t[a][b] = E[x_a conj(x_b)]).  Test/diagnostic entry point for the
+ * E-step of Proposed_method_NMSEvsTp.py:61-69. */
+int sbce_estep(const sbce_dims* d, const sbce_ptrs* p, int estep_mode,
+               void* moments, void* hip_stream);
+
+/* One M-step from given moments: builds R = sum_p u u^H + sum_t (psi psi^H)(x)S_t
+ * and B^H, solves R X = B^H and writes theta = conj(X) in reference vec order
+ * (Proposed_method_NMSEvsTp.py:70-80 with commutation_matrix.py:3-8 applied).
+ * If `r_out` / `rhs_out` are non-NULL the normal equations ([B][L][L] and
+ * [B][L][n_rx] complex) are copied there before the solve. */
+int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments,
+               int solve_mode, void* r_out, void* rhs_out, void* hip_stream);
+
+/* Per-trial NMSE ||theta - h||^2 / ||h||^2 (Proposed_method_NMSEvsTp.py:172). */
+int sbce_nmse(const sbce_dims* d, const void* theta, const void* h_true,
+              double* nmse_out, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SBCE_H_ */

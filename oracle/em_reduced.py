@@ -1,0 +1,131 @@
+"""Reduced-form float64 restatement of the EM estimator (oracle face 2).
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Model (SURVEY.md §8 preamble): theta = vec(H_c), H_c is n_rx x L with
+L = P * n_tx (P = number of RIS-phase rows, N+1 with the direct path), column
+index p*n_tx + a, so theta[(p*n_tx + a)*n_rx + r] = H_c[r, p*n_tx + a]
+(PMd/PM.py:11-17 'F'-order vec).  With u_{t,j} = psi_t (x) x_j the reference's
+regressor is Z_{t,j} = u^T (x) I_{n_rx} (PMd/Proposed_method_NMSEvsTp.py:65), so
+  * Z theta = H_c u,  Z^H Z = conj(u u^H) (x) I,  Z^H y = vec(y u^H)
+    (the commutation identity of PMd/commutation_matrix.py:3-8);
+  * the K x K normal equations of PMd/Proposed_method_NMSEvsTp.py:70-80 collapse
+    to ONE L x L Hermitian system with n_rx right-hand sides:  H_c R = B with
+      R = sum_p u_p u_p^H + sum_t (psi_t psi_t^H) (x) S_t,
+      B = sum_p y_p u_p^H + sum_t y_t (psi_t (x) m_t)^H,
+    m_t = E[x | y_t], S_t = E[x x^H | y_t] under the posterior beta_{t,j}
+    (PMd/Proposed_method_NMSEvsTp.py:61-69; posterior exponent uses varn**2).
+"""
+import numpy as np
+
+
+def u_from_zp(Z_p, n_rx):
+    """Pilot regressors u_p (T_p x L) from the reference's Z_p list (row 0 of
+    u^T (x) I holds u at every n_rx-th column)."""
+    Z = np.asarray(Z_p)
+    return Z[:, 0, ::n_rx].copy()
+
+
+def cons_from_aps(all_possibleSymbols, M):
+    """Constellation in table order: the last stream cycles fastest in
+    itertools.product order (PMd/Proposed_method_NMSEvsTp.py:32-38)."""
+    return np.asarray(all_possibleSymbols)[:M, -1].copy()
+
+
+def aps_from_cons(cons, n_tx):
+    """All J = M^n_tx hypotheses in itertools.product order (first stream slowest)."""
+    cons = np.asarray(cons)
+    M = cons.size
+    idx = np.indices((M,) * n_tx).reshape(n_tx, -1).T
+    return cons[idx]
+
+
+def heff(theta, Psi, n_tx, n_rx):
+    """Effective channel per symbol H_eff(t) = sum_p psi_{p,t} H_c[:, p*n_tx:(p+1)*n_tx]
+    -> (T, n_rx, n_tx)."""
+    P = Psi.shape[0]
+    H3 = np.asarray(theta).reshape(P, n_tx, n_rx)          # [p, a, r]
+    return np.einsum("par,pt->tra", H3, Psi)
+
+
+def estep_moments(theta, Y_d, Psi, aps, varn, mode="soft", chunk=8):
+    """Posterior moments per data symbol.
+
+    mode 'soft': beta_{t,j} = softmax_j(-||y_t - Z_{t,j} theta||^2 / varn^2)
+                 (PMd/Proposed_method_NMSEvsTp.py:61-69)
+    mode 'hard': one-hot at argmax_j beta (first index on ties)
+                 (PMd/ML_detecctor.py:65-75)
+    Returns m (T, n_tx), S (T, n_tx, n_tx) with S[a,b] = E[x_a conj(x_b)],
+    dmin (T,) and logZ (T,) = log sum_j exp(-(d_j - dmin)/varn^2).
+    """
+    aps = np.asarray(aps)
+    J, n_tx = aps.shape
+    n_rx = Y_d.shape[1]
+    H = heff(theta, Psi, n_tx, n_rx)                          # (T, n_rx, n_tx)
+    T = Y_d.shape[0]
+    m = np.empty((T, n_tx), dtype=complex)
+    S = np.empty((T, n_tx, n_tx), dtype=complex)
+    dmin = np.empty(T)
+    logZ = np.empty(T)
+    inv = 1.0 / np.power(varn, 2)
+    outer = aps[:, :, None] * np.conj(aps)[:, None, :]       # (J, n_tx, n_tx)
+    for t0 in range(0, T, chunk):
+        t1 = min(T, t0 + chunk)
+        Hx = np.einsum("tra,ja->tjr", H[t0:t1], aps)          # (c, J, n_rx)
+        r = Y_d[t0:t1, None, :] - Hx
+        d = np.sum(r.real ** 2 + r.imag ** 2, axis=2)         # (c, J)
+        dm = d.min(axis=1)
+        dmin[t0:t1] = dm
+        if mode == "hard":
+            js = np.argmin(d, axis=1)
+            w = np.zeros_like(d)
+            w[np.arange(t1 - t0), js] = 1.0
+            logZ[t0:t1] = 0.0
+        else:
+            w = np.exp(-(d - dm[:, None]) * inv)
+            z = w.sum(axis=1)
+            logZ[t0:t1] = np.log(z)
+            w /= z[:, None]
+        m[t0:t1] = w @ aps
+        S[t0:t1] = np.einsum("tj,jab->tab", w, outer)
+    return m, S, dmin, logZ
+
+
+def mstep_build(U_p, Y_p, Psi, Y_d, m, S):
+    """Reduced normal equations (R: L x L Hermitian, rhs = B^H: L x n_rx)."""
+    P, T = Psi.shape
+    n_tx = m.shape[1]
+    L = P * n_tx
+    R = U_p.T @ np.conj(U_p)
+    R = R + np.einsum("pt,qt,tab->paqb", Psi, np.conj(Psi), S).reshape(L, L)
+    rhs = U_p.T @ np.conj(Y_p)
+    rhs = rhs + np.einsum("pt,ta,tr->par", Psi, m, np.conj(Y_d)).reshape(L, -1)
+    return R, rhs
+
+
+def mstep_solve(R, rhs):
+    """H_c R = B  <=>  R H_c^H = B^H; theta[l*n_rx + r] = conj(X[l, r])
+    (PMd/Proposed_method_NMSEvsTp.py:80 np.linalg.solve on the K x K form)."""
+    X = np.linalg.solve(R, rhs)
+    return np.conj(X).reshape(-1)
+
+
+def em_reduced(Y_d, Y_p, U_p, Psi, aps, varn, itera, theta0, mode="soft",
+               return_trace=False):
+    """Reduced-form EM over one trial.  Inputs in array form:
+    Y_d (T_d, n_rx), Y_p (T_p, n_rx), U_p (T_p, L), Psi (P, T_d), aps (J, n_tx)."""
+    theta = np.asarray(theta0, dtype=complex).reshape(-1)
+    trace = []
+    for _ in range(itera):
+        m, S, _, _ = estep_moments(theta, Y_d, Psi, aps, varn, mode)
+        R, rhs = mstep_build(U_p, Y_p, Psi, Y_d, m, S)
+        theta = mstep_solve(R, rhs)
+        trace.append(theta.copy())
+    return (theta, trace) if return_trace else theta
+
+
+def nmse(theta, h):
+    """PMd/Proposed_method_NMSEvsTp.py:172: ||theta - h||^2 / ||h||^2."""
+    theta = np.asarray(theta).reshape(-1)
+    h = np.asarray(h).reshape(-1)
+    return float(np.sum(np.abs(theta - h) ** 2) / np.sum(np.abs(h) ** 2))

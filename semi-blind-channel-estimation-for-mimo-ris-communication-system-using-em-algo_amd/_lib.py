@@ -1,0 +1,93 @@
+"""ctypes binding of libsbce.so (C-ABI declared in include/sbce.h).
+
+This is the ONLY way the package reaches its compute path.  There is no CPU
+fallback: if the shared library is missing, or no HIP device is visible, the
+calls raise ``SbceUnavailable``.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsbce.so")
+
+SBCE_ABI_VERSION = 1
+SBCE_ESTEP_SOFT = 0
+SBCE_ESTEP_HARD = 1
+SBCE_SOLVE_CHOL = 0
+SBCE_SOLVE_CHOL_DROP = 1
+SBCE_STATUS_NONHPD = 1
+
+EXPORTED = ("sbce_abi_version", "sbce_strerror", "sbce_workspace_bytes", "sbce_em",
+            "sbce_estep", "sbce_mstep", "sbce_nmse")
+
+
+class SbceUnavailable(RuntimeError):
+    """libsbce.so is not built or no GPU is available (the product never falls back)."""
+
+
+class SbceError(RuntimeError):
+    pass
+
+
+class Dims(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int32), ("n_tx", ctypes.c_int32), ("n_rx", ctypes.c_int32),
+                ("n_psi", ctypes.c_int32), ("t_p", ctypes.c_int32), ("t_d", ctypes.c_int32),
+                ("m", ctypes.c_int32), ("reserved", ctypes.c_int32), ("varn", ctypes.c_double)]
+
+
+class Ptrs(ctypes.Structure):
+    _fields_ = [("y_d", ctypes.c_void_p), ("y_p", ctypes.c_void_p), ("psi_d", ctypes.c_void_p),
+                ("u_p", ctypes.c_void_p), ("cons", ctypes.c_void_p), ("theta", ctypes.c_void_p),
+                ("x_d_true", ctypes.c_void_p), ("llf", ctypes.c_void_p),
+                ("h_true", ctypes.c_void_p), ("iters_done", ctypes.c_void_p),
+                ("status", ctypes.c_void_p), ("workspace", ctypes.c_void_p),
+                ("workspace_bytes", ctypes.c_size_t)]
+
+
+_lib = None
+
+
+def load(path=None):
+    """Load libsbce.so (CPU-safe: loading does not touch the GPU)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise SbceUnavailable(f"{p} not built: run __graft_entry__.build()")
+    lib = ctypes.CDLL(p)
+    lib.sbce_abi_version.restype = ctypes.c_int
+    lib.sbce_abi_version.argtypes = []
+    lib.sbce_strerror.restype = ctypes.c_char_p
+    lib.sbce_strerror.argtypes = [ctypes.c_int]
+    lib.sbce_workspace_bytes.restype = ctypes.c_int
+    lib.sbce_workspace_bytes.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(ctypes.c_size_t)]
+    lib.sbce_em.restype = ctypes.c_int
+    lib.sbce_em.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Ptrs), ctypes.c_int,
+                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    lib.sbce_estep.restype = ctypes.c_int
+    lib.sbce_estep.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Ptrs), ctypes.c_int,
+                               ctypes.c_void_p, ctypes.c_void_p]
+    lib.sbce_mstep.restype = ctypes.c_int
+    lib.sbce_mstep.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Ptrs), ctypes.c_void_p,
+                               ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.sbce_nmse.restype = ctypes.c_int
+    lib.sbce_nmse.argtypes = [ctypes.POINTER(Dims), ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.c_void_p, ctypes.c_void_p]
+    if lib.sbce_abi_version() != SBCE_ABI_VERSION:
+        raise SbceUnavailable("libsbce ABI version mismatch")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().sbce_strerror(rc).decode()
+        raise SbceError(f"{what} failed: {msg} ({rc})")
+
+
+def workspace_bytes(dims):
+    n = ctypes.c_size_t(0)
+    check(load().sbce_workspace_bytes(ctypes.byref(dims), ctypes.byref(n)), "sbce_workspace_bytes")
+    return n.value

@@ -1,0 +1,190 @@
+// extern "C" entry points of libsbce.so (declared in include/sbce.h).
+//
+// The EM loop replaces em() of "Proposed method/Proposed_method_NMSEvsTp.py":50-83
+// for a whole batch of Monte-Carlo trials: per iteration one E-step launch over
+// every (trial, symbol), one normal-equation build and one batched Cholesky
+// solve, all stream-ordered, with no host synchronisation and no allocation.
+#include <string.h>
+
+#include "sbce_internal.h"
+
+using namespace sbce;
+
+namespace {
+
+constexpr size_t kAlign = 256;
+size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
+
+struct Carve {
+    size_t mom, R, rhs, done, total;
+};
+
+bool make_problem(const sbce_dims* d, Problem& pb) {
+    if (!d) return false;
+    if (d->batch < 0 || d->n_tx < 1 || d->n_rx < 1 || d->n_psi < 1 || d->t_p < 0 || d->t_d < 1 ||
+        d->m < 2 || d->reserved != 0 || !(d->varn > 0.0))
+        return false;
+    if (d->n_tx > 4 || d->n_rx > 8) return false;
+    pb.B = d->batch; pb.NT = d->n_tx; pb.NR = d->n_rx; pb.P = d->n_psi;
+    pb.Tp = d->t_p; pb.Td = d->t_d; pb.M = d->m; pb.varn = d->varn;
+    pb.L = pb.P * pb.NT;
+    pb.K = pb.L * pb.NR;
+    return true;
+}
+
+Carve carve(const Problem& pb) {
+    Carve c;
+    const size_t MS = (size_t)pb.NT + (size_t)pb.NT * pb.NT;
+    c.mom = 0;
+    c.R = align_up(c.mom + (size_t)pb.B * pb.Td * MS * sizeof(cd));
+    c.rhs = align_up(c.R + (size_t)pb.B * pb.L * pb.L * sizeof(cd));
+    c.done = align_up(c.rhs + (size_t)pb.B * pb.L * pb.NR * sizeof(cd));
+    c.total = align_up(c.done + (size_t)pb.B * sizeof(int32_t));
+    return c;
+}
+
+int hip_rc(hipError_t e) { return e == hipSuccess ? SBCE_OK : SBCE_EHIP; }
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+int check_ptrs(const sbce_ptrs* p, const Problem& pb, bool need_ws) {
+    if (!p) return SBCE_EINVAL;
+    const void* req[] = {p->y_d, p->y_p, p->psi_d, p->u_p, p->cons, p->theta};
+    for (const void* q : req)
+        if (!q || !aligned16(q)) return SBCE_EINVAL;
+    if (pb.Tp == 0) { /* pilots optional */ }
+    if (need_ws) {
+        if (!p->workspace || !aligned16(p->workspace)) return SBCE_EINVAL;
+        if (p->workspace_bytes < carve(pb).total) return SBCE_EWORKSPACE;
+    }
+    return SBCE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sbce_abi_version(void) { return SBCE_ABI_VERSION; }
+
+const char* sbce_strerror(int code) {
+    switch (code) {
+        case SBCE_OK: return "ok";
+        case SBCE_EINVAL: return "invalid argument (dims, null or misaligned pointer)";
+        case SBCE_EUNSUPPORTED: return "shape not supported by the compiled kernel set";
+        case SBCE_EHIP: return "HIP launch failed";
+        case SBCE_EWORKSPACE: return "workspace too small";
+    }
+    return "unknown error";
+}
+
+int sbce_workspace_bytes(const sbce_dims* d, size_t* bytes) {
+    Problem pb;
+    if (!bytes || !make_problem(d, pb)) return SBCE_EINVAL;
+    *bytes = carve(pb).total;
+    return SBCE_OK;
+}
+
+int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, int solve_mode,
+            void* hip_stream) {
+    Problem pb;
+    if (!make_problem(d, pb) || iters < 0) return SBCE_EINVAL;
+    int rc = check_ptrs(p, pb, true);
+    if (rc) return rc;
+    if (!estep_supported(pb, estep_mode)) return SBCE_EUNSUPPORTED;
+    if (solve_mode != SBCE_SOLVE_CHOL && solve_mode != SBCE_SOLVE_CHOL_DROP) return SBCE_EINVAL;
+    if (p->llf && !p->x_d_true) return SBCE_EINVAL;
+    if (pb.B == 0 || iters == 0) return SBCE_OK;
+    hipStream_t s = (hipStream_t)hip_stream;
+    const Carve c = carve(pb);
+    char* ws = (char*)p->workspace;
+    int32_t* done = (int32_t*)(ws + c.done);
+    if (hipMemsetAsync(done, 0, (size_t)pb.B * sizeof(int32_t), s) != hipSuccess) return SBCE_EHIP;
+    if (p->status && hipMemsetAsync(p->status, 0, (size_t)pb.B * sizeof(int32_t), s) != hipSuccess)
+        return SBCE_EHIP;
+    const bool early = p->h_true != nullptr;
+
+    EstepArgs ea;
+    ea.yd = (const cd*)p->y_d; ea.psid = (const cd*)p->psi_d; ea.theta = (const cd*)p->theta;
+    ea.cons = (const cd*)p->cons; ea.mom = (cd*)(ws + c.mom); ea.done = early ? done : nullptr;
+    MstepArgs ma;
+    ma.yd = ea.yd; ma.yp = (const cd*)p->y_p; ma.psid = ea.psid; ma.up = (const cd*)p->u_p;
+    ma.mom = ea.mom; ma.R = (cd*)(ws + c.R); ma.rhs = (cd*)(ws + c.rhs); ma.theta = (cd*)p->theta;
+    ma.status = p->status; ma.done = ea.done; ma.solve_mode = solve_mode;
+
+    for (int it = 0; it < iters; ++it) {
+        if ((rc = hip_rc(launch_estep(pb, ea, estep_mode, s)))) return rc;
+        if ((rc = hip_rc(launch_mstep_build(pb, ma, s)))) return rc;
+        if ((rc = hip_rc(launch_chol_solve(pb, ma, s)))) return rc;
+        if (p->llf &&
+            (rc = hip_rc(launch_llf(pb, ma.theta, ma.yp, ma.up, ma.yd, ma.psid,
+                                    (const cd*)p->x_d_true, p->llf, iters, it, ea.done, s))))
+            return rc;
+        if (early &&
+            (rc = hip_rc(launch_early_stop(pb, ma.theta, (const cd*)p->h_true, done, p->iters_done,
+                                           it, s))))
+            return rc;
+    }
+    if (!early && p->iters_done) {
+        // every trial ran all iterations: fill with `iters` via a tiny host-free memset pattern
+        // (int32 fill is done on device by hipMemsetD32Async)
+        if (hipMemsetD32Async((hipDeviceptr_t)p->iters_done, iters, (size_t)pb.B, s) != hipSuccess)
+            return SBCE_EHIP;
+    }
+    return SBCE_OK;
+}
+
+int sbce_estep(const sbce_dims* d, const sbce_ptrs* p, int estep_mode, void* moments,
+               void* hip_stream) {
+    Problem pb;
+    if (!make_problem(d, pb)) return SBCE_EINVAL;
+    int rc = check_ptrs(p, pb, false);
+    if (rc) return rc;
+    if (!moments || !aligned16(moments)) return SBCE_EINVAL;
+    if (!estep_supported(pb, estep_mode)) return SBCE_EUNSUPPORTED;
+    if (pb.B == 0) return SBCE_OK;
+    EstepArgs ea;
+    ea.yd = (const cd*)p->y_d; ea.psid = (const cd*)p->psi_d; ea.theta = (const cd*)p->theta;
+    ea.cons = (const cd*)p->cons; ea.mom = (cd*)moments; ea.done = nullptr;
+    return hip_rc(launch_estep(pb, ea, estep_mode, (hipStream_t)hip_stream));
+}
+
+int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int solve_mode,
+               void* r_out, void* rhs_out, void* hip_stream) {
+    Problem pb;
+    if (!make_problem(d, pb)) return SBCE_EINVAL;
+    int rc = check_ptrs(p, pb, true);
+    if (rc) return rc;
+    if (!moments) return SBCE_EINVAL;
+    if (pb.B == 0) return SBCE_OK;
+    hipStream_t s = (hipStream_t)hip_stream;
+    const Carve c = carve(pb);
+    char* ws = (char*)p->workspace;
+    if (p->status && hipMemsetAsync(p->status, 0, (size_t)pb.B * sizeof(int32_t), s) != hipSuccess)
+        return SBCE_EHIP;
+    MstepArgs ma;
+    ma.yd = (const cd*)p->y_d; ma.yp = (const cd*)p->y_p; ma.psid = (const cd*)p->psi_d;
+    ma.up = (const cd*)p->u_p; ma.mom = (const cd*)moments; ma.R = (cd*)(ws + c.R);
+    ma.rhs = (cd*)(ws + c.rhs); ma.theta = (cd*)p->theta; ma.status = p->status; ma.done = nullptr;
+    ma.solve_mode = solve_mode;
+    if ((rc = hip_rc(launch_mstep_build(pb, ma, s)))) return rc;
+    if (r_out &&
+        hipMemcpyAsync(r_out, ma.R, (size_t)pb.B * pb.L * pb.L * sizeof(cd), hipMemcpyDeviceToDevice,
+                       s) != hipSuccess)
+        return SBCE_EHIP;
+    if (rhs_out &&
+        hipMemcpyAsync(rhs_out, ma.rhs, (size_t)pb.B * pb.L * pb.NR * sizeof(cd),
+                       hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return SBCE_EHIP;
+    return hip_rc(launch_chol_solve(pb, ma, s));
+}
+
+int sbce_nmse(const sbce_dims* d, const void* theta, const void* h_true, double* nmse_out,
+              void* hip_stream) {
+    Problem pb;
+    if (!make_problem(d, pb) || !theta || !h_true || !nmse_out) return SBCE_EINVAL;
+    if (pb.B == 0) return SBCE_OK;
+    return hip_rc(launch_nmse(pb, (const cd*)theta, (const cd*)h_true, nmse_out,
+                              (hipStream_t)hip_stream));
+}
+
+}  // extern "C"

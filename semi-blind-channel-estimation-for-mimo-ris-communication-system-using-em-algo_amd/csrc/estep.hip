@@ -1,0 +1,477 @@
+// E-step kernel: per-symbol posterior moments over all J = M^n_tx hypotheses.
+//
+// Reference: "Proposed method/Proposed_method_NMSEvsTp.py":61-71 (exact soft
+// posterior beta_{t,j} = exp(-||y_t - Z_{t,j} theta||^2/varn^2) / sum) and
+// "Proposed method/ML_detecctor.py":65-77 (hard "log-max": argmax beta).
+//
+// Reduced form (SURVEY.md §8 preamble): Z_{t,j} theta = H_eff(t) x_j with
+// H_eff(t) = sum_p psi_{p,t} H_c[:, p*n_tx:(p+1)*n_tx].  The streams are split
+// into A = {0..NA-1} and B = {NA..NT-1}; hypothesis j = i*JB + k (itertools.product
+// order, first stream slowest) with i indexing A and k indexing B.  Then
+//   r_{ik} = (y - H_A x_A(i)) - H_B x_B(k) = p_i - q_k,
+//   d_{ik} = ||p_i||^2 + ||q_k||^2 - 2 Re(p_i^H q_k)     (2*NR FMA + 1 add),
+// and the moments m_t = E[x], S_t = E[x x^H] follow from per-lane sums:
+//   lane k keeps  c_k = sum_i w_ik,  mu_k[a] = sum_i w_ik x_a(i)   (a in A),
+//   and shared    nu[a] = sum w |x_a|^2,  kap = sum w x_0 conj(x_1)  (A pair);
+//   B-side and A x B cross moments come from c_k x_b(k) and mu_k[a] conj(x_b(k)).
+//
+// Mapping (CDNA4, wave64): one SYMBOL lives in one segment of S lanes of ONE
+// wave (S = min(JB, 64)); every reduction is intra-wave (xor shuffles), waves
+// never synchronise.  Each lane holds KP values of k (q_k in registers) and
+// sweeps all i; p_i (pre-scaled by -2) and ||p_i||^2 are computed by the wave
+// into LDS, 64 entries at a time, and read back as broadcasts.
+//
+// Softmax numerics: weights are exp(-(d - m)/varn^2) with m a running,
+// segment-uniform minimum distance (log-sum-exp; the reference uses an
+// unbounded-exponent mpmath/gmpy2 exp instead).  A chunk of CH x KP hypotheses
+// per lane is skipped when every lane's distances exceed m + 50*varn^2: each
+// skipped weight is < e^-50 = 2e-22 of the segment maximum (total < 1e-17
+// relative for J <= 2^24), far below float64 resolution of the sums.
+#include "sbce_internal.h"
+
+namespace sbce {
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kCH = 4;              // i-values per inner chunk
+constexpr double kSkipThr = 50.0;   // skip weights below e^-50 of the running max
+
+struct EstepConst {
+    int B, Td, P, M, lm;       // lm = log2(M)
+    int S, SPW;                // lanes per symbol, symbols per wave
+    int JA, JB, npass, CI, CIp;
+    int nparts;                // H_eff partial-sum split per output
+    int heff_cd, ptab_cd;      // per-wave LDS carve (complex doubles)
+    double inv_s2, thr_d;
+};
+
+__device__ __forceinline__ double seg_min(double v, int S) {
+    for (int off = S >> 1; off >= 1; off >>= 1) v = fmin(v, shfl_xor_d(v, off));
+    return v;
+}
+__device__ __forceinline__ double seg_sum(double v, int S) {
+    for (int off = S >> 1; off >= 1; off >>= 1) v += shfl_xor_d(v, off);
+    return v;
+}
+__device__ __forceinline__ cd seg_sum(cd v, int S) {
+    return cmk(seg_sum(v.x, S), seg_sum(v.y, S));
+}
+
+template <int NT, int NR, int KP, int MODE>
+__global__ __launch_bounds__(256) void estep_kernel(EstepArgs a, EstepConst c) {
+    constexpr int NA = NT / 2;
+    constexpr int NB = NT - NA;
+    constexpr int NO = NT * NR;
+    constexpr int NPA = NA * (NA - 1) / 2;   // pairs inside A (0 or 1)
+    constexpr int NPB = NB * (NB - 1) / 2;   // pairs inside B (0 or 1)
+    constexpr int PST = NR + 1;              // ptab row stride (complex doubles)
+    static_assert(NA <= 2 && NB <= 2, "exact E-step supports n_tx <= 4");
+
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cd* s_cons = reinterpret_cast<cd*>(smem);
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    cd* s_heff = s_cons + 64 + wave * (c.heff_cd + c.ptab_cd);
+    cd* s_ptab = s_heff + c.heff_cd;
+
+    for (int i = threadIdx.x; i < c.M; i += blockDim.x) s_cons[i] = a.cons[i];
+    __syncthreads();
+
+    const long nsym = (long)c.B * c.Td;
+    const long wsym0 = ((long)blockIdx.x * kWavesPerBlock + wave) * c.SPW;
+    if (wsym0 >= nsym) return;                       // whole wave out of range
+    const int S = c.S;
+    const int seg = lane / S;
+    const int sl = lane & (S - 1);
+    long gsym = wsym0 + seg;
+    bool valid = gsym < nsym;
+    if (!valid) gsym = nsym - 1;                     // compute on a real symbol, skip write
+    const int b = (int)(gsym / c.Td);
+    const int t = (int)(gsym - (long)b * c.Td);
+    if (a.done && a.done[b]) valid = false;
+
+    // ---------------- effective channel H_eff(t): heff[a*NR + r] --------------
+    {
+        const cd* th = a.theta + (size_t)b * c.P * NO;      // [p][a][r]
+        const cd* ps = a.psid + (size_t)gsym * c.P;
+        const int ntask = NO * c.nparts;
+        cd* part = s_ptab + seg * ntask;
+        for (int task = sl; task < ntask; task += S) {
+            const int o = task % NO, pp = task / NO;
+            cd acc = czero();
+            for (int p = pp; p < c.P; p += c.nparts) acc = cfma(acc, ps[p], th[p * NO + o]);
+            part[task] = acc;
+        }
+        wave_sync();
+        for (int o = sl; o < NO; o += S) {
+            cd s = part[o];
+            for (int pp = 1; pp < c.nparts; ++pp) s = cadd(s, part[pp * NO + o]);
+            s_heff[seg * NO + o] = s;
+        }
+        wave_sync();
+    }
+    const cd* H = s_heff + seg * NO;
+    cd y[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) y[r] = a.yd[(size_t)gsym * NR + r];
+
+    const int mask = c.M - 1;
+    const double inv_s2 = c.inv_s2;
+
+    // per-lane state
+    double mshift = INFINITY;
+    double tot_c = 0.0;
+    cd tot_muA[NA > 0 ? NA : 1];
+    double nu[NA > 0 ? NA : 1];
+    cd kap = czero();
+    cd tot_mB[NB];
+    double tot_nB[NB];
+    cd tot_kB = czero();
+    cd tot_X[NA > 0 ? NA : 1][NB];
+#pragma unroll
+    for (int q = 0; q < (NA > 0 ? NA : 1); ++q) {
+        tot_muA[q] = czero(); nu[q] = 0.0;
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) tot_X[q][bb] = czero();
+    }
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) { tot_mB[bb] = czero(); tot_nB[bb] = 0.0; }
+    double best_d = INFINITY;
+    int best_j = 0x7fffffff;
+
+    for (int pass = 0; pass < c.npass; ++pass) {
+        // ---- this lane's KP hypotheses of B: q_k = H_B x_B(k) ----
+        cd q[KP][NR];
+        double gam[KP];
+        double ck[KP];
+        cd mu[KP][NA > 0 ? NA : 1];
+#pragma unroll
+        for (int cc = 0; cc < KP; ++cc) {
+            const int k = pass * S * KP + cc * S + sl;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) q[cc][r] = czero();
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb) {
+                const cd x = s_cons[(k >> (c.lm * (NB - 1 - bb))) & mask];
+#pragma unroll
+                for (int r = 0; r < NR; ++r) q[cc][r] = cfma(q[cc][r], H[(NA + bb) * NR + r], x);
+            }
+            double g = 0.0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) g += cabs2(q[cc][r]);
+            gam[cc] = g;
+            ck[cc] = 0.0;
+#pragma unroll
+            for (int q2 = 0; q2 < (NA > 0 ? NA : 1); ++q2) mu[cc][q2] = czero();
+        }
+
+        for (int i0 = 0; i0 < c.JA; i0 += c.CI) {
+            // ---- p_i = y - H_A x_A(i), stored as (-2 p_i, ||p_i||^2) ----
+            wave_sync();
+            cd* pt = s_ptab + seg * c.CIp * PST;
+            for (int e = sl; e < c.CIp; e += S) {
+                cd* row = pt + e * PST;
+                if (e < c.CI) {
+                    const int i = i0 + e;
+                    double al = 0.0;
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) {
+                        cd pr = y[r];
+#pragma unroll
+                        for (int q2 = 0; q2 < NA; ++q2) {
+                            const cd x = s_cons[(i >> (c.lm * (NA - 1 - q2))) & mask];
+                            const cd hx = cmul(H[q2 * NR + r], x);
+                            pr = csub(pr, hx);
+                        }
+                        al += cabs2(pr);
+                        row[r] = cscale(pr, -2.0);
+                    }
+                    row[NR] = cmk(al, 0.0);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) row[r] = czero();
+                    row[NR] = cmk(INFINITY, 0.0);
+                }
+            }
+            wave_sync();
+
+            for (int i1 = 0; i1 < c.CIp; i1 += kCH) {
+                double d[kCH][KP];
+#pragma unroll
+                for (int ii = 0; ii < kCH; ++ii) {
+                    const cd* row = pt + (i1 + ii) * PST;
+                    cd pm[NR];
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) pm[r] = row[r];
+                    const double al = row[NR].x;
+#pragma unroll
+                    for (int cc = 0; cc < KP; ++cc) {
+                        double acc = al + gam[cc];
+#pragma unroll
+                        for (int r = 0; r < NR; ++r) {
+                            acc = fma(pm[r].x, q[cc][r].x, acc);
+                            acc = fma(pm[r].y, q[cc][r].y, acc);
+                        }
+                        d[ii][cc] = acc;
+                    }
+                }
+                if (MODE == SBCE_ESTEP_HARD) {
+#pragma unroll
+                    for (int ii = 0; ii < kCH; ++ii) {
+                        const int i = i0 + i1 + ii;
+#pragma unroll
+                        for (int cc = 0; cc < KP; ++cc) {
+                            const int j = i * c.JB + pass * S * KP + cc * S + sl;
+                            const double dv = d[ii][cc];
+                            if (dv < best_d || (dv == best_d && j < best_j)) { best_d = dv; best_j = j; }
+                        }
+                    }
+                    continue;
+                }
+                double cm = d[0][0];
+#pragma unroll
+                for (int ii = 0; ii < kCH; ++ii)
+#pragma unroll
+                    for (int cc = 0; cc < KP; ++cc) cm = fmin(cm, d[ii][cc]);
+
+                if (__any(cm < mshift)) {
+                    const double mn = seg_min(fmin(cm, mshift), S);
+                    const double f = (mshift == INFINITY) ? 0.0 : fexp_neg((mn - mshift) * inv_s2);
+                    mshift = mn;
+                    tot_c *= f; tot_kB = cscale(tot_kB, f); kap = cscale(kap, f);
+#pragma unroll
+                    for (int q2 = 0; q2 < (NA > 0 ? NA : 1); ++q2) {
+                        tot_muA[q2] = cscale(tot_muA[q2], f); nu[q2] *= f;
+#pragma unroll
+                        for (int bb = 0; bb < NB; ++bb) tot_X[q2][bb] = cscale(tot_X[q2][bb], f);
+                    }
+#pragma unroll
+                    for (int bb = 0; bb < NB; ++bb) { tot_mB[bb] = cscale(tot_mB[bb], f); tot_nB[bb] *= f; }
+#pragma unroll
+                    for (int cc = 0; cc < KP; ++cc) {
+                        ck[cc] *= f;
+#pragma unroll
+                        for (int q2 = 0; q2 < (NA > 0 ? NA : 1); ++q2) mu[cc][q2] = cscale(mu[cc][q2], f);
+                    }
+                }
+                if (!__any(cm <= mshift + c.thr_d)) continue;   // whole chunk negligible
+
+#pragma unroll
+                for (int ii = 0; ii < kCH; ++ii) {
+                    const int i = i0 + i1 + ii;
+                    cd xa[NA > 0 ? NA : 1];
+                    double xa2[NA > 0 ? NA : 1];
+#pragma unroll
+                    for (int q2 = 0; q2 < NA; ++q2) {
+                        xa[q2] = s_cons[(i >> (c.lm * (NA - 1 - q2))) & mask];
+                        xa2[q2] = cabs2(xa[q2]);
+                    }
+                    cd x01 = czero();
+                    if (NPA) x01 = cmulc(xa[0], xa[NA > 1 ? 1 : 0]);
+#pragma unroll
+                    for (int cc = 0; cc < KP; ++cc) {
+                        const double w = fexp_neg((mshift - d[ii][cc]) * inv_s2);
+                        ck[cc] += w;
+#pragma unroll
+                        for (int q2 = 0; q2 < NA; ++q2) {
+                            mu[cc][q2] = caxpy(mu[cc][q2], w, xa[q2]);
+                            nu[q2] = fma(w, xa2[q2], nu[q2]);
+                        }
+                        if (NPA) kap = caxpy(kap, w, x01);
+                    }
+                }
+            }
+        }
+        if (MODE == SBCE_ESTEP_SOFT) {
+            // ---- fold this pass's per-k sums into the lane totals ----
+#pragma unroll
+            for (int cc = 0; cc < KP; ++cc) {
+                const int k = pass * S * KP + cc * S + sl;
+                cd xb[NB];
+#pragma unroll
+                for (int bb = 0; bb < NB; ++bb) xb[bb] = s_cons[(k >> (c.lm * (NB - 1 - bb))) & mask];
+                tot_c += ck[cc];
+#pragma unroll
+                for (int bb = 0; bb < NB; ++bb) {
+                    tot_mB[bb] = caxpy(tot_mB[bb], ck[cc], xb[bb]);
+                    tot_nB[bb] = fma(ck[cc], cabs2(xb[bb]), tot_nB[bb]);
+                }
+                if (NPB) tot_kB = caxpy(tot_kB, ck[cc], cmulc(xb[0], xb[NB > 1 ? 1 : 0]));
+#pragma unroll
+                for (int q2 = 0; q2 < NA; ++q2) {
+                    tot_muA[q2] = cadd(tot_muA[q2], mu[cc][q2]);
+#pragma unroll
+                    for (int bb = 0; bb < NB; ++bb) tot_X[q2][bb] = cfmac(tot_X[q2][bb], mu[cc][q2], xb[bb]);
+                }
+            }
+        }
+    }
+
+    constexpr int MS = NT + NT * NT;
+    cd* out = a.mom + (size_t)gsym * MS;
+    if (MODE == SBCE_ESTEP_HARD) {
+        for (int off = S >> 1; off >= 1; off >>= 1) {
+            const double od = shfl_xor_d(best_d, off);
+            const int oj = __shfl_xor(best_j, off);
+            if (od < best_d || (od == best_d && oj < best_j)) { best_d = od; best_j = oj; }
+        }
+        if (valid && sl == 0) {
+            cd x[NT];
+#pragma unroll
+            for (int s2 = 0; s2 < NT; ++s2) x[s2] = s_cons[(best_j >> (c.lm * (NT - 1 - s2))) & mask];
+#pragma unroll
+            for (int s2 = 0; s2 < NT; ++s2) {
+                out[s2] = x[s2];
+#pragma unroll
+                for (int s3 = 0; s3 < NT; ++s3) out[NT + s2 * NT + s3] = cmulc(x[s2], x[s3]);
+            }
+        }
+        return;
+    }
+
+    // ---- segment reductions (all lanes of a segment share mshift) ----
+    tot_c = seg_sum(tot_c, S);
+    kap = seg_sum(kap, S);
+    tot_kB = seg_sum(tot_kB, S);
+#pragma unroll
+    for (int q2 = 0; q2 < NA; ++q2) {
+        tot_muA[q2] = seg_sum(tot_muA[q2], S);
+        nu[q2] = seg_sum(nu[q2], S);
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) tot_X[q2][bb] = seg_sum(tot_X[q2][bb], S);
+    }
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) { tot_mB[bb] = seg_sum(tot_mB[bb], S); tot_nB[bb] = seg_sum(tot_nB[bb], S); }
+
+    if (valid && sl == 0) {
+        const double iz = 1.0 / tot_c;
+        cd m[NT];
+        cd Sm[NT][NT];
+#pragma unroll
+        for (int q2 = 0; q2 < NA; ++q2) {
+            m[q2] = cscale(tot_muA[q2], iz);
+            Sm[q2][q2] = cmk(nu[q2] * iz, 0.0);
+        }
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) {
+            m[NA + bb] = cscale(tot_mB[bb], iz);
+            Sm[NA + bb][NA + bb] = cmk(tot_nB[bb] * iz, 0.0);
+        }
+        if (NPA) { Sm[0][NA > 1 ? 1 : 0] = cscale(kap, iz); Sm[NA > 1 ? 1 : 0][0] = cconj(cscale(kap, iz)); }
+        if (NPB) {
+            Sm[NA][NT - 1] = cscale(tot_kB, iz);
+            Sm[NT - 1][NA] = cconj(cscale(tot_kB, iz));
+        }
+#pragma unroll
+        for (int q2 = 0; q2 < NA; ++q2)
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb) {
+                const cd v = cscale(tot_X[q2][bb], iz);
+                Sm[q2][NA + bb] = v;
+                Sm[NA + bb][q2] = cconj(v);
+            }
+#pragma unroll
+        for (int s2 = 0; s2 < NT; ++s2) {
+            out[s2] = m[s2];
+#pragma unroll
+            for (int s3 = 0; s3 < NT; ++s3) out[NT + s2 * NT + s3] = Sm[s2][s3];
+        }
+    }
+}
+
+struct Geometry {
+    EstepConst c;
+    int KP;
+    size_t lds;
+    long blocks;
+};
+
+bool make_geometry(const Problem& pb, Geometry& g) {
+    if (pb.NT < 1 || pb.NT > 4 || pb.NR < 1 || pb.NR > 8) return false;
+    if (pb.M < 2 || pb.M > 64 || (pb.M & (pb.M - 1))) return false;
+    int lm = 0;
+    while ((1 << lm) < pb.M) ++lm;
+    const int NA = pb.NT / 2, NB = pb.NT - NA;
+    const long JA = 1L << (lm * NA), JB = 1L << (lm * NB);
+    if (JA * JB > (1L << 24)) return false;
+    EstepConst& c = g.c;
+    c.B = pb.B; c.Td = pb.Td; c.P = pb.P; c.M = pb.M; c.lm = lm;
+    c.JA = (int)JA; c.JB = (int)JB;
+    if (JB >= 256) { g.KP = 4; c.S = 64; }
+    else { g.KP = 1; c.S = (int)(JB < 64 ? JB : 64); }
+    c.SPW = 64 / c.S;
+    c.npass = (int)(JB / ((long)c.S * g.KP));
+    c.CI = (int)(JA < c.S ? JA : c.S);
+    c.CIp = (c.CI + kCH - 1) / kCH * kCH;
+    const int NO = pb.NT * pb.NR;
+    c.nparts = c.S >= NO ? c.S / NO : 1;
+    c.heff_cd = c.SPW * NO;
+    const int ptab = c.SPW * c.CIp * (pb.NR + 1);
+    const int part = c.SPW * NO * c.nparts;
+    c.ptab_cd = ptab > part ? ptab : part;
+    c.inv_s2 = 1.0 / (pb.varn * pb.varn);
+    c.thr_d = kSkipThr * pb.varn * pb.varn;
+    g.lds = (size_t)(64 + kWavesPerBlock * (c.heff_cd + c.ptab_cd)) * sizeof(cd);
+    const long nsym = (long)pb.B * pb.Td;
+    const long waves = (nsym + c.SPW - 1) / c.SPW;
+    g.blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    return g.lds <= 160 * 1024;
+}
+
+template <int NT, int NR, int KP>
+hipError_t dispatch_mode(const Geometry& g, const EstepArgs& a, int mode, hipStream_t s) {
+    if (mode == SBCE_ESTEP_HARD)
+        hipLaunchKernelGGL((estep_kernel<NT, NR, KP, SBCE_ESTEP_HARD>), dim3((unsigned)g.blocks),
+                           dim3(256), g.lds, s, a, g.c);
+    else
+        hipLaunchKernelGGL((estep_kernel<NT, NR, KP, SBCE_ESTEP_SOFT>), dim3((unsigned)g.blocks),
+                           dim3(256), g.lds, s, a, g.c);
+    return hipGetLastError();
+}
+
+template <int NT, int NR>
+hipError_t dispatch_kp(const Geometry& g, const EstepArgs& a, int mode, hipStream_t s) {
+    if constexpr (NT >= 3) {
+        if (g.KP == 4) return dispatch_mode<NT, NR, 4>(g, a, mode, s);
+    }
+    return dispatch_mode<NT, NR, 1>(g, a, mode, s);
+}
+
+template <int NT>
+hipError_t dispatch_nr(int NR, const Geometry& g, const EstepArgs& a, int mode, hipStream_t s) {
+    switch (NR) {
+        case 1: return dispatch_kp<NT, 1>(g, a, mode, s);
+        case 2: return dispatch_kp<NT, 2>(g, a, mode, s);
+        case 3: return dispatch_kp<NT, 3>(g, a, mode, s);
+        case 4: return dispatch_kp<NT, 4>(g, a, mode, s);
+        case 5: return dispatch_kp<NT, 5>(g, a, mode, s);
+        case 6: return dispatch_kp<NT, 6>(g, a, mode, s);
+        case 7: return dispatch_kp<NT, 7>(g, a, mode, s);
+        case 8: return dispatch_kp<NT, 8>(g, a, mode, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+bool estep_supported(const Problem& pb, int mode) {
+    Geometry g;
+    return (mode == SBCE_ESTEP_SOFT || mode == SBCE_ESTEP_HARD) && make_geometry(pb, g);
+}
+
+hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStream_t s) {
+    Geometry g;
+    if (!make_geometry(pb, g)) return hipErrorInvalidValue;
+    if (g.blocks == 0) return hipSuccess;
+    switch (pb.NT) {
+        case 1: return dispatch_nr<1>(pb.NR, g, a, mode, s);
+        case 2: return dispatch_nr<2>(pb.NR, g, a, mode, s);
+        case 3: return dispatch_nr<3>(pb.NR, g, a, mode, s);
+        case 4: return dispatch_nr<4>(pb.NR, g, a, mode, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace sbce

@@ -1,0 +1,368 @@
+// M-step kernels: reduced normal equations + batched Hermitian solve.
+//
+// Reference: "Proposed method/Proposed_method_NMSEvsTp.py":70-80 accumulates the
+// K x K system  sum beta Z^H Z,  sum beta Z^H y  (K = (N+1) n_tx n_rx) and calls
+// np.linalg.solve (LAPACK zgesv).  With Z = u^T (x) I_{n_rx} the commutation
+// identity ("Proposed method/commutation_matrix.py":3-8) gives
+// Z^H Z = conj(u u^H) (x) I, so the system is block-diagonal in the receive
+// antenna: H_c R = B with the L x L Hermitian
+//   R = sum_p u_p u_p^H + sum_t (psi_t psi_t^H) (x) S_t
+// and B^H = sum_p u_p y_p^H + sum_t (psi_t (x) m_t) y_t^H  (L x n_rx).
+// The pilot terms are rebuilt every iteration by the reference (:72-74); here
+// they are summed in the same pass as the data terms (never stored).
+#include "sbce_internal.h"
+
+namespace sbce {
+
+namespace {
+
+// ------------------------------------------------------------------ R build
+// One thread per block pair (p >= q) of one trial; the NT x NT block of R at
+// rows p*NT.., cols q*NT.. and its Hermitian mirror.  S_t is wave-uniform.
+template <int NT>
+__global__ __launch_bounds__(256) void rbuild_kernel(MstepArgs a, int B, int P, int Tp, int Td,
+                                                     int L) {
+    const int b = blockIdx.y;
+    if (a.done && a.done[b]) return;
+    const int npairs = P * (P + 1) / 2;
+    const int pi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pi >= npairs) return;
+    int p = (int)((sqrt(8.0 * pi + 1.0) - 1.0) * 0.5);
+    while ((p + 1) * (p + 2) / 2 <= pi) ++p;
+    while (p * (p + 1) / 2 > pi) --p;
+    const int q = pi - p * (p + 1) / 2;
+    constexpr int MS = NT + NT * NT;
+
+    cd acc[NT][NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = czero();
+
+    const cd* up = a.up + (size_t)b * Tp * L;
+    for (int tp = 0; tp < Tp; ++tp) {
+        cd ua[NT], ub[NT];
+#pragma unroll
+        for (int i = 0; i < NT; ++i) { ua[i] = up[tp * L + p * NT + i]; ub[i] = up[tp * L + q * NT + i]; }
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = cfmac(acc[i][j], ua[i], ub[j]);
+    }
+    const cd* ps = a.psid + (size_t)b * Td * P;
+    const cd* mom = a.mom + (size_t)b * Td * MS;
+    for (int t = 0; t < Td; ++t) {
+        const cd w = cmulc(ps[t * P + p], ps[t * P + q]);
+        const cd* St = mom + t * MS + NT;
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = cfma(acc[i][j], w, St[i * NT + j]);
+    }
+    cd* R = a.R + (size_t)b * L * L;
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            R[(size_t)(p * NT + i) * L + q * NT + j] = acc[i][j];
+            if (p != q) R[(size_t)(q * NT + j) * L + p * NT + i] = cconj(acc[i][j]);
+        }
+}
+
+// ------------------------------------------------------------------ B^H build
+// One thread per row l = p*NT + a of one trial (L x NR right-hand sides).
+template <int NR>
+__global__ __launch_bounds__(256) void rhs_kernel(MstepArgs a, int B, int P, int NT, int Tp,
+                                                  int Td, int L) {
+    const int b = blockIdx.y;
+    if (a.done && a.done[b]) return;
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= L) return;
+    const int p = l / NT, ai = l - p * NT;
+    const int MS = NT + NT * NT;
+    cd acc[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc[r] = czero();
+    const cd* up = a.up + (size_t)b * Tp * L;
+    const cd* yp = a.yp + (size_t)b * Tp * NR;
+    for (int tp = 0; tp < Tp; ++tp) {
+        const cd u = up[tp * L + l];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) acc[r] = cfmac(acc[r], u, yp[tp * NR + r]);
+    }
+    const cd* ps = a.psid + (size_t)b * Td * P;
+    const cd* mom = a.mom + (size_t)b * Td * MS;
+    const cd* yd = a.yd + (size_t)b * Td * NR;
+    for (int t = 0; t < Td; ++t) {
+        const cd w = cmul(ps[t * P + p], mom[t * MS + ai]);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) acc[r] = cfmac(acc[r], w, yd[t * NR + r]);
+    }
+    cd* rhs = a.rhs + ((size_t)b * L + l) * NR;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) rhs[r] = acc[r];
+}
+
+// ------------------------------------------------------------------ Cholesky + solve
+// One 256-thread workgroup per trial.  Left-looking blocked Cholesky R = L L^H
+// (lower, in place in R), block columns of NBC; the active panel (rows jb..L-1)
+// lives in LDS, the already factored columns are read from global memory (L2).
+// Then L y = B^H, L^H x = y with x in LDS, theta = conj(x) in reference order.
+constexpr int NBC = 16;
+
+__global__ __launch_bounds__(256) void chol_solve_kernel(MstepArgs a, int L, int NR) {
+    const int b = blockIdx.x;
+    if (a.done && a.done[b]) return;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cd* panel = reinterpret_cast<cd*>(smem);                 // [L][NBC]
+    cd* x = panel + (size_t)L * NBC;                         // [L][NR]
+    double& s_tol = *reinterpret_cast<double*>(x + (size_t)L * NR);
+    int& s_flag = *reinterpret_cast<int*>(x + (size_t)L * NR + 1);
+    cd* R = a.R + (size_t)b * L * L;
+    const int tid = threadIdx.x;
+    const int nth = blockDim.x;
+
+    if (tid == 0) {
+        double mx = 0.0;
+        for (int i = 0; i < L; ++i) mx = fmax(mx, R[(size_t)i * L + i].x);
+        s_tol = mx * 1e-14;
+        s_flag = 0;
+    }
+    __syncthreads();
+    const double tol = s_tol;
+
+    for (int jb = 0; jb < L; jb += NBC) {
+        const int w = (L - jb) < NBC ? (L - jb) : NBC;
+        const int rows = L - jb;
+        // 1. load panel (lower part of columns jb..jb+w-1, rows jb..L-1)
+        for (int e = tid; e < rows * NBC; e += nth) {
+            const int i = e / NBC, cc = e - i * NBC;
+            panel[e] = (cc < w) ? R[(size_t)(jb + i) * L + jb + cc] : czero();
+        }
+        __syncthreads();
+        // 2. panel -= L[jb+i, 0:jb] * L[jb+c, 0:jb]^H   (left-looking update)
+        if (jb > 0) {
+            for (int i = tid; i < rows; i += nth) {
+                cd acc[NBC];
+#pragma unroll
+                for (int cc = 0; cc < NBC; ++cc) acc[cc] = czero();
+                const cd* Li = R + (size_t)(jb + i) * L;
+                for (int k = 0; k < jb; ++k) {
+                    const cd lik = Li[k];
+#pragma unroll
+                    for (int cc = 0; cc < NBC; ++cc) {
+                        if (cc < w && cc <= i) acc[cc] = cfmac(acc[cc], lik, R[(size_t)(jb + cc) * L + k]);
+                    }
+                }
+#pragma unroll
+                for (int cc = 0; cc < NBC; ++cc) panel[i * NBC + cc] = csub(panel[i * NBC + cc], acc[cc]);
+            }
+            __syncthreads();
+        }
+        // 3. factor the panel column by column (right-looking inside the panel)
+        for (int cc = 0; cc < w; ++cc) {
+            const double dia = panel[cc * NBC + cc].x;
+            double piv;
+            bool drop = false;
+            if (!(dia > tol)) {
+                if (tid == 0) s_flag = 1;
+                if (a.solve_mode == SBCE_SOLVE_CHOL_DROP) drop = true;
+                piv = sqrt(fmax(dia, tol));
+            } else {
+                piv = sqrt(dia);
+            }
+            const double inv = drop ? 0.0 : 1.0 / piv;
+            for (int i = cc + 1 + tid; i < rows; i += nth) panel[i * NBC + cc] = cscale(panel[i * NBC + cc], inv);
+            __syncthreads();
+            if (tid == 0) panel[cc * NBC + cc] = cmk(drop ? 0.0 : piv, 0.0);
+            const int ncol = w - cc - 1;
+            if (ncol > 0) {
+                for (int e = tid; e < rows * ncol; e += nth) {
+                    const int i = e / ncol, c2 = cc + 1 + (e - i * ncol);
+                    if (i >= c2) panel[i * NBC + c2] = csub(panel[i * NBC + c2],
+                                                            cmulc(panel[i * NBC + cc], panel[c2 * NBC + cc]));
+                }
+            }
+            __syncthreads();
+        }
+        // 4. write the factored panel back (lower part)
+        for (int e = tid; e < rows * NBC; e += nth) {
+            const int i = e / NBC, cc = e - i * NBC;
+            if (cc < w && i >= cc) R[(size_t)(jb + i) * L + jb + cc] = panel[e];
+        }
+        __syncthreads();
+    }
+
+    // ---- forward: L y = rhs ----
+    const cd* rhs = a.rhs + (size_t)b * L * NR;
+    for (int e = tid; e < L * NR; e += nth) x[e] = rhs[e];
+    __syncthreads();
+    for (int k = 0; k < L; ++k) {
+        const double lkk = R[(size_t)k * L + k].x;
+        if (tid < NR) x[k * NR + tid] = (lkk > 0.0) ? cscale(x[k * NR + tid], 1.0 / lkk) : czero();
+        __syncthreads();
+        for (int e = tid; e < (L - k - 1) * NR; e += nth) {
+            const int i = k + 1 + e / NR, r = e % NR;
+            x[i * NR + r] = csub(x[i * NR + r], cmul(R[(size_t)i * L + k], x[k * NR + r]));
+        }
+        __syncthreads();
+    }
+    // ---- backward: L^H x = y ----
+    for (int i = L - 1; i >= 0; --i) {
+        const double lii = R[(size_t)i * L + i].x;
+        if (tid < NR) x[i * NR + tid] = (lii > 0.0) ? cscale(x[i * NR + tid], 1.0 / lii) : czero();
+        __syncthreads();
+        for (int e = tid; e < i * NR; e += nth) {
+            const int k = e / NR, r = e % NR;
+            x[k * NR + r] = csub(x[k * NR + r], cmulc(x[i * NR + r], R[(size_t)i * L + k]));
+        }
+        __syncthreads();
+    }
+    cd* th = a.theta + (size_t)b * L * NR;
+    for (int e = tid; e < L * NR; e += nth) th[e] = cconj(x[e]);
+    if (tid == 0 && a.status) a.status[b] |= s_flag ? SBCE_STATUS_NONHPD : 0;
+}
+
+// ------------------------------------------------------------------ small per-trial kernels
+__device__ double block_sum(double v, double* sh) {
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane == 0) sh[wave] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += sh[w];
+    return s;
+}
+
+__global__ __launch_bounds__(256) void nmse_kernel(const cd* theta, const cd* h, double* out, int K) {
+    __shared__ double sh[4];
+    const int b = blockIdx.x;
+    double num = 0.0, den = 0.0;
+    for (int e = threadIdx.x; e < K; e += blockDim.x) {
+        const cd hv = h[(size_t)b * K + e];
+        num += cabs2(csub(theta[(size_t)b * K + e], hv));
+        den += cabs2(hv);
+    }
+    num = block_sum(num, sh);
+    den = block_sum(den, sh);
+    if (threadIdx.x == 0) out[b] = num / den;
+}
+
+// LLF of "Proposed method/IterationsvsLLF.py":49-50,76:
+//   -T_d n_tx ln M - (T_d+T_p) ln(pi varn^2) - (||Y_p - Z_p th|| + ||Y_d - Z_d th||)/varn^2
+// with Z_d built from the TRUE symbols (genie) and UNsquared norms.
+__global__ __launch_bounds__(256) void llf_kernel(const cd* theta, const cd* yp, const cd* up,
+                                                  const cd* yd, const cd* psid, const cd* xd,
+                                                  double* llf, const int32_t* done, int P, int NT,
+                                                  int NR, int Tp, int Td, int M, double varn,
+                                                  int iters, int it) {
+    __shared__ double sh[4];
+    const int b = blockIdx.x;
+    if (done && done[b]) return;
+    const int L = P * NT;
+    const cd* th = theta + (size_t)b * L * NR;
+    double sp = 0.0, sd = 0.0;
+    for (int e = threadIdx.x; e < Tp * NR; e += blockDim.x) {
+        const int tp = e / NR, r = e % NR;
+        cd acc = yp[((size_t)b * Tp + tp) * NR + r];
+        const cd* u = up + ((size_t)b * Tp + tp) * L;
+        for (int l = 0; l < L; ++l) acc = csub(acc, cmul(th[l * NR + r], u[l]));
+        sp += cabs2(acc);
+    }
+    for (int e = threadIdx.x; e < Td * NR; e += blockDim.x) {
+        const int t = e / NR, r = e % NR;
+        cd acc = yd[((size_t)b * Td + t) * NR + r];
+        const cd* ps = psid + ((size_t)b * Td + t) * P;
+        const cd* x = xd + ((size_t)b * Td + t) * NT;
+        for (int p = 0; p < P; ++p) {
+            cd hx = czero();
+            for (int ai = 0; ai < NT; ++ai) hx = cfma(hx, th[(p * NT + ai) * NR + r], x[ai]);
+            acc = csub(acc, cmul(ps[p], hx));
+        }
+        sd += cabs2(acc);
+    }
+    sp = block_sum(sp, sh);
+    sd = block_sum(sd, sh);
+    if (threadIdx.x == 0) {
+        const double v2 = varn * varn;
+        llf[(size_t)b * iters + it] = -(double)Td * NT * log((double)M) -
+                                      (double)(Td + Tp) * log(M_PI * v2) - sqrt(sp) / v2 -
+                                      sqrt(sd) / v2;
+    }
+}
+
+// Oracle early stop of "Proposed method/PM.py":110-112:
+//   if |‖theta‖ - ‖h‖| < 1 and l != 0: break
+__global__ __launch_bounds__(256) void early_stop_kernel(const cd* theta, const cd* h, int32_t* done,
+                                                         int32_t* iters_done, int K, int it) {
+    __shared__ double sh[4];
+    const int b = blockIdx.x;
+    if (done[b]) return;
+    double nt = 0.0, nh = 0.0;
+    for (int e = threadIdx.x; e < K; e += blockDim.x) {
+        nt += cabs2(theta[(size_t)b * K + e]);
+        nh += cabs2(h[(size_t)b * K + e]);
+    }
+    nt = block_sum(nt, sh);
+    nh = block_sum(nh, sh);
+    if (threadIdx.x == 0) {
+        if (iters_done) iters_done[b] = it + 1;
+        if (it != 0 && fabs(sqrt(nt) - sqrt(nh)) < 1.0) done[b] = 1;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t s) {
+    const int npairs = pb.P * (pb.P + 1) / 2;
+    dim3 g1((npairs + 255) / 256, pb.B);
+    switch (pb.NT) {
+        case 1: hipLaunchKernelGGL(rbuild_kernel<1>, g1, dim3(256), 0, s, a, pb.B, pb.P, pb.Tp, pb.Td, pb.L); break;
+        case 2: hipLaunchKernelGGL(rbuild_kernel<2>, g1, dim3(256), 0, s, a, pb.B, pb.P, pb.Tp, pb.Td, pb.L); break;
+        case 3: hipLaunchKernelGGL(rbuild_kernel<3>, g1, dim3(256), 0, s, a, pb.B, pb.P, pb.Tp, pb.Td, pb.L); break;
+        case 4: hipLaunchKernelGGL(rbuild_kernel<4>, g1, dim3(256), 0, s, a, pb.B, pb.P, pb.Tp, pb.Td, pb.L); break;
+        default: return hipErrorInvalidValue;
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    dim3 g2((pb.L + 255) / 256, pb.B);
+    switch (pb.NR) {
+#define SBCE_RHS(n) case n: hipLaunchKernelGGL(rhs_kernel<n>, g2, dim3(256), 0, s, a, pb.B, pb.P, pb.NT, pb.Tp, pb.Td, pb.L); break;
+        SBCE_RHS(1) SBCE_RHS(2) SBCE_RHS(3) SBCE_RHS(4) SBCE_RHS(5) SBCE_RHS(6) SBCE_RHS(7) SBCE_RHS(8)
+#undef SBCE_RHS
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+size_t chol_lds_bytes(int L, int NR) { return ((size_t)L * NBC + (size_t)L * NR + 2) * sizeof(cd); }
+
+hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s) {
+    const size_t lds = chol_lds_bytes(pb.L, pb.NR);
+    if (lds > 150 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(chol_solve_kernel, dim3(pb.B), dim3(256), lds, s, a, pb.L, pb.NR);
+    return hipGetLastError();
+}
+
+hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(nmse_kernel, dim3(pb.B), dim3(256), 0, s, theta, h, out, pb.K);
+    return hipGetLastError();
+}
+
+hipError_t launch_llf(const Problem& pb, const cd* theta, const cd* yp, const cd* up, const cd* yd,
+                      const cd* psid, const cd* xd, double* llf, int iters, int it,
+                      const int32_t* done, hipStream_t s) {
+    hipLaunchKernelGGL(llf_kernel, dim3(pb.B), dim3(256), 0, s, theta, yp, up, yd, psid, xd, llf, done,
+                       pb.P, pb.NT, pb.NR, pb.Tp, pb.Td, pb.M, pb.varn, iters, it);
+    return hipGetLastError();
+}
+
+hipError_t launch_early_stop(const Problem& pb, const cd* theta, const cd* h, int32_t* done,
+                             int32_t* iters_done, int it, hipStream_t s) {
+    hipLaunchKernelGGL(early_stop_kernel, dim3(pb.B), dim3(256), 0, s, theta, h, done, iters_done,
+                       pb.K, it);
+    return hipGetLastError();
+}
+
+}  // namespace sbce

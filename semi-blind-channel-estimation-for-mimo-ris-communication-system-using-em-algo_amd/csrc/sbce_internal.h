@@ -1,0 +1,121 @@
+// Internal device helpers and launch declarations for libsbce (gfx950 / CDNA4).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "../../include/sbce.h"
+
+namespace sbce {
+
+// complex double, interleaved (numpy complex128 memory)
+typedef double2 cd;
+
+__device__ __forceinline__ cd cmk(double r, double i) { cd z; z.x = r; z.y = i; return z; }
+__device__ __forceinline__ cd czero() { return cmk(0.0, 0.0); }
+__device__ __forceinline__ cd cadd(cd a, cd b) { return cmk(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ cd csub(cd a, cd b) { return cmk(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ cd cconj(cd a) { return cmk(a.x, -a.y); }
+__device__ __forceinline__ cd cscale(cd a, double s) { return cmk(a.x * s, a.y * s); }
+__device__ __forceinline__ cd cmul(cd a, cd b) {
+    return cmk(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
+}
+// a * conj(b)
+__device__ __forceinline__ cd cmulc(cd a, cd b) {
+    return cmk(fma(a.x, b.x, a.y * b.y), fma(a.y, b.x, -a.x * b.y));
+}
+// acc + a*b
+__device__ __forceinline__ cd cfma(cd acc, cd a, cd b) {
+    acc.x = fma(a.x, b.x, acc.x); acc.x = fma(-a.y, b.y, acc.x);
+    acc.y = fma(a.x, b.y, acc.y); acc.y = fma(a.y, b.x, acc.y);
+    return acc;
+}
+// acc + a*conj(b)
+__device__ __forceinline__ cd cfmac(cd acc, cd a, cd b) {
+    acc.x = fma(a.x, b.x, acc.x); acc.x = fma(a.y, b.y, acc.x);
+    acc.y = fma(a.y, b.x, acc.y); acc.y = fma(-a.x, b.y, acc.y);
+    return acc;
+}
+// acc + s*a  (s real)
+__device__ __forceinline__ cd caxpy(cd acc, double s, cd a) {
+    acc.x = fma(s, a.x, acc.x); acc.y = fma(s, a.y, acc.y); return acc;
+}
+__device__ __forceinline__ double cabs2(cd a) { return fma(a.x, a.x, a.y * a.y); }
+
+// exp(z) for z <= ~0 (z may be -inf).  Cody-Waite reduction z = k ln2 + r,
+// |r| <= ln2/2, degree-12 Taylor polynomial in Horner form (truncation
+// r^13/13! < 1.7e-16 relative), then 2^k by v_ldexp_f64 (exact; underflows to
+// 0 below 2^-1074).  18 f64 VALU ops, no special-case branches: the E-step
+// only ever evaluates non-positive log-weights.
+__device__ __forceinline__ double fexp_neg(double z) {
+    z = fmax(z, -745.5);
+    const double kd = __builtin_rint(z * 1.4426950408889634074);
+    double r = fma(-kd, 6.93147180559945286227e-01, z);
+    r = fma(-kd, 2.31904681384629955842e-17, r);
+    double p = 2.08767569878680989792e-09;          // 1/12!
+    p = fma(p, r, 2.50521083854417187751e-08);      // 1/11!
+    p = fma(p, r, 2.75573192239858906526e-07);      // 1/10!
+    p = fma(p, r, 2.75573192239858906526e-06);      // 1/9!
+    p = fma(p, r, 2.48015873015873015873e-05);      // 1/8!
+    p = fma(p, r, 1.98412698412698412698e-04);      // 1/7!
+    p = fma(p, r, 1.38888888888888888889e-03);      // 1/6!
+    p = fma(p, r, 8.33333333333333333333e-03);      // 1/5!
+    p = fma(p, r, 4.16666666666666666667e-02);      // 1/4!
+    p = fma(p, r, 1.66666666666666666667e-01);      // 1/3!
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return __builtin_amdgcn_ldexp(p, (int)kd);
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ double shfl_xor_d(double v, int m) { return __shfl_xor(v, m); }
+
+// ------------------------------------------------------------------ launch API
+struct Problem {
+    int B, NT, NR, P, Tp, Td, M, L, K;
+    double varn;
+};
+
+struct EstepArgs {
+    const cd* yd;      // [B][Td][NR]
+    const cd* psid;    // [B][Td][P]
+    const cd* theta;   // [B][K]
+    const cd* cons;    // [M]
+    cd* mom;           // [B][Td][NT + NT*NT]
+    const int32_t* done;  // [B] or null
+};
+
+struct MstepArgs {
+    const cd* yd;
+    const cd* yp;      // [B][Tp][NR]
+    const cd* psid;
+    const cd* up;      // [B][Tp][L]
+    const cd* mom;
+    cd* R;             // [B][L][L]
+    cd* rhs;           // [B][L][NR]
+    cd* theta;         // [B][K]
+    int32_t* status;   // [B] or null
+    const int32_t* done;
+    int solve_mode;
+};
+
+hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStream_t s);
+bool estep_supported(const Problem& pb, int mode);
+hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t s);
+hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s);
+hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* out,
+                       hipStream_t s);
+hipError_t launch_llf(const Problem& pb, const cd* theta, const cd* yp, const cd* up,
+                      const cd* yd, const cd* psid, const cd* xd, double* llf, int iters,
+                      int it, const int32_t* done, hipStream_t s);
+hipError_t launch_early_stop(const Problem& pb, const cd* theta, const cd* h,
+                             int32_t* done, int32_t* iters_done, int it, hipStream_t s);
+
+}  // namespace sbce

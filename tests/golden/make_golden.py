@@ -1,0 +1,270 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE's own
+estimator functions in this (CPU) container.
+
+This script is test infrastructure. It reads /root/reference (read-only) as the
+oracle of record and is never run on the GPU box; only the .npz files it writes
+travel. Nothing here is imported by the product package.
+
+How the reference is loaded:
+  * every reference script runs a Monte-Carlo sweep and ``plt.show()`` at module
+    top level, so only its ``import`` and ``def`` statements are executed
+    (``ast`` filter), into a namespace pre-seeded with the module globals the
+    functions read (``N``, ``n_tx``, ``beta_min``/``beta_max``, ``qamCons``,
+    ``Z_d``, ``h``);
+  * ``gmpy2`` is not installed: ``gmpy2.exp`` is bound to ``mpmath.exp`` (both
+    return a 53-bit-mantissa number with unbounded exponent);
+  * ``Proposed method/QAM.py`` uses the NumPy aliases removed in NumPy 2
+    (``np.int``/``np.float``/``np.complex``): they are restored as the builtins.
+  * ``sys.dont_write_bytecode`` keeps ``__pycache__`` out of the reference tree.
+
+Synthetic data for every case is produced by the reference's own helpers
+(``channelMatrix``, ``symbols``, ``pilotSymbols``, ``irsMatrix``,
+``receivedSignals``) in the reference's own RNG call order after
+``np.random.seed(seed)``, so the fixtures also pin the build's signal-model
+replay (``signal_model.py``).
+
+Usage:  python tests/golden/make_golden.py [case ...]     (default: all cases)
+"""
+import ast
+import contextlib
+import io
+import os
+import sys
+import time
+from multiprocessing import Pool
+
+sys.dont_write_bytecode = True
+os.environ.setdefault("MPLBACKEND", "Agg")
+
+import numpy as np  # noqa: E402
+
+REF = "/root/reference"
+PMD = os.path.join(REF, "Proposed method")
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _shim_env():
+    import mpmath
+    for name, typ in (("int", int), ("float", float), ("complex", complex)):
+        if not hasattr(np, name):
+            setattr(np, name, typ)
+    sys.modules.setdefault("gmpy2", mpmath)
+    if PMD not in sys.path:
+        sys.path.insert(0, PMD)
+
+
+def load_defs(path, **globs):
+    """Execute only the import/def statements of a reference script."""
+    _shim_env()
+    src = open(path).read()
+    tree = ast.parse(src, filename=path)
+    keep = [n for n in tree.body
+            if isinstance(n, (ast.Import, ast.ImportFrom, ast.FunctionDef))]
+    mod = ast.Module(body=keep, type_ignores=[])
+    ns = {"__name__": "refdefs", "np": np}
+    ns.update(globs)
+    with contextlib.redirect_stdout(io.StringIO()):
+        exec(compile(mod, path, "exec"), ns)
+    return ns
+
+
+def nmse(theta, h):
+    theta = np.asarray(theta).reshape(-1)
+    return float(np.sum(np.abs(theta - h) ** 2) / np.sum(np.abs(h) ** 2))
+
+
+def quiet(fn, *a):
+    with contextlib.redirect_stdout(io.StringIO()):
+        return fn(*a)
+
+
+def _gen_northstar(ns, seed, N, n_tx, n_rx, T_d, T_p, M, varn):
+    """PMd/Proposed_method_NMSEvsTp.py call order (:155-163)."""
+    np.random.seed(seed)
+    h = quiet(ns["channelMatrix"], n_tx, n_rx, N, 1)
+    X_d, aps = ns["symbols"](n_tx, M, T_d)[:2]
+    X_p = ns["pilotSymbols"](n_tx, M, T_p)
+    Ptp, Ptd = ns["irsMatrix"](T_p, T_d, N, 0, 1)
+    Ptd = np.insert(Ptd, 0, np.ones((1, T_d), dtype="complex128"), axis=0)
+    Y_p, Y_d, Z_p, Z_d, h0 = ns["receivedSignals"](T_p, T_d, Ptp, Ptd, n_rx, n_tx,
+                                                   X_d, X_p, h, varn, M)
+    return dict(h=h, X_d=X_d, aps=aps, X_p=X_p, Ptp=Ptp, Ptd=Ptd, Y_p=Y_p, Y_d=Y_d,
+                Z_p=Z_p, Z_d=Z_d, h0=h0)
+
+
+def _pack(d, **extra):
+    """Store the inputs in array form (lists of per-symbol arrays are stacked)."""
+    out = dict(
+        h=np.asarray(d["h"]),
+        X_d=np.stack(d["X_d"])[..., 0],
+        X_p=np.stack(d["X_p"])[..., 0],
+        aps=np.asarray(d["aps"]),
+        Ptp=np.asarray(d["Ptp"]),
+        Ptd=np.asarray(d["Ptd"]),
+        Y_p=np.stack(d["Y_p"])[..., 0],
+        Y_d=np.stack(d["Y_d"])[..., 0],
+        Z_p=np.stack(d["Z_p"]),
+        h0=np.asarray(d["h0"]).reshape(-1),
+    )
+    out.update(extra)
+    return out
+
+
+def _cons(M):
+    _shim_env()
+    import QAM as qp  # reference's vendored komm QAM, Proposed method/QAM.py:246-336
+    return np.asarray(qp.QAModulation(M).constellation)
+
+
+# ----------------------------------------------------------------------------- cases
+
+def case_kat1(seed):
+    """KAT-1: PMd/Proposed_method_NMSEvsTp.py helpers + em (:50-83)."""
+    N, n_tx, n_rx, T_d, T_p, M, varn = 8, 2, 2, 40, 12, 4, 0.1
+    ns = load_defs(os.path.join(PMD, "Proposed_method_NMSEvsTp.py"),
+                   N=N, n_tx=n_tx, n_rx=n_rx, beta_min=0.0, beta_max=2 * np.pi)
+    d = _gen_northstar(ns, seed, N, n_tx, n_rx, T_d, T_p, M, varn)
+    res = {}
+    for it in (1, 2):
+        th = quiet(ns["em"], d["Y_d"], d["Y_p"], T_d, T_p, d["Z_p"], d["Ptd"], d["aps"],
+                   M, varn, it, d["h0"])
+        res[f"theta_it{it}"] = np.asarray(th).reshape(-1)
+    extra = dict(res)
+    extra["nmse_it2"] = nmse(res["theta_it2"], d["h"])
+    extra["nmse_init"] = nmse(d["h0"], d["h"])
+    if seed == 7:
+        # same data through the LLF / hard-ML / PM variants
+        ns_llf = load_defs(os.path.join(PMD, "IterationsvsLLF.py"), N=N,
+                           beta_min=0.0, beta_max=2 * np.pi)
+        th, llf = quiet(ns_llf["em"], d["Y_d"], d["Y_p"], T_d, T_p, d["Z_p"], d["Z_d"],
+                        d["Ptd"], d["aps"], M, varn, 2, d["h0"], n_tx)
+        extra["llf_soft_theta"] = np.asarray(th).reshape(-1)
+        extra["llf_soft"] = np.asarray(llf).reshape(-1)
+        ns_ml = load_defs(os.path.join(PMD, "ML_detecctor.py"), N=N, n_tx=n_tx,
+                          Z_d=d["Z_d"], beta_min=0.0, beta_max=2 * np.pi)
+        th, llf = quiet(ns_ml["em"], d["Y_d"], d["Y_p"], T_d, T_p, d["Z_p"], d["Ptd"],
+                        d["aps"], M, varn, 2, d["h0"])
+        extra["ml_theta"] = np.asarray(th).reshape(-1)
+        extra["ml_llf"] = np.asarray(llf).reshape(-1)
+        cons = _cons(M)
+        ns_pm = load_defs(os.path.join(PMD, "PM.py"), N=N, beta_min=0.0,
+                          beta_max=2 * np.pi)
+        th = quiet(ns_pm["em_pm"], d["Y_d"], d["Y_p"], T_d, T_p, d["Z_p"], d["Ptd"],
+                   d["aps"], M, varn, 3, d["h0"], d["h"], n_tx, 0, d["X_d"], cons)
+        extra["pm_r0_theta"] = np.asarray(th).reshape(-1)
+        ns_pmb = load_defs(os.path.join(PMD, "PM_beta.py"), N=N, qamCons=cons,
+                           beta_min=0.0, beta_max=2 * np.pi)
+        th = quiet(ns_pmb["em_pm"], d["Y_d"], d["Y_p"], T_d, T_p, d["Z_p"], d["Ptd"],
+                   M, varn, 3, d["h0"], d["h"], n_tx, 1, d["X_d"], cons)
+        extra["pmbeta_r1_theta"] = np.asarray(th).reshape(-1)
+        ns_all = load_defs(os.path.join(PMD, "all_detectorsvsTd.py"), N=N, n_tx=n_tx,
+                           qamCons=cons, h=d["h"], Z_d=d["Z_d"], beta_min=0.0,
+                           beta_max=2 * np.pi)
+        th = quiet(ns_all["em_zf"], d["Y_d"], d["Y_p"], T_d, T_p, d["Z_p"], d["Ptd"],
+                   d["aps"], M, varn, 3, d["h0"], d["h"])
+        extra["zf_theta"] = np.asarray(th).reshape(-1)
+        th = quiet(ns_all["em_mmse"], d["Y_d"], d["Y_p"], T_d, T_p, d["Z_p"], d["Ptd"],
+                   d["aps"], M, varn, 3, d["h0"], d["h"])
+        extra["mmse_theta"] = np.asarray(th).reshape(-1)
+    return f"kat1_s{seed}", _pack(d, N=N, n_tx=n_tx, n_rx=n_rx, T_d=T_d, T_p=T_p, M=M,
+                                  varn=varn, seed=seed, **extra)
+
+
+def case_kat2():
+    """KAT-2: PMd/SNR/all_Detectors.py, em (:242-274), driver order :362-377."""
+    N, n_tx, n_rx, T_d, T_p, M, itera = 10, 2, 2, 50, 12, 4, 5
+    SNR = [-5, 0, 5, 10, 15, 20]
+    varns = np.array([10 / np.power(10, s / 10) for s in SNR])
+    ns = load_defs(os.path.join(PMD, "SNR", "all_Detectors.py"), N=N, n_tx=n_tx,
+                   beta_min=0.0, beta_max=2 * np.pi)
+    np.random.seed(0)
+    h = quiet(ns["channelMatrix"], n_tx, n_rx, N, 1)
+    X_d, aps, qamCons = ns["symbols"](n_tx, M, T_d)
+    X_p = ns["pilotSymbols"](n_tx, M, T_p)
+    Ptp, Ptd = ns["irsMatrix"](T_p, T_d, N, 0, 1)
+    Ptd = np.insert(Ptd, 0, np.ones((1, T_d), dtype="complex128"), axis=0)
+    Yps, Yds, h0s, thetas, thetas_ml, nm, nm_ml = [], [], [], [], [], [], []
+    for k in range(len(SNR)):
+        Y_p, Y_d, Z_p, Z_d, h0 = ns["receivedSignals"](T_p, T_d, Ptp, Ptd, n_rx, n_tx,
+                                                        X_d, X_p, h, varns[k], M)
+        th = quiet(ns["em"], Y_d, Y_p, T_d, T_p, Z_p, Ptd, aps, M, varns[k], itera, h0)
+        thm = quiet(ns["em_ml"], Y_d, Y_p, T_d, T_p, Z_p, Ptd, aps, M, varns[k], itera, h0)
+        Yps.append(np.stack(Y_p)[..., 0]); Yds.append(np.stack(Y_d)[..., 0])
+        h0s.append(np.asarray(h0).reshape(-1))
+        thetas.append(np.asarray(th).reshape(-1)); thetas_ml.append(np.asarray(thm).reshape(-1))
+        nm.append(nmse(th, h)); nm_ml.append(nmse(thm, h))
+    return "kat2_snr", dict(
+        h=h, X_d=np.stack(X_d)[..., 0], X_p=np.stack(X_p)[..., 0], aps=aps, Ptp=Ptp,
+        Ptd=Ptd, Z_p=np.stack(Z_p), Y_p=np.stack(Yps), Y_d=np.stack(Yds),
+        h0=np.stack(h0s), theta=np.stack(thetas), theta_ml=np.stack(thetas_ml),
+        nmse=np.array(nm), nmse_ml=np.array(nm_ml), snr=np.array(SNR), varn=varns,
+        N=N, n_tx=n_tx, n_rx=n_rx, T_d=T_d, T_p=T_p, M=M, itera=itera, seed=0)
+
+
+def case_shape(name, N, n_tx, n_rx, T_d, T_p, M, varn, itera, seed):
+    """Extra shapes through the north-star em (odd stream splits, 16/64-QAM)."""
+    ns = load_defs(os.path.join(PMD, "Proposed_method_NMSEvsTp.py"),
+                   N=N, n_tx=n_tx, n_rx=n_rx, beta_min=0.0, beta_max=2 * np.pi)
+    d = _gen_northstar(ns, seed, N, n_tx, n_rx, T_d, T_p, M, varn)
+    th = quiet(ns["em"], d["Y_d"], d["Y_p"], T_d, T_p, d["Z_p"], d["Ptd"], d["aps"], M,
+               varn, itera, d["h0"])
+    return name, _pack(d, N=N, n_tx=n_tx, n_rx=n_rx, T_d=T_d, T_p=T_p, M=M, varn=varn,
+                       itera=itera, seed=seed, theta=np.asarray(th).reshape(-1),
+                       nmse=nmse(th, d["h"]))
+
+
+def case_root():
+    """Root-level Proposed_method_NMSEvsTp.py: zero init, float path (:43-69),
+    C-order h (:16), N x T_p DFT over T_p plus a ones row (:73-77, :129)."""
+    N, n_tx, n_rx, T_d, T_p, M, varn, itera = 4, 2, 2, 10, 6, 4, 0.1, 3
+    ns = load_defs(os.path.join(REF, "Proposed_method_NMSEvsTp.py"), N=N, n_tx=n_tx,
+                   beta_min=0.0, beta_max=2 * np.pi)
+    np.random.seed(3)
+    h = quiet(ns["channelMatrix"], n_tx, n_rx, N, 1)
+    X_d, aps = ns["symbols"](n_tx, M, T_d)
+    Ptp, Ptd = ns["irsMatrix"](T_p, T_d, N, 0, 1)
+    Ptp = np.insert(Ptp, 0, np.ones((1, T_p), dtype="complex128"), axis=0)
+    Ptd = np.insert(Ptd, 0, np.ones((1, T_d), dtype="complex128"), axis=0)
+    X_p = ns["pilotSymbols"](n_tx, M, T_p)
+    Y_p, Y_d, Z_p, Z_d = ns["receivedSignals"](T_p, T_d, Ptp, Ptd, n_rx, n_tx, X_d, X_p,
+                                               h, varn, M)
+    th = quiet(ns["em"], Y_d, Y_p, T_d, T_p, Z_p, Ptd, aps, M, varn, itera)
+    d = dict(h=h, X_d=X_d, aps=aps, X_p=X_p, Ptp=Ptp, Ptd=Ptd, Y_p=Y_p, Y_d=Y_d, Z_p=Z_p,
+             h0=np.zeros(len(h), dtype=complex))
+    return "root_tp", _pack(d, N=N, n_tx=n_tx, n_rx=n_rx, T_d=T_d, T_p=T_p, M=M,
+                            varn=varn, itera=itera, seed=3,
+                            theta=np.asarray(th).reshape(-1), nmse=nmse(th, h))
+
+
+def case_qam():
+    """Constellation tables of the vendored komm QAM (PMd/QAM.py:320-322)."""
+    return "qam", {f"cons{M}": _cons(M) for M in (4, 16, 64, 256)}
+
+
+CASES = {
+    "qam": (case_qam, ()),
+    "kat1_s7": (case_kat1, (7,)),
+    "kat1_s11": (case_kat1, (11,)),
+    "kat2_snr": (case_kat2, ()),
+    "root_tp": (case_root, ()),
+    "nt4_m4": (case_shape, ("nt4_m4", 3, 4, 4, 16, 8, 4, 0.1, 2, 5)),
+    "nt3_m4": (case_shape, ("nt3_m4", 3, 3, 2, 10, 8, 4, 0.2, 2, 9)),
+    "nt1_m16": (case_shape, ("nt1_m16", 5, 1, 3, 20, 6, 16, 0.3, 3, 4)),
+    "nt2_m16": (case_shape, ("nt2_m16", 4, 2, 2, 12, 8, 16, 0.5, 2, 6)),
+    "nt2_m64": (case_shape, ("nt2_m64", 3, 2, 2, 6, 10, 64, 1.0, 2, 8)),
+}
+
+
+def run(name):
+    fn, args = CASES[name]
+    t0 = time.time()
+    key, arrays = fn(*args)
+    np.savez_compressed(os.path.join(OUT, key + ".npz"), **arrays)
+    return key, time.time() - t0
+
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(CASES)
+    with Pool(min(len(names), 7)) as pool:
+        for key, dt in pool.imap_unordered(run, names):
+            print(f"{key}: {dt:.1f}s", flush=True)

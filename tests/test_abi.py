@@ -1,0 +1,79 @@
+"""CPU tier: the C-ABI library loads and exports every symbol include/sbce.h
+declares; struct layouts agree between C (gcc) and the ctypes binding; argument
+validation works without touching a GPU."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "sbce.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(sbce_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_expected_entry_points(sbce):
+    assert _declared() == sorted(sbce._lib.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol(sbce):
+    lib = sbce._lib.load()
+    for name in _declared():
+        assert hasattr(lib, name), name
+    assert lib.sbce_abi_version() == sbce._lib.SBCE_ABI_VERSION
+    assert lib.sbce_strerror(-1)
+
+
+def test_struct_layout_matches_c(sbce, tmp_path):
+    """Compile a probe against include/sbce.h with gcc and compare sizes/offsets."""
+    probe = tmp_path / "probe.c"
+    probe.write_text(r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "sbce.h"
+int main(void) {
+  printf("%zu %zu %zu %zu\n", sizeof(sbce_dims), offsetof(sbce_dims, varn),
+         sizeof(sbce_ptrs), offsetof(sbce_ptrs, workspace_bytes));
+  return 0;
+}''')
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(probe), "-o", str(exe)],
+                   check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    L = sbce._lib
+    assert [int(v) for v in out] == [ctypes.sizeof(L.Dims), L.Dims.varn.offset,
+                                     ctypes.sizeof(L.Ptrs), L.Ptrs.workspace_bytes.offset]
+
+
+def test_workspace_and_validation_without_gpu(sbce):
+    L = sbce._lib
+    lib = L.load()
+    d = L.Dims(1000, 4, 4, 65, 16, 256, 16, 0, 0.1)
+    n = L.workspace_bytes(d)
+    Lw = 65 * 4
+    expect = 1000 * 256 * 20 * 16 + 1000 * Lw * Lw * 16 + 1000 * Lw * 4 * 16
+    assert expect <= n <= expect + 4 * 256 + 4000
+    bad = L.Dims(1, 9, 4, 65, 16, 256, 16, 0, 0.1)     # n_tx > 4
+    nb = ctypes.c_size_t(0)
+    assert lib.sbce_workspace_bytes(ctypes.byref(bad), ctypes.byref(nb)) == -1
+    bad2 = L.Dims(1, 2, 2, 5, 4, 8, 4, 0, 0.0)         # varn must be > 0
+    assert lib.sbce_workspace_bytes(ctypes.byref(bad2), ctypes.byref(nb)) == -1
+    # null pointers are rejected before any HIP call
+    p = L.Ptrs()
+    assert lib.sbce_em(ctypes.byref(d), ctypes.byref(p), 1, 0, 0, None) == -1
+
+
+def test_product_path_fails_loudly_without_gpu(sbce):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    d = {"Y_d": None}
+    with pytest.raises(sbce.SbceUnavailable):
+        sbce.em_batch(*(None,) * 5, 0.1, 1, None)
+    del d

@@ -1,0 +1,201 @@
+"""GPU tier: the HIP path through the C-ABI against the reference's golden
+vectors and the CPU oracle.
+
+Tolerances (float64 everywhere): theta relative max-error <= 1e-10 against the
+reference's own em() on well-posed fixtures (measured ~1e-14); the north-star
+bar "NMSE curve within 1e-3 relative" is asserted separately and is met with
+~10 orders of margin.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden, rel, ref_lists
+from oracle.em_reduced import (em_reduced, estep_moments, mstep_build, mstep_solve, u_from_zp,
+                               cons_from_aps, nmse)
+
+pytestmark = pytest.mark.gpu
+
+SOFT_CASES = ["kat1_s7", "kat1_s11", "nt3_m4", "nt1_m16", "root_tp", "nt4_m4", "nt2_m16",
+              "nt2_m64"]
+THETA_TOL = 1e-10
+
+
+def _itera(d):
+    return int(d["itera"]) if "itera" in d else 2
+
+
+@pytest.mark.parametrize("case", SOFT_CASES)
+def test_em_matches_reference(sbce, case):
+    """Drop-in em() (reference signature) vs the reference em() output."""
+    d = golden(case)
+    Y_d, Y_p, Z_p = ref_lists(d)
+    h0 = None if case == "root_tp" else d["h0"].reshape(-1, 1)
+    th = sbce.em(Y_d, Y_p, int(d["T_d"]), int(d["T_p"]), Z_p, d["Ptd"], d["aps"], int(d["M"]),
+                 float(d["varn"]), _itera(d), h0)
+    ref = d["theta"] if "theta" in d else d["theta_it2"]
+    assert th.shape == (ref.size, 1) and th.dtype == np.complex128
+    assert rel(th, ref) < THETA_TOL
+
+
+def test_em_single_iteration_and_inputs_untouched(sbce):
+    d = golden("kat1_s7")
+    Y_d, Y_p, Z_p = ref_lists(d)
+    h0 = d["h0"].reshape(-1, 1).copy()
+    Y0 = [y.copy() for y in Y_d]
+    th = sbce.em(Y_d, Y_p, 40, 12, Z_p, d["Ptd"], d["aps"], 4, float(d["varn"]), 1, h0)
+    assert rel(th, d["theta_it1"]) < THETA_TOL
+    assert np.array_equal(h0, d["h0"].reshape(-1, 1))
+    assert all(np.array_equal(a, b) for a, b in zip(Y_d, Y0))
+
+
+def test_em_ml_matches_reference(sbce):
+    d = golden("kat1_s7")
+    Y_d, Y_p, Z_p = ref_lists(d)
+    th = sbce.em_ml(Y_d, Y_p, 40, 12, Z_p, d["Ptd"], d["aps"], 4, float(d["varn"]), 2,
+                    d["h0"].reshape(-1, 1))
+    assert rel(th, d["ml_theta"]) < THETA_TOL
+
+
+def test_llf_matches_reference(sbce):
+    """IterationsvsLLF.em (soft) and ML_detecctor.em (hard) per-iteration LLF."""
+    d = golden("kat1_s7")
+    Y_d, Y_p, Z_p = ref_lists(d)
+    Ud = np.einsum("pt,ta->tpa", d["Ptd"], d["X_d"]).reshape(40, -1)
+    Z_d = [np.kron(u[None], np.eye(2)) for u in Ud]
+    th, llf = sbce.em_llf(Y_d, Y_p, 40, 12, Z_p, Z_d, d["Ptd"], d["aps"], 4, float(d["varn"]), 2,
+                          d["h0"].reshape(-1, 1), 2)
+    assert llf.shape == (2, 1)
+    assert rel(th, d["llf_soft_theta"]) < THETA_TOL
+    assert rel(llf, d["llf_soft"]) < 1e-12
+    th, llf = sbce.em_ml_llf(Y_d, Y_p, 40, 12, Z_p, d["Ptd"], d["aps"], 4, float(d["varn"]), 2,
+                             d["h0"].reshape(-1, 1), Z_d=Z_d)
+    assert rel(th, d["ml_theta"]) < THETA_TOL
+    assert rel(llf, d["ml_llf"]) < 1e-12
+
+
+def test_nmse_vs_snr_curve_kat2(sbce):
+    """The north-star parity target: NMSE-vs-SNR of PMd/SNR/all_Detectors.py em (exact) and
+    em_ml, one trial, SNR -5..20 dB, all six points in ONE batched call."""
+    k = golden("kat2_snr")
+    Up = u_from_zp(k["Z_p"], 2)
+    cons = cons_from_aps(k["aps"], 4)
+    B = 6
+    for mode, key, nkey in (("soft", "theta", "nmse"), ("hard", "theta_ml", "nmse_ml")):
+        thetas = []
+        for i in range(B):    # varn differs per SNR point: one call per point
+            r = sbce.em_batch(k["Y_d"][i][None], k["Y_p"][i][None], k["Ptd"].T[None], Up[None],
+                              cons, float(k["varn"][i]), 5, k["h0"][i][None], mode=mode)
+            thetas.append(r["theta"][0])
+        for i in range(B):
+            assert rel(thetas[i], k[key][i]) < 1e-9
+            nm = nmse(thetas[i], k["h"])
+            assert abs(nm / k[nkey][i] - 1) < 1e-9          # measured parity
+            assert abs(nm / k[nkey][i] - 1) < 1e-3          # north-star bar
+
+
+def _random_problem(rng, B, n_tx, n_rx, N, T_p, T_d, M, varn, sbce, seed=0):
+    return sbce.signal_model.synthetic_batch(B, n_tx, n_rx, N, T_p, T_d, M, varn, seed=seed)
+
+
+@pytest.mark.parametrize("shape", [
+    # (n_tx, n_rx, N, T_p, T_d, M, snr_db)
+    (1, 3, 5, 6, 20, 16, 10),
+    (2, 2, 8, 12, 40, 4, 20),
+    (2, 2, 8, 12, 40, 4, -5),
+    (2, 4, 6, 8, 24, 16, 15),
+    (2, 2, 3, 10, 12, 64, 25),
+    (3, 2, 3, 8, 20, 16, 20),
+    (4, 4, 4, 16, 12, 4, 20),
+    (4, 4, 8, 16, 6, 16, 20),
+    (4, 4, 8, 16, 6, 16, 0),
+    (4, 8, 2, 8, 4, 16, 20),
+])
+def test_estep_moments_vs_oracle(sbce, shape):
+    """Device E-step (sbce_estep) vs the oracle's posterior moments, including the
+    cfg-1 kernel instantiation (n_tx=n_rx=4, 16-QAM: 65,536 hypotheses per symbol)
+    at high SNR (exp-skip active) and low SNR (no skipping)."""
+    n_tx, n_rx, N, T_p, T_d, M, snr = shape
+    varn = float(sbce.signal_model.snr_to_varn(snr))
+    b = sbce.signal_model.synthetic_batch(2, n_tx, n_rx, N, T_p, T_d, M, varn, seed=11)
+    aps = sbce.qam.all_possible_symbols(b["cons"], n_tx)
+    m, S = sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx)
+    mh, Sh = sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx, "hard")
+    for i in range(2):
+        m0, S0, _, _ = estep_moments(b["theta0"][i], b["y_d"][i], b["psi_d"][i].T, aps, varn)
+        scale = np.abs(b["cons"]).max() ** 2
+        assert np.abs(m[i] - m0).max() < 1e-11 * scale
+        assert np.abs(S[i] - S0).max() < 1e-11 * scale
+        mh0, Sh0, _, _ = estep_moments(b["theta0"][i], b["y_d"][i], b["psi_d"][i].T, aps, varn,
+                                       "hard")
+        assert np.array_equal(mh[i], mh0) and np.allclose(Sh[i], Sh0, rtol=0, atol=1e-13)
+
+
+@pytest.mark.parametrize("shape", [(2, 2, 8, 12, 40, 4), (4, 4, 16, 16, 40, 16),
+                                   (3, 3, 6, 10, 30, 4), (1, 2, 5, 6, 12, 16)])
+def test_mstep_normal_equations_and_solve_vs_oracle(sbce, shape):
+    n_tx, n_rx, N, T_p, T_d, M = shape
+    varn = 0.3
+    b = sbce.signal_model.synthetic_batch(3, n_tx, n_rx, N, T_p, T_d, M, varn, seed=5)
+    aps = sbce.qam.all_possible_symbols(b["cons"], n_tx)
+    ms, Ss = [], []
+    for i in range(3):
+        m0, S0, _, _ = estep_moments(b["theta0"][i], b["y_d"][i], b["psi_d"][i].T, aps, varn)
+        ms.append(m0)
+        Ss.append(S0)
+    th, R, rhs, status = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"],
+                                          np.stack(ms), np.stack(Ss), varn)
+    for i in range(3):
+        R0, rhs0 = mstep_build(b["u_p"][i], b["y_p"][i], b["psi_d"][i].T, b["y_d"][i], ms[i], Ss[i])
+        assert rel(R[i], R0) < 1e-13
+        assert rel(rhs[i], rhs0) < 1e-13
+        th0 = mstep_solve(R0, rhs0)
+        cond = np.linalg.cond(R0)
+        assert rel(th[i], th0) < max(1e-12, 1e-15 * cond), cond
+        assert status[i] == 0
+
+
+def test_cfg1_shape_full_em_vs_oracle(sbce):
+    """BASELINE cfg 1 shape (Nt=Nr=4, N_RIS=64, T_p=16, T_d=256, 16-QAM, SNR 20 dB):
+    one trial, two EM iterations, device vs the float64 oracle."""
+    varn = float(sbce.signal_model.snr_to_varn(20.0))
+    b = sbce.signal_model.synthetic_batch(1, 4, 4, 64, 16, 256, 16, varn, seed=1)
+    aps = sbce.qam.all_possible_symbols(b["cons"], 4)
+    r = sbce.em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, 2, b["theta0"])
+    th0 = em_reduced(b["y_d"][0], b["y_p"][0], b["u_p"][0], b["psi_d"][0].T, aps, varn, 2,
+                     b["theta0"][0])
+    R0, _ = mstep_build(b["u_p"][0], b["y_p"][0], b["psi_d"][0].T, b["y_d"][0],
+                        *estep_moments(th0, b["y_d"][0], b["psi_d"][0].T, aps, varn)[:2])
+    cond = np.linalg.cond(R0)
+    assert rel(r["theta"][0], th0) < max(1e-10, 1e-14 * cond)
+    assert abs(nmse(r["theta"][0], b["h"][0]) / nmse(th0, b["h"][0]) - 1) < 1e-3
+
+
+def test_batch_equals_single_and_is_deterministic(sbce):
+    varn = 0.2
+    b = sbce.signal_model.synthetic_batch(5, 2, 2, 6, 8, 20, 16, varn, seed=3)
+    r = sbce.em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, 3, b["theta0"])
+    r2 = sbce.em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, 3, b["theta0"])
+    assert np.array_equal(r["theta"], r2["theta"])
+    for i in range(5):
+        ri = sbce.em_batch(b["y_d"][i:i + 1], b["y_p"][i:i + 1], b["psi_d"][i:i + 1],
+                           b["u_p"][i:i + 1], b["cons"], varn, 3, b["theta0"][i:i + 1])
+        assert np.array_equal(ri["theta"][0], r["theta"][i])
+    assert (r["iters_done"] == 3).all()
+
+
+def test_device_nmse(sbce):
+    b = sbce.signal_model.synthetic_batch(4, 2, 2, 5, 6, 10, 4, 0.1, seed=2)
+    out = sbce.nmse_batch(b["theta0"], b["h"]).cpu().numpy()
+    want = [nmse(b["theta0"][i], b["h"][i]) for i in range(4)]
+    assert np.allclose(out, want, rtol=1e-13)
+
+
+def test_singular_system_flags_and_drop_mode(sbce):
+    """Rank-deficient normal equations (L > T_p + T_d at high SNR): status flagged;
+    'drop' mode stays finite."""
+    varn = 0.01
+    b = sbce.signal_model.synthetic_batch(1, 2, 2, 20, 4, 6, 4, varn, seed=9)   # L = 42 > 4 + 6
+    r = sbce.em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, 1, b["theta0"],
+                      solve="drop")
+    assert np.isfinite(r["theta"]).all()
+    assert r["status"][0] & sbce._lib.SBCE_STATUS_NONHPD

@@ -1,0 +1,216 @@
+"""CPU tier: the oracle (both faces) and the host-side signal model are pinned
+against golden vectors produced by the reference's own functions
+(tests/golden/make_golden.py, SURVEY.md §8c known-answer values)."""
+import numpy as np
+import pytest
+
+from conftest import golden, rel
+from oracle.em_loop import em_loop, llf_genie
+from oracle.em_reduced import (em_reduced, u_from_zp, cons_from_aps, aps_from_cons, nmse,
+                               estep_moments, mstep_build, mstep_solve)
+
+SOFT_CASES = ["kat1_s7", "kat1_s11", "nt3_m4", "nt1_m16", "root_tp", "nt4_m4", "nt2_m16",
+              "nt2_m64"]
+
+
+def _run_reduced(d, mode="soft", itera=None):
+    n_rx = int(d["n_rx"])
+    it = itera or (int(d["itera"]) if "itera" in d else 2)
+    return em_reduced(d["Y_d"], d["Y_p"], u_from_zp(d["Z_p"], n_rx), d["Ptd"], d["aps"],
+                      float(d["varn"]), it, d["h0"], mode=mode, return_trace=True)
+
+
+@pytest.mark.parametrize("case", SOFT_CASES)
+def test_reduced_oracle_matches_reference_em(case):
+    d = golden(case)
+    th, _ = _run_reduced(d)
+    ref = d["theta"] if "theta" in d else d["theta_it2"]
+    assert rel(th, ref) < 1e-12
+
+
+def test_kat1_known_answers():
+    """seed 7 NMSE(theta0)=0.3124412991124182, NMSE(em)=7.765079093716e-02;
+    seed 11 NMSE(em)=5.305423058721e-02."""
+    d7, d11 = golden("kat1_s7"), golden("kat1_s11")
+    assert abs(nmse(d7["h0"], d7["h"]) - 0.3124412991124182) < 1e-13
+    assert abs(float(d7["nmse_it2"]) - 7.765079093716e-02) < 1e-13
+    assert abs(float(d11["nmse_it2"]) - 5.305423058721e-02) < 1e-13
+    th, tr = _run_reduced(d7)
+    assert rel(tr[0], d7["theta_it1"]) < 1e-12
+    assert abs(nmse(th, d7["h"]) / 7.765079093716e-02 - 1) < 1e-10
+
+
+def test_loop_oracle_matches_reference():
+    d = golden("kat1_s7")
+    Y_d = [y[:, None] for y in d["Y_d"]]
+    Y_p = [y[:, None] for y in d["Y_p"]]
+    th = em_loop(Y_d, Y_p, 40, 12, list(d["Z_p"]), d["Ptd"], d["aps"], 4, float(d["varn"]), 2,
+                 d["h0"])
+    assert rel(th, d["theta_it2"]) < 1e-12
+    thm = em_loop(Y_d, Y_p, 40, 12, list(d["Z_p"]), d["Ptd"], d["aps"], 4, float(d["varn"]), 2,
+                  d["h0"], hard=True)
+    assert rel(thm, d["ml_theta"]) < 1e-12
+
+
+def test_hard_ml_and_llf_match_reference():
+    """IterationsvsLLF.em and ML_detecctor.em on the KAT-1 seed-7 data."""
+    d = golden("kat1_s7")
+    n_rx, varn = 2, float(d["varn"])
+    Ud = np.einsum("pt,ta->tpa", d["Ptd"], d["X_d"]).reshape(d["Y_d"].shape[0], -1)
+    Zd = np.stack([np.kron(u[None], np.eye(n_rx)) for u in Ud])
+    for mode, key_th, key_llf in (("soft", "llf_soft_theta", "llf_soft"),
+                                  ("hard", "ml_theta", "ml_llf")):
+        th, tr = _run_reduced(d, mode=mode, itera=2)
+        assert rel(th, d[key_th]) < 1e-12
+        llf = [llf_genie(t, d["Y_p"][..., None], d["Z_p"], d["Y_d"][..., None], Zd, 40, 12, 2, 4,
+                         varn) for t in tr]
+        assert rel(llf, d[key_llf]) < 1e-12
+
+
+def test_kat2_nmse_vs_snr_curve():
+    """KAT-2: PMd/SNR/all_Detectors.py em at SNR -5..20 dB (the north-star curve)."""
+    k = golden("kat2_snr")
+    Up = u_from_zp(k["Z_p"], 2)
+    survey = [7.116100579890e-01, 4.735312842427e-01, 1.325647368276e-01, 2.408388722975e-01,
+              5.924439598782e-02, 2.295354158055e-01]
+    for i in range(6):
+        th = em_reduced(k["Y_d"][i], k["Y_p"][i], Up, k["Ptd"], k["aps"], float(k["varn"][i]), 5,
+                        k["h0"][i])
+        assert rel(th, k["theta"][i]) < 1e-12
+        assert abs(nmse(th, k["h"]) / k["nmse"][i] - 1) < 1e-10
+        assert abs(k["nmse"][i] / survey[i] - 1) < 1e-10
+        thm = em_reduced(k["Y_d"][i], k["Y_p"][i], Up, k["Ptd"], k["aps"], float(k["varn"][i]),
+                         5, k["h0"][i], mode="hard")
+        assert rel(thm, k["theta_ml"][i]) < 1e-12
+
+
+def test_constellation_and_hypothesis_order(sbce):
+    q = golden("qam")
+    for M in (4, 16, 64, 256):
+        assert np.array_equal(sbce.qam.qam_constellation(M), q[f"cons{M}"])
+    assert sbce.qam.energy_per_symbol(16) == 10.0
+    for case in ("kat1_s7", "nt2_m16", "nt3_m4", "nt4_m4"):
+        d = golden(case)
+        M, n_tx = int(d["M"]), int(d["n_tx"])
+        cons = cons_from_aps(d["aps"], M)
+        assert np.array_equal(cons, q[f"cons{M}"])
+        assert np.array_equal(aps_from_cons(cons, n_tx), d["aps"])
+        assert np.array_equal(sbce.qam.all_possible_symbols(cons, n_tx), d["aps"])
+
+
+def test_signal_model_replays_reference_rng(sbce):
+    """np.random.seed(s) + the north-star call order reproduces the reference's data."""
+    sm = sbce.signal_model
+    for case in ("kat1_s7", "nt3_m4", "nt2_m16"):
+        d = golden(case)
+        N, n_tx, n_rx = int(d["N"]), int(d["n_tx"]), int(d["n_rx"])
+        T_d, T_p, M, varn = int(d["T_d"]), int(d["T_p"]), int(d["M"]), float(d["varn"])
+        np.random.seed(int(d["seed"]))
+        h = sm.channel_matrix(n_tx, n_rx, N, 1.0)
+        X_d, aps = sm.symbols(n_tx, M, T_d)
+        X_p = sm.pilot_symbols(n_tx, M, T_p)
+        Ptp, Ptd = sm.irs_matrix(T_p, T_d, N)
+        Ptd = sm.insert_direct(Ptd)
+        Y_p, Y_d, U_p, U_d, h0 = sm.received_signals(T_p, T_d, Ptp, Ptd, n_rx, n_tx, X_d, X_p, h,
+                                                     varn)
+        assert np.array_equal(h, d["h"])
+        assert np.array_equal(np.stack(X_d)[..., 0], d["X_d"])
+        assert np.array_equal(np.stack(X_p)[..., 0], d["X_p"])
+        assert np.array_equal(aps, d["aps"])
+        assert np.array_equal(Ptd, d["Ptd"]) and np.array_equal(Ptp, d["Ptp"])
+        assert rel(Y_p, d["Y_p"]) < 1e-14 and rel(Y_d, d["Y_d"]) < 1e-14
+        assert rel(U_p, u_from_zp(d["Z_p"], n_rx)) == 0.0
+        assert rel(h0, d["h0"]) < 1e-12
+
+
+def test_root_variant_replay(sbce):
+    """Root-level script: C-order h, N x T_p DFT over T_p plus a ones row (pilots drawn after
+    the RIS phases)."""
+    sm = sbce.signal_model
+    d = golden("root_tp")
+    N, n_tx, n_rx, T_d, T_p, M = 4, 2, 2, 10, 6, 4
+    np.random.seed(3)
+    h = sm.channel_matrix(n_tx, n_rx, N, 1.0, order="C")
+    X_d, aps = sm.symbols(n_tx, M, T_d)
+    Ptp, Ptd = sm.irs_matrix(T_p, T_d, N, pilot="dft_tp")
+    Ptp, Ptd = sm.insert_direct(Ptp), sm.insert_direct(Ptd)
+    X_p = sm.pilot_symbols(n_tx, M, T_p)
+    Y_p, Y_d, U_p, _, _ = sm.received_signals(T_p, T_d, Ptp, Ptd, n_rx, n_tx, X_d, X_p, h, 0.1,
+                                              with_initial=False)
+    assert np.array_equal(h, d["h"])
+    assert rel(Y_d, d["Y_d"]) < 1e-14 and rel(Y_p, d["Y_p"]) < 1e-14
+
+
+def test_moments_are_consistent():
+    """E-step moments: S Hermitian PSD with diag >= |m|^2; hard mode gives x x^H."""
+    rng = np.random.default_rng(0)
+    d = golden("nt2_m16")
+    theta = d["h0"] + 0.1 * (rng.normal(size=d["h0"].shape) + 1j * rng.normal(size=d["h0"].shape))
+    m, S, dmin, logZ = estep_moments(theta, d["Y_d"], d["Ptd"], d["aps"], float(d["varn"]))
+    assert np.allclose(S, np.conj(np.transpose(S, (0, 2, 1))))
+    for t in range(S.shape[0]):
+        assert np.linalg.eigvalsh(S[t] - np.outer(m[t], np.conj(m[t]))).min() > -1e-12
+    mh, Sh, _, _ = estep_moments(theta, d["Y_d"], d["Ptd"], d["aps"], float(d["varn"]), "hard")
+    assert np.allclose(Sh, mh[:, :, None] * np.conj(mh[:, None, :]))
+
+
+def test_reduced_normal_equations_equal_kronecker_form():
+    """The commutation identity: (conj(R) (x) I, vec(B)) equals the reference's K x K
+    sums sum w Z^H Z, sum w Z^H y built from dense Kronecker regressors."""
+    d = golden("nt3_m4")
+    n_rx, n_tx = int(d["n_rx"]), int(d["n_tx"])
+    Up = u_from_zp(d["Z_p"], n_rx)
+    m, S, _, _ = estep_moments(d["h0"], d["Y_d"], d["Ptd"], d["aps"], float(d["varn"]))
+    R, rhs = mstep_build(Up, d["Y_p"], d["Ptd"], d["Y_d"], m, S)
+    # dense reference-form sums with the same posterior
+    aps = d["aps"]
+    J = aps.shape[0]
+    P, T = d["Ptd"].shape
+    K = P * n_tx * n_rx
+    A = np.zeros((K, K), complex)
+    bvec = np.zeros((K, 1), complex)
+    H = np.asarray(d["h0"])
+    for t in range(T):
+        psi = d["Ptd"][:, t]
+        Zs = [np.kron(np.kron(psi[None], aps[j][None]), np.eye(n_rx)) for j in range(J)]
+        dd = np.array([np.linalg.norm(d["Y_d"][t][:, None] - Z @ H[:, None]) ** 2 for Z in Zs])
+        w = np.exp(-(dd - dd.min()) / float(d["varn"]) ** 2)
+        w /= w.sum()
+        for j in range(J):
+            A += w[j] * np.conj(Zs[j]).T @ Zs[j]
+            bvec += w[j] * np.conj(Zs[j]).T @ d["Y_d"][t][:, None]
+    for t in range(len(d["Z_p"])):
+        A += np.conj(d["Z_p"][t]).T @ d["Z_p"][t]
+        bvec += np.conj(d["Z_p"][t]).T @ d["Y_p"][t][:, None]
+    assert rel(np.kron(np.conj(R), np.eye(n_rx)), A) < 1e-12
+    assert rel(np.conj(rhs).reshape(-1), bvec) < 1e-12
+    assert rel(mstep_solve(R, rhs), np.linalg.solve(A, bvec)) < 1e-10
+
+
+def _fexp_neg_numpy(z):
+    """Bit-level numpy mirror of csrc/sbce_internal.h fexp_neg (Cody-Waite + degree-12)."""
+    z = np.maximum(z, -745.5)
+    kd = np.rint(z * 1.4426950408889634074)
+    # the device reduction is an FMA; kd*ln2_hi (11 x 53 bits) is exact in x87 long double
+    ld = np.longdouble
+    r = (ld(z) - kd.astype(ld) * ld(6.93147180559945286227e-01)).astype(np.float64)
+    r = r - kd * 2.31904681384629955842e-17
+    c = [1.0, 1.0, 0.5, 1.66666666666666666667e-01, 4.16666666666666666667e-02,
+         8.33333333333333333333e-03, 1.38888888888888888889e-03, 1.98412698412698412698e-04,
+         2.48015873015873015873e-05, 2.75573192239858906526e-06, 2.75573192239858906526e-07,
+         2.50521083854417187751e-08, 2.08767569878680989792e-09]
+    p = np.full_like(r, c[12])
+    for k in range(11, -1, -1):
+        p = p * r + c[k]
+    return np.ldexp(p, kd.astype(np.int64))
+
+
+def test_device_exp_polynomial_accuracy():
+    """The E-step's exp() (sbce_internal.h fexp_neg) is accurate to a few ulp on [-745, 0]."""
+    z = -np.concatenate([np.linspace(0, 1, 2001), np.linspace(1, 700, 20001)])
+    got = _fexp_neg_numpy(z)
+    want = np.exp(z)
+    rel_err = np.abs(got - want) / want
+    assert rel_err.max() < 1e-15
+    assert _fexp_neg_numpy(np.array([-np.inf]))[0] == 0.0
+    assert _fexp_neg_numpy(np.array([0.0]))[0] == 1.0
