@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Benchmark: EM-iterations/s of the MI355X EM semi-blind channel estimator.
+
+Metric (BASELINE.json): EM-iterations/sec (whole node) on Nt=Nr=4, N_RIS=64,
+T_p=16, T_d=256, 16-QAM (BASELINE configs[1]: 1000 Monte-Carlo trials x 20 EM
+iterations per GPU), SNR 20 dB, exact soft E-step, float64.
+
+A "step" = one full estimator call (``sbce_em``: 20 EM iterations, E-step +
+M-step) over the whole per-GPU batch of trials, inputs resident in HBM.
+value = (trials on all ranks x EM iterations x steps) / max-over-ranks time.
+
+Multi-GPU (``torchrun --nproc-per-node N``): Monte-Carlo trials shard across
+ranks (each rank its own trials, weak scaling, no data-path collective); the
+only collective is ONE all-reduce (RCCL) of the per-rank NMSE accumulators
+after the timed region, as in the reference's Monte-Carlo average
+(Proposed_method_NMSEvsTp.py:176).
+
+Also reported (one JSON line on rank 0):
+  roofline      E-step kernel (dominant) timed live with HIP events on the
+                launch stream; algorithmic flops per launch;
+                peak = FP64 rate of MI355X; traffic from the committed
+                rocprofv3 PMC summary when present.
+  cpu_baseline  the build's vectorised float64 NumPy port of the same
+                algorithm (oracle/em_reduced.py) on a bounded sample of the
+                same workload, on this host's cores (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector (= FP64 matrix); half the guide's 157.3 TF FP32
+HBM_PEAK_GBS = 8000.0
+
+CONFIGS = {
+    # name: (n_tx, n_rx, N_RIS, T_p, T_d, M, trials per GPU, EM iterations)
+    "cfg1": (4, 4, 64, 16, 256, 16, 1000, 20),
+    "plumbing": (2, 2, 16, 16, 50, 4, 10, 10),
+}
+
+
+def estep_flops_per_trial_iter(n_tx, n_rx, T_d, M):
+    """Minimal data-independent E-step work: every one of the T_d*M^n_tx hypotheses
+    needs its distance d = a_i + g_k - 2 Re(p_i^H q_k): 2*n_rx real FMAs (4*n_rx flop)
+    + 1 add + 1 compare.  Exp/accumulate work is data dependent (skipped for
+    hypotheses below e^-50 of the running maximum) and not counted."""
+    return T_d * (M ** n_tx) * (4 * n_rx + 2)
+
+
+def estep_bytes_per_trial_iter(n_tx, n_rx, P, T_d):
+    """Minimal HBM bytes of one E-step per trial: y_d, psi_d, theta read once,
+    moments written once (complex128)."""
+    K = P * n_tx * n_rx
+    return 16 * (T_d * n_rx + T_d * P + K + T_d * (n_tx + n_tx * n_tx))
+
+
+def load_pmc_traffic(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(cfg, varn, seed, iters=2):
+    """Oracle port (vectorised float64 NumPy reduced form) on 1 trial x `iters` EM
+    iterations of the same configuration: ~10-30 s of CPU work."""
+    import importlib
+    from oracle.em_reduced import em_reduced
+    pkg = importlib.import_module(
+        "semi-blind-channel-estimation-for-mimo-ris-communication-system-using-em-algo_amd")
+    n_tx, n_rx, N, T_p, T_d, M, _, _ = cfg
+    b = pkg.signal_model.synthetic_batch(1, n_tx, n_rx, N, T_p, T_d, M, varn, seed=seed + 12345)
+    aps = pkg.qam.all_possible_symbols(b["cons"], n_tx)
+    t0 = time.perf_counter()
+    em_reduced(b["y_d"][0], b["y_p"][0], b["u_p"][0], b["psi_d"][0].T, aps, varn, iters,
+               b["theta0"][0])
+    dt = time.perf_counter() - t0
+    cores = len(os.sched_getaffinity(0))
+    threads = os.environ.get("OMP_NUM_THREADS")
+    return {"value": iters / dt, "unit": "EM-iterations/s", "cores": cores,
+            "kind": "port",
+            "sample": f"1 trial x {iters} EM iterations of the same config, oracle/em_reduced.py "
+                      f"(NumPy float64, BLAS threads={threads or 'default'}), {dt:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="cfg1", choices=sorted(CONFIGS))
+    ap.add_argument("--trials", type=int, default=None, help="trials per GPU")
+    ap.add_argument("--iters", type=int, default=None, help="EM iterations per step")
+    ap.add_argument("--snr", type=float, default=20.0)
+    ap.add_argument("--mode", default="soft", choices=["soft", "hard"])
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-reps", type=int, default=5)
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_estep_latest.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as ge
+    pkg = ge.package()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    cfg = list(CONFIGS[args.config])
+    if args.trials:
+        cfg[6] = args.trials
+    if args.iters:
+        cfg[7] = args.iters
+    n_tx, n_rx, N, T_p, T_d, M, B, iters = cfg
+    varn = float(pkg.signal_model.snr_to_varn(args.snr))
+
+    # ---- synthetic inputs for this rank's trials, resident in HBM before timing ----
+    batch = pkg.signal_model.synthetic_batch(B, n_tx, n_rx, N, T_p, T_d, M, varn,
+                                             seed=args.seed * 1000003 + rank)
+    eng = pkg.em.EMEngine(batch, varn, mode=args.mode)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        eng.run(iters)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.run(iters)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    # ---- the one collective: Monte-Carlo NMSE accumulators (sum NMSE, count) ----
+    nm = eng.nmse()
+    acc = torch.stack([nm.sum(), torch.tensor(float(B), dtype=torch.float64, device="cuda")])
+    if world > 1:
+        dist.all_reduce(acc, op=dist.ReduceOp.SUM)
+    nmse_mean = float(acc[0] / acc[1])
+    nonhpd = int((eng.status != 0).sum().item())
+
+    # ---- dominant-kernel timing: E-step launches with HIP events on the launch stream ----
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    eng.estep()
+    e0.record(stream)
+    for _ in range(args.kernel_reps):
+        eng.estep()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    estep_ms = e0.elapsed_time(e1) / args.kernel_reps
+    e0.record(stream)
+    for _ in range(args.kernel_reps):
+        eng.mstep()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    mstep_ms = e0.elapsed_time(e1) / args.kernel_reps
+
+    P = N + 1
+    flops = estep_flops_per_trial_iter(n_tx, n_rx, T_d, M) * B
+    algo_bytes = estep_bytes_per_trial_iter(n_tx, n_rx, P, T_d) * B
+    achieved_tf = flops / (estep_ms * 1e-3) / 1e12
+    pmc = load_pmc_traffic(args.pmc)
+    traffic = None
+    if pmc and pmc.get("config") == args.config and pmc.get("trials") == B:
+        traffic = pmc.get("hbm_bytes_per_launch")
+
+    value = world * B * iters * args.steps / elapsed
+    line = {
+        "metric": "EM-iterations/sec (whole node) + NMSE@SNR; Nt=Nr=4, N_RIS=64, Tp=16 Td=256",
+        "value": value,
+        "unit": "EM-iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (Rayleigh channels, 16-QAM, uniform RIS phases, CN noise; numpy Generator)",
+        "config": {"workload": args.config, "n_tx": n_tx, "n_rx": n_rx, "N_RIS": N, "T_p": T_p,
+                   "T_d": T_d, "M": M, "trials_per_gpu": B, "em_iters": iters,
+                   "snr_db": args.snr, "estep": args.mode, "parallelism": f"trials-sharded x{world}"},
+        "nmse_mean": nmse_mean,
+        "nonhpd_trials": nonhpd,
+        "kernels_ms": {"estep": estep_ms, "mstep_build_plus_solve": mstep_ms},
+        "roofline": {"bound": "fp64", "pipe": "VALU (FP64 vector)", "kernel": "estep_kernel",
+                     "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "algorithmic_bytes": algo_bytes,
+                     "hbm_GBps_algorithmic": algo_bytes / (estep_ms * 1e-3) / 1e9,
+                     "hbm_frac_algorithmic": algo_bytes / (estep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "flops_per_launch": flops},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(cfg, varn, args.seed)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

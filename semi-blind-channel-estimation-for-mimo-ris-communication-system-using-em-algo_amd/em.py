@@ -271,3 +271,72 @@ def nmse_batch(theta, h):
     _lib.check(lib.sbce_nmse(dims, th.data_ptr(), hh.data_ptr(), out.data_ptr(),
                              torch.cuda.current_stream().cuda_stream), "sbce_nmse")
     return out
+
+
+class EMEngine:
+    """Pre-allocated device state for repeated batched EM runs (benchmark / sweeps).
+
+    All buffers (observations, phases, pilot regressors, theta, workspace) stay
+    resident in HBM; ``run()`` resets theta from theta0 with a device copy and
+    issues ONE sbce_em call on the current stream.  Nothing is allocated or
+    synchronised inside ``run()``.
+    """
+
+    def __init__(self, batch, varn, mode="soft", solve="chol", x_d_true=None, h_true=None):
+        torch = _torch()
+        self.torch = torch
+        self.lib = _lib.load()
+
+        def dev(x):
+            if x is None:
+                return None
+            if isinstance(x, torch.Tensor):
+                return x.to("cuda").contiguous()
+            return _dev(torch, x, np.complex128)
+
+        self.y_d, self.y_p = dev(batch["y_d"]), dev(batch["y_p"])
+        self.psi_d, self.u_p = dev(batch["psi_d"]), dev(batch["u_p"])
+        self.cons, self.theta0 = dev(batch["cons"]), dev(batch["theta0"])
+        self.h = dev(h_true if h_true is not None else batch.get("h"))
+        self.theta = self.theta0.clone()
+        B, T_d, n_rx = self.y_d.shape
+        T_p, P, L = self.y_p.shape[1], self.psi_d.shape[2], self.u_p.shape[2]
+        self.n_tx, self.n_rx, self.B, self.T_d, self.T_p, self.P = L // P, n_rx, B, T_d, T_p, P
+        self.M = self.cons.shape[0]
+        self.varn = float(varn)
+        self.dims = _lib.Dims(B, self.n_tx, n_rx, P, T_p, T_d, self.M, 0, self.varn)
+        self.ws = torch.empty(max(_lib.workspace_bytes(self.dims), 16), dtype=torch.uint8,
+                              device="cuda")
+        self.status = torch.zeros(B, dtype=torch.int32, device="cuda")
+        self.mode, self.solve = _MODES[mode], _SOLVES[solve]
+        self.x_d = dev(x_d_true)
+        self.mom = torch.zeros((B, T_d, self.n_tx + self.n_tx ** 2), dtype=torch.complex128,
+                               device="cuda")
+        self.ptrs = _lib.Ptrs(self.y_d.data_ptr(), self.y_p.data_ptr(), self.psi_d.data_ptr(),
+                              self.u_p.data_ptr(), self.cons.data_ptr(), self.theta.data_ptr(),
+                              None, None, None, None, self.status.data_ptr(), self.ws.data_ptr(),
+                              self.ws.numel())
+
+    def run(self, itera):
+        """One full EM (itera iterations) over the whole batch, stream-ordered."""
+        self.theta.copy_(self.theta0)
+        rc = self.lib.sbce_em(self.dims, self.ptrs, int(itera), self.mode, self.solve,
+                              self.torch.cuda.current_stream().cuda_stream)
+        _lib.check(rc, "sbce_em")
+        return self.theta
+
+    def estep(self):
+        """One E-step launch over the batch from the current theta (for kernel timing)."""
+        rc = self.lib.sbce_estep(self.dims, self.ptrs, self.mode, self.mom.data_ptr(),
+                                 self.torch.cuda.current_stream().cuda_stream)
+        _lib.check(rc, "sbce_estep")
+
+    def mstep(self):
+        """One M-step launch sequence from the last E-step moments (for kernel timing)."""
+        rc = self.lib.sbce_mstep(self.dims, self.ptrs, self.mom.data_ptr(), self.solve, None,
+                                 None, self.torch.cuda.current_stream().cuda_stream)
+        _lib.check(rc, "sbce_mstep")
+
+    def nmse(self):
+        """Per-trial NMSE of the current theta against h (device, sbce_nmse)."""
+        return nmse_batch(self.theta, self.h)

@@ -130,7 +130,7 @@ def test_estep_moments_vs_oracle(sbce, shape):
         assert np.array_equal(mh[i], mh0) and np.allclose(Sh[i], Sh0, rtol=0, atol=1e-13)
 
 
-@pytest.mark.parametrize("shape", [(2, 2, 8, 12, 40, 4), (4, 4, 16, 16, 40, 16),
+@pytest.mark.parametrize("shape", [(2, 2, 8, 12, 40, 4), (4, 4, 16, 16, 80, 16),
                                    (3, 3, 6, 10, 30, 4), (1, 2, 5, 6, 12, 16)])
 def test_mstep_normal_equations_and_solve_vs_oracle(sbce, shape):
     n_tx, n_rx, N, T_p, T_d, M = shape
@@ -150,8 +150,9 @@ def test_mstep_normal_equations_and_solve_vs_oracle(sbce, shape):
         assert rel(rhs[i], rhs0) < 1e-13
         th0 = mstep_solve(R0, rhs0)
         cond = np.linalg.cond(R0)
+        assert cond < 1e12, "test shape must be well posed"
         assert rel(th[i], th0) < max(1e-12, 1e-15 * cond), cond
-        assert status[i] == 0
+        assert status[i] == 0, cond
 
 
 def test_cfg1_shape_full_em_vs_oracle(sbce):
