@@ -1,0 +1,68 @@
+"""Monte-Carlo trial sharding across GPUs (one process per GPU, torch.distributed).
+
+The reference averages per-trial NMSE/LLF over Monte-Carlo trials
+("Proposed method/Proposed_method_NMSEvsTp.py":154-176; SNR/all_Detectors.py:362-395).
+Trials are independent, so they shard with NO data-path collective: rank g of G
+owns trials {i : i mod G == g} of every sweep point, runs them through one
+batched sbce_em call per point, and the only exchange is ONE all-reduce of the
+per-point accumulators [sum NMSE, trial count, sum LLF per iteration] at the
+end of the sweep (RCCL over xGMI with backend "nccl"; gloo in the CPU tests).
+
+Determinism: each rank sums its trials in ascending trial order; the all-reduce
+then adds G partial sums (order fixed by the backend), so 1/2/4/8-GPU results
+agree to a few ulp of the mean.
+"""
+import numpy as np
+
+
+def shard(n_trials, world, rank):
+    """Trial indices owned by `rank` (strided, so every rank sees every sweep region)."""
+    if not (0 <= rank < world):
+        raise ValueError("rank out of range")
+    return np.arange(rank, n_trials, world, dtype=np.int64)
+
+
+class Accumulators:
+    """Per-sweep-point sums, packed into one float64 vector for a single all-reduce."""
+
+    def __init__(self, n_points, n_iters=0):
+        self.n_points = n_points
+        self.n_iters = n_iters
+        self.nmse = np.zeros(n_points)
+        self.count = np.zeros(n_points)
+        self.llf = np.zeros((n_points, n_iters))
+
+    def add(self, point, nmse_values, llf_values=None):
+        v = np.sort(np.asarray(nmse_values, dtype=float).reshape(-1))   # order-independent
+        self.nmse[point] += float(np.sum(v))
+        self.count[point] += v.size
+        if llf_values is not None and self.n_iters:
+            self.llf[point] += np.sum(np.asarray(llf_values, dtype=float).reshape(-1, self.n_iters),
+                                      axis=0)
+
+    def pack(self):
+        return np.concatenate([self.nmse, self.count, self.llf.reshape(-1)])
+
+    def unpack(self, vec):
+        P, I = self.n_points, self.n_iters
+        self.nmse = vec[:P].copy()
+        self.count = vec[P:2 * P].copy()
+        self.llf = vec[2 * P:].reshape(P, I).copy()
+        return self
+
+    def allreduce(self, dist=None, device=None):
+        """ONE all-reduce(sum) of every accumulator (no-op when not distributed)."""
+        if dist is None or not dist.is_available() or not dist.is_initialized():
+            return self
+        import torch
+        t = torch.from_numpy(self.pack())
+        if device is not None:
+            t = t.to(device)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return self.unpack(t.cpu().numpy())
+
+    def mean_nmse(self):
+        return self.nmse / np.maximum(self.count, 1)
+
+    def mean_llf(self):
+        return self.llf / np.maximum(self.count, 1)[:, None]

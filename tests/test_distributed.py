@@ -1,0 +1,73 @@
+"""CPU tier: the multi-GPU path (trial sharding + one all-reduce of the NMSE/LLF
+accumulators) exercised with the gloo backend at world sizes 2 and 4.  Per-trial
+NMSE comes from the CPU oracle here (the GPU path is covered by -m gpu); what is
+under test is the partition and the reduction."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT, PKG
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _trial_nmse(sbce, trial, varn):
+    from oracle.em_reduced import em_reduced, nmse
+    b = sbce.signal_model.synthetic_batch(1, 2, 2, 4, 8, 12, 4, varn, seed=1000 + trial)
+    aps = sbce.qam.all_possible_symbols(b["cons"], 2)
+    th = em_reduced(b["y_d"][0], b["y_p"][0], b["u_p"][0], b["psi_d"][0].T, aps, varn, 2,
+                    b["theta0"][0])
+    return nmse(th, b["h"][0])
+
+
+def _worker(rank, world, port, n_trials, varns, out):
+    import importlib
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sbce = importlib.import_module(PKG)
+    acc = sbce.distributed.Accumulators(len(varns))
+    for pt, varn in enumerate(varns):
+        mine = sbce.distributed.shard(n_trials, world, rank)
+        acc.add(pt, [_trial_nmse(sbce, int(i), varn) for i in mine])
+    acc.allreduce(dist)
+    out[rank] = acc.pack().tolist()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_sweep_matches_single_process(sbce, world):
+    n_trials, varns = 7, [1.0, 0.1]
+    ref = sbce.distributed.Accumulators(len(varns))
+    for pt, varn in enumerate(varns):
+        ref.add(pt, [_trial_nmse(sbce, i, varn) for i in range(n_trials)])
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), n_trials, varns, out), nprocs=world, join=True)
+    for r in range(world):
+        got = sbce.distributed.Accumulators(len(varns)).unpack(np.array(out[r]))
+        assert np.array_equal(got.count, ref.count)
+        assert np.allclose(got.mean_nmse(), ref.mean_nmse(), rtol=1e-14, atol=0)
+
+
+def test_shard_partition_is_exact(sbce):
+    for n in (1, 7, 1000):
+        for world in (1, 2, 3, 8):
+            parts = [sbce.distributed.shard(n, world, r) for r in range(world)]
+            allidx = np.sort(np.concatenate(parts))
+            assert np.array_equal(allidx, np.arange(n))
+    with pytest.raises(ValueError):
+        sbce.distributed.shard(10, 2, 2)
