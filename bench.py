@@ -131,7 +131,7 @@ def main():
     # ---- synthetic inputs for this rank's trials, resident in HBM before timing ----
     batch = pkg.signal_model.synthetic_batch(B, n_tx, n_rx, N, T_p, T_d, M, varn,
                                              seed=args.seed * 1000003 + rank)
-    eng = pkg.em.EMEngine(batch, varn, mode=args.mode)
+    eng = pkg.EMEngine(batch, varn, mode=args.mode)
     torch.cuda.synchronize()
 
     def barrier():
