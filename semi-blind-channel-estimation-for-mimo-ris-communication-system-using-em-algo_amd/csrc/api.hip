@@ -90,7 +90,7 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     if (!make_problem(d, pb) || iters < 0) return SBCE_EINVAL;
     int rc = check_ptrs(p, pb, true);
     if (rc) return rc;
-    if (!estep_supported(pb, estep_mode)) return SBCE_EUNSUPPORTED;
+    if (!estep_supported(pb, estep_mode) || !chol_supported(pb)) return SBCE_EUNSUPPORTED;
     if (solve_mode != SBCE_SOLVE_CHOL && solve_mode != SBCE_SOLVE_CHOL_DROP) return SBCE_EINVAL;
     if (p->llf && !p->x_d_true) return SBCE_EINVAL;
     if (pb.B == 0 || iters == 0) return SBCE_OK;
@@ -155,6 +155,7 @@ int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int 
     int rc = check_ptrs(p, pb, true);
     if (rc) return rc;
     if (!moments) return SBCE_EINVAL;
+    if (!chol_supported(pb)) return SBCE_EUNSUPPORTED;
     if (pb.B == 0) return SBCE_OK;
     hipStream_t s = (hipStream_t)hip_stream;
     const Carve c = carve(pb);

@@ -1,0 +1,242 @@
+// Batched Hermitian solve of the reduced M-step system  R X = B^H  (one trial per
+// workgroup), replacing np.linalg.solve ("Proposed method/Proposed_method_NMSEvsTp.py":80,
+// LAPACK zgesv on the K x K system) by a Cholesky factorisation of the L x L
+// Hermitian R (commutation_matrix.py:3-8 identity, SURVEY.md §8 preamble).
+//
+// Design (gfx950): left-looking blocked Cholesky, panel width NB = 16, with the
+// panel REGISTER-resident: thread t owns panel rows t, t+nth, ... (RPT rows), so
+//   * the left-looking update  A[i, jb:jb+16] -= L[i, 0:jb] L[jb:jb+16, 0:jb]^H
+//     streams the thread's own row of L (contiguous) against a 16 x KC top block
+//     staged in LDS (broadcast reads);
+//   * the 16 x 16 diagonal block is factored by ONE wave in LDS (wave-level
+//     syncs only), which also forward-solves the 16-row block of y = L^{-1} B^H;
+//   * every other panel row does its own 16-wide triangular solve and its
+//     y update in registers (no barriers);
+// so a panel costs 2 barriers per KC-chunk of the update plus 3, instead of
+// 2 per column.  The back substitution L^H x = y is blocked by 16 the same way.
+// Pivots <= 1e-14 * max(diag R) are flagged (status bit 0); solve_mode DROP
+// zeroes that direction, CHOL clamps the pivot to the tolerance.
+#include "sbce_internal.h"
+
+namespace sbce {
+
+namespace {
+
+constexpr int NB = 16;   // panel width (columns)
+constexpr int KC = 32;   // k-chunk of the left-looking update
+
+template <int RPT, bool YLDS>
+__global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int NR) {
+    const int b = blockIdx.x;
+    if (a.done && a.done[b]) return;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cd* T = reinterpret_cast<cd*>(smem);        // [NB][KC]
+    cd* D = T + NB * KC;                        // [NB][NB]
+    double* dinv = reinterpret_cast<double*>(D + NB * NB);   // [NB]
+    double* red = dinv + NB;                    // [16] reduction scratch
+    int* flag = reinterpret_cast<int*>(red + 16);
+    cd* ylds = reinterpret_cast<cd*>(red + 18);  // [L][NR] when YLDS
+    cd* R = a.R + (size_t)b * L * L;
+    cd* y = YLDS ? ylds : a.rhs + (size_t)b * L * NR;
+    const int tid = threadIdx.x, nth = blockDim.x;
+    const int lane = tid & 63, wave = tid >> 6;
+
+    // ---- tolerance from max diag(R); y = B^H ----
+    double mx = 0.0;
+    for (int i = tid; i < L; i += nth) mx = fmax(mx, R[(size_t)i * L + i].x);
+    for (int off = 32; off >= 1; off >>= 1) mx = fmax(mx, shfl_xor_d(mx, off));
+    if (lane == 0) red[wave] = mx;
+    if (YLDS) {
+        const cd* rhs = a.rhs + (size_t)b * L * NR;
+        for (int e = tid; e < L * NR; e += nth) y[e] = rhs[e];
+    }
+    if (tid == 0) *flag = 0;
+    __syncthreads();
+    double tol = 0.0;
+    for (int w = 0; w < (nth >> 6); ++w) tol = fmax(tol, red[w]);
+    tol *= 1e-14;
+
+    // ================= factorisation + fused forward substitution =================
+    for (int jb = 0; jb < L; jb += NB) {
+        const int w = (L - jb) < NB ? (L - jb) : NB;
+        const int rows = L - jb;
+        cd row[RPT][NB];
+#pragma unroll
+        for (int s = 0; s < RPT; ++s) {
+            const int i = tid + s * nth;
+#pragma unroll
+            for (int c = 0; c < NB; ++c)
+                row[s][c] = (i < rows && c < w) ? R[(size_t)(jb + i) * L + jb + c] : czero();
+        }
+        // ---- left-looking update with the already factored columns 0..jb-1 ----
+        for (int k0 = 0; k0 < jb; k0 += KC) {
+            const int kc = (jb - k0) < KC ? (jb - k0) : KC;
+            __syncthreads();
+            for (int e = tid; e < NB * KC; e += nth) {
+                const int c = e / KC, k = e - c * KC;
+                T[e] = (c < w && k < kc) ? R[(size_t)(jb + c) * L + k0 + k] : czero();
+            }
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < RPT; ++s) {
+                const int i = tid + s * nth;
+                if (i < rows) {
+                    const cd* Li = R + (size_t)(jb + i) * L + k0;
+                    for (int k = 0; k < kc; ++k) {
+                        const cd lik = Li[k];
+#pragma unroll
+                        for (int c = 0; c < NB; ++c) {
+                            const cd t = T[c * KC + k];
+                            // row[c] -= lik * conj(t)
+                            row[s][c].x = fma(-lik.x, t.x, row[s][c].x);
+                            row[s][c].x = fma(-lik.y, t.y, row[s][c].x);
+                            row[s][c].y = fma(-lik.y, t.x, row[s][c].y);
+                            row[s][c].y = fma(lik.x, t.y, row[s][c].y);
+                        }
+                    }
+                }
+            }
+        }
+        // ---- diagonal block -> LDS, factored by wave 0 ----
+#pragma unroll
+        for (int s = 0; s < RPT; ++s) {
+            const int i = tid + s * nth;
+            if (i < w) {
+#pragma unroll
+                for (int c = 0; c < NB; ++c) D[i * NB + c] = row[s][c];
+            }
+        }
+        __syncthreads();
+        if (wave == 0) {
+            for (int c = 0; c < w; ++c) {
+                const double dia = D[c * NB + c].x;
+                const bool bad = !(dia > tol);
+                const bool drop = bad && a.solve_mode == SBCE_SOLVE_CHOL_DROP;
+                const double piv = sqrt(bad ? tol : dia);
+                const double inv = drop ? 0.0 : 1.0 / piv;
+                wave_sync();
+                if (lane == 0) {
+                    D[c * NB + c] = cmk(drop ? 0.0 : piv, 0.0);
+                    dinv[c] = inv;
+                    if (bad) *flag = 1;
+                }
+                const int r = c + 1 + lane;
+                if (r < w) D[r * NB + c] = cscale(D[r * NB + c], inv);
+                wave_sync();
+                // trailing 16x16 update: D[r][c2] -= D[r][c] conj(D[c2][c]),  c < c2 <= r < w
+                for (int e = lane; e < NB * NB; e += 64) {
+                    const int rr = e / NB, c2 = e - rr * NB;
+                    if (c2 > c && rr >= c2 && rr < w)
+                        D[e] = csub(D[e], cmulc(D[rr * NB + c], D[c2 * NB + c]));
+                }
+                wave_sync();
+            }
+            // forward-solve the y block: y_c = (y_c - sum_{c'<c} D[c][c'] y_c') * dinv[c]
+            if (lane < NR) {
+                for (int c = 0; c < w; ++c) {
+                    cd v = y[(jb + c) * NR + lane];
+                    for (int c2 = 0; c2 < c; ++c2) v = csub(v, cmul(D[c * NB + c2], y[(jb + c2) * NR + lane]));
+                    y[(jb + c) * NR + lane] = cscale(v, dinv[c]);
+                }
+            }
+        }
+        __syncthreads();
+        // ---- panel rows: TRSM against the factored diagonal block, y update, write-back ----
+#pragma unroll
+        for (int s = 0; s < RPT; ++s) {
+            const int i = tid + s * nth;
+            cd* dst = R + (size_t)(jb + i) * L + jb;
+            if (i < w) {
+                for (int c = 0; c <= i; ++c) dst[c] = D[i * NB + c];
+            } else if (i < rows) {
+#pragma unroll
+                for (int c = 0; c < NB; ++c) {
+                    if (c < w) {
+                        cd v = row[s][c];
+#pragma unroll
+                        for (int c2 = 0; c2 < NB; ++c2)
+                            if (c2 < c) v = csub(v, cmulc(row[s][c2], D[c * NB + c2]));
+                        row[s][c] = cscale(v, dinv[c]);
+                    }
+                }
+                for (int r = 0; r < NR; ++r) {
+                    cd acc = y[(jb + i) * NR + r];
+#pragma unroll
+                    for (int c = 0; c < NB; ++c)
+                        if (c < w) acc = csub(acc, cmul(row[s][c], y[(jb + c) * NR + r]));
+                    y[(jb + i) * NR + r] = acc;
+                }
+#pragma unroll
+                for (int c = 0; c < NB; ++c)
+                    if (c < w) dst[c] = row[s][c];
+            }
+        }
+        __syncthreads();
+    }
+
+    // ================= blocked back substitution  L^H x = y =================
+    const int nblk = (L + NB - 1) / NB;
+    for (int kb = nblk - 1; kb >= 0; --kb) {
+        const int k0 = kb * NB;
+        const int w = (L - k0) < NB ? (L - k0) : NB;
+        if (wave == 0) {
+            // x_c = (y_c - sum_{c'>c} conj(L[c'][c]) x_c') / L[c][c]
+            if (lane < NR) {
+                for (int c = w - 1; c >= 0; --c) {
+                    cd v = y[(k0 + c) * NR + lane];
+                    for (int c2 = c + 1; c2 < w; ++c2)
+                        v = csub(v, cmulc(y[(k0 + c2) * NR + lane], R[(size_t)(k0 + c2) * L + k0 + c]));
+                    const double lcc = R[(size_t)(k0 + c) * L + k0 + c].x;
+                    y[(k0 + c) * NR + lane] = (lcc > 0.0) ? cscale(v, 1.0 / lcc) : czero();
+                }
+            }
+        }
+        __syncthreads();
+        // y[k] -= sum_c conj(L[k0+c][k]) x[k0+c]   for k < k0
+        for (int e = tid; e < k0 * NR; e += nth) {
+            const int k = e / NR, r = e - k * NR;
+            cd acc = y[k * NR + r];
+#pragma unroll
+            for (int c = 0; c < NB; ++c)
+                if (c < w) acc = csub(acc, cmulc(y[(k0 + c) * NR + r], R[(size_t)(k0 + c) * L + k]));
+            y[k * NR + r] = acc;
+        }
+        __syncthreads();
+    }
+    cd* th = a.theta + (size_t)b * L * NR;
+    for (int e = tid; e < L * NR; e += nth) th[e] = cconj(y[e]);
+    if (tid == 0 && a.status) a.status[b] |= *flag ? SBCE_STATUS_NONHPD : 0;
+}
+
+template <int RPT, bool YLDS>
+hipError_t launch_rpt(const Problem& pb, const MstepArgs& a, int nth, size_t lds, hipStream_t s) {
+    hipLaunchKernelGGL((chol_solve_kernel<RPT, YLDS>), dim3(pb.B), dim3(nth), lds, s, a, pb.L, pb.NR);
+    return hipGetLastError();
+}
+
+template <bool YLDS>
+hipError_t launch_y(const Problem& pb, const MstepArgs& a, int nth, int rpt, size_t lds,
+                    hipStream_t s) {
+    switch (rpt) {
+        case 1: return launch_rpt<1, YLDS>(pb, a, nth, lds, s);
+        case 2: return launch_rpt<2, YLDS>(pb, a, nth, lds, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+bool chol_supported(const Problem& pb) { return pb.L >= 1 && pb.L <= 1024; }
+
+hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s) {
+    if (!chol_supported(pb)) return hipErrorInvalidValue;
+    int nth = (pb.L + 63) / 64 * 64;
+    if (nth > 512) nth = 512;
+    const int rpt = (pb.L + nth - 1) / nth;
+    const size_t base = (size_t)(NB * KC + NB * NB) * sizeof(cd) + (NB + 18) * sizeof(double);
+    const size_t ybytes = (size_t)pb.L * pb.NR * sizeof(cd);
+    if (ybytes <= 48 * 1024) return launch_y<true>(pb, a, nth, rpt, base + ybytes, s);
+    return launch_y<false>(pb, a, nth, rpt, base, s);
+}
+
+}  // namespace sbce

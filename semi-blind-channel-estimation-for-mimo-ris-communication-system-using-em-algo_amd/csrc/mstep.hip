@@ -103,126 +103,6 @@ __global__ __launch_bounds__(256) void rhs_kernel(MstepArgs a, int B, int P, int
     for (int r = 0; r < NR; ++r) rhs[r] = acc[r];
 }
 
-// ------------------------------------------------------------------ Cholesky + solve
-// One 256-thread workgroup per trial.  Left-looking blocked Cholesky R = L L^H
-// (lower, in place in R), block columns of NBC; the active panel (rows jb..L-1)
-// lives in LDS, the already factored columns are read from global memory (L2).
-// Then L y = B^H, L^H x = y with x in LDS, theta = conj(x) in reference order.
-constexpr int NBC = 16;
-
-__global__ __launch_bounds__(256) void chol_solve_kernel(MstepArgs a, int L, int NR) {
-    const int b = blockIdx.x;
-    if (a.done && a.done[b]) return;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    cd* panel = reinterpret_cast<cd*>(smem);                 // [L][NBC]
-    cd* x = panel + (size_t)L * NBC;                         // [L][NR]
-    double& s_tol = *reinterpret_cast<double*>(x + (size_t)L * NR);
-    int& s_flag = *reinterpret_cast<int*>(x + (size_t)L * NR + 1);
-    cd* R = a.R + (size_t)b * L * L;
-    const int tid = threadIdx.x;
-    const int nth = blockDim.x;
-
-    if (tid == 0) {
-        double mx = 0.0;
-        for (int i = 0; i < L; ++i) mx = fmax(mx, R[(size_t)i * L + i].x);
-        s_tol = mx * 1e-14;
-        s_flag = 0;
-    }
-    __syncthreads();
-    const double tol = s_tol;
-
-    for (int jb = 0; jb < L; jb += NBC) {
-        const int w = (L - jb) < NBC ? (L - jb) : NBC;
-        const int rows = L - jb;
-        // 1. load panel (lower part of columns jb..jb+w-1, rows jb..L-1)
-        for (int e = tid; e < rows * NBC; e += nth) {
-            const int i = e / NBC, cc = e - i * NBC;
-            panel[e] = (cc < w) ? R[(size_t)(jb + i) * L + jb + cc] : czero();
-        }
-        __syncthreads();
-        // 2. panel -= L[jb+i, 0:jb] * L[jb+c, 0:jb]^H   (left-looking update)
-        if (jb > 0) {
-            for (int i = tid; i < rows; i += nth) {
-                cd acc[NBC];
-#pragma unroll
-                for (int cc = 0; cc < NBC; ++cc) acc[cc] = czero();
-                const cd* Li = R + (size_t)(jb + i) * L;
-                for (int k = 0; k < jb; ++k) {
-                    const cd lik = Li[k];
-#pragma unroll
-                    for (int cc = 0; cc < NBC; ++cc) {
-                        if (cc < w && cc <= i) acc[cc] = cfmac(acc[cc], lik, R[(size_t)(jb + cc) * L + k]);
-                    }
-                }
-#pragma unroll
-                for (int cc = 0; cc < NBC; ++cc) panel[i * NBC + cc] = csub(panel[i * NBC + cc], acc[cc]);
-            }
-            __syncthreads();
-        }
-        // 3. factor the panel column by column (right-looking inside the panel)
-        for (int cc = 0; cc < w; ++cc) {
-            const double dia = panel[cc * NBC + cc].x;
-            double piv;
-            bool drop = false;
-            if (!(dia > tol)) {
-                if (tid == 0) s_flag = 1;
-                if (a.solve_mode == SBCE_SOLVE_CHOL_DROP) drop = true;
-                piv = sqrt(fmax(dia, tol));
-            } else {
-                piv = sqrt(dia);
-            }
-            const double inv = drop ? 0.0 : 1.0 / piv;
-            for (int i = cc + 1 + tid; i < rows; i += nth) panel[i * NBC + cc] = cscale(panel[i * NBC + cc], inv);
-            __syncthreads();
-            if (tid == 0) panel[cc * NBC + cc] = cmk(drop ? 0.0 : piv, 0.0);
-            const int ncol = w - cc - 1;
-            if (ncol > 0) {
-                for (int e = tid; e < rows * ncol; e += nth) {
-                    const int i = e / ncol, c2 = cc + 1 + (e - i * ncol);
-                    if (i >= c2) panel[i * NBC + c2] = csub(panel[i * NBC + c2],
-                                                            cmulc(panel[i * NBC + cc], panel[c2 * NBC + cc]));
-                }
-            }
-            __syncthreads();
-        }
-        // 4. write the factored panel back (lower part)
-        for (int e = tid; e < rows * NBC; e += nth) {
-            const int i = e / NBC, cc = e - i * NBC;
-            if (cc < w && i >= cc) R[(size_t)(jb + i) * L + jb + cc] = panel[e];
-        }
-        __syncthreads();
-    }
-
-    // ---- forward: L y = rhs ----
-    const cd* rhs = a.rhs + (size_t)b * L * NR;
-    for (int e = tid; e < L * NR; e += nth) x[e] = rhs[e];
-    __syncthreads();
-    for (int k = 0; k < L; ++k) {
-        const double lkk = R[(size_t)k * L + k].x;
-        if (tid < NR) x[k * NR + tid] = (lkk > 0.0) ? cscale(x[k * NR + tid], 1.0 / lkk) : czero();
-        __syncthreads();
-        for (int e = tid; e < (L - k - 1) * NR; e += nth) {
-            const int i = k + 1 + e / NR, r = e % NR;
-            x[i * NR + r] = csub(x[i * NR + r], cmul(R[(size_t)i * L + k], x[k * NR + r]));
-        }
-        __syncthreads();
-    }
-    // ---- backward: L^H x = y ----
-    for (int i = L - 1; i >= 0; --i) {
-        const double lii = R[(size_t)i * L + i].x;
-        if (tid < NR) x[i * NR + tid] = (lii > 0.0) ? cscale(x[i * NR + tid], 1.0 / lii) : czero();
-        __syncthreads();
-        for (int e = tid; e < i * NR; e += nth) {
-            const int k = e / NR, r = e % NR;
-            x[k * NR + r] = csub(x[k * NR + r], cmulc(x[i * NR + r], R[(size_t)i * L + k]));
-        }
-        __syncthreads();
-    }
-    cd* th = a.theta + (size_t)b * L * NR;
-    for (int e = tid; e < L * NR; e += nth) th[e] = cconj(x[e]);
-    if (tid == 0 && a.status) a.status[b] |= s_flag ? SBCE_STATUS_NONHPD : 0;
-}
-
 // ------------------------------------------------------------------ small per-trial kernels
 __device__ double block_sum(double v, double* sh) {
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
@@ -333,15 +213,6 @@ hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t
 #undef SBCE_RHS
         default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
-}
-
-size_t chol_lds_bytes(int L, int NR) { return ((size_t)L * NBC + (size_t)L * NR + 2) * sizeof(cd); }
-
-hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s) {
-    const size_t lds = chol_lds_bytes(pb.L, pb.NR);
-    if (lds > 150 * 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(chol_solve_kernel, dim3(pb.B), dim3(256), lds, s, a, pb.L, pb.NR);
     return hipGetLastError();
 }
 

@@ -110,6 +110,7 @@ hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStre
 bool estep_supported(const Problem& pb, int mode);
 hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s);
+bool chol_supported(const Problem& pb);
 hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* out,
                        hipStream_t s);
 hipError_t launch_llf(const Problem& pb, const cd* theta, const cd* yp, const cd* up,
