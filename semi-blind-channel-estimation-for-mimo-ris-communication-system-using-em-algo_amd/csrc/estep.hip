@@ -27,6 +27,8 @@
 // per lane is skipped when every lane's distances exceed m + 50*varn^2: each
 // skipped weight is < e^-50 = 2e-22 of the segment maximum (total < 1e-17
 // relative for J <= 2^24), far below float64 resolution of the sums.
+#include <stdlib.h>
+
 #include "sbce_internal.h"
 
 namespace sbce {
@@ -381,6 +383,363 @@ __global__ __launch_bounds__(256) void estep_kernel(EstepArgs a, EstepConst c) {
     }
 }
 
+// ============================================================================
+// MFMA variant (gfx950 FP64 matrix cores) for JA >= 16 and JB >= 16.
+//
+// One wave per symbol.  The hypothesis grid (i over A, k over B) is tiled in
+// 16 x 16 tiles; each tile's distances
+//     d_ik = (alpha_i + gamma_k) + sum_kk P'[i][kk] Q[kk][k],
+// with P' = (-2 Re p_i, -2 Im p_i) and Q = (Re q_k, Im q_k) (K = 2*NR padded to
+// a multiple of 4), come out of KPAD/4 chained v_mfma_f64_16x16x4f64 whose
+// accumulator is initialised with alpha_i + gamma_k.  Lane l owns column
+// k = 16*kt + (l & 15) and rows i = 16*t + (l >> 4) + 4*j (j < 4), so the
+// per-k posterior sums (c_k, mu_k) are per lane, exactly like the VALU kernel.
+// The VALU only does the running minimum, the skip test and (rarely, at high
+// SNR) the exp/accumulate work, in parallel with the matrix pipe.
+// P' lives in LDS in MFMA-operand order ([tile][step][64 lanes], conflict-free
+// ds_read_b64), 256 i-entries per chunk.
+// ============================================================================
+typedef double d4v __attribute__((ext_vector_type(4)));
+
+constexpr int kMfmaWaves = 2;
+constexpr int kChunk = 256;
+
+struct MfmaConst {
+    int B, Td, P, M, lm;
+    int JA, JB, chunk, nparts;
+    int tab_d;                 // per-wave LDS doubles
+    double inv_s2, thr_d;
+};
+
+template <int NT, int NR, int MODE>
+__global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst c) {
+    constexpr int NA = NT / 2;
+    constexpr int NB = NT - NA;
+    constexpr int NO = NT * NR;
+    constexpr int K2 = 2 * NR;
+    constexpr int STEPS = (K2 + 3) / 4;
+    constexpr int NPA = NA * (NA - 1) / 2;
+    constexpr int NPB = NB * (NB - 1) / 2;
+    static_assert(NA >= 1 && NA <= 2 && NB <= 2, "mfma E-step: 2 <= n_tx <= 4");
+
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cd* s_cons = reinterpret_cast<cd*>(smem);
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    double* wbase = reinterpret_cast<double*>(s_cons + 64) + (size_t)wave * c.tab_d;
+    cd* s_heff = reinterpret_cast<cd*>(wbase);                 // NO
+    double* s_al = wbase + 2 * NO;                             // chunk
+    double* s_tab = s_al + c.chunk;                            // chunk/16 * STEPS * 64
+
+    for (int i = threadIdx.x; i < c.M; i += blockDim.x) s_cons[i] = a.cons[i];
+    __syncthreads();
+
+    const long nsym = (long)c.B * c.Td;
+    long gsym = (long)blockIdx.x * kMfmaWaves + wave;
+    if (gsym >= nsym) return;
+    const int b = (int)(gsym / c.Td);
+    const int t = (int)(gsym - (long)b * c.Td);
+    if (a.done && a.done[b]) return;
+    const int mask = c.M - 1;
+
+    // ---------------- H_eff(t) ----------------
+    {
+        const cd* th = a.theta + (size_t)b * c.P * NO;
+        const cd* ps = a.psid + (size_t)gsym * c.P;
+        const int ntask = NO * c.nparts;
+        cd* part = reinterpret_cast<cd*>(s_tab);
+        if (lane < ntask) {
+            const int o = lane % NO, pp = lane / NO;
+            cd acc = czero();
+            for (int p = pp; p < c.P; p += c.nparts) acc = cfma(acc, ps[p], th[p * NO + o]);
+            part[lane] = acc;
+        }
+        wave_sync();
+        if (lane < NO) {
+            cd s2 = part[lane];
+            for (int pp = 1; pp < c.nparts; ++pp) s2 = cadd(s2, part[pp * NO + lane]);
+            s_heff[lane] = s2;
+        }
+        wave_sync();
+    }
+    const cd* H = s_heff;
+    const double inv_s2 = c.inv_s2;
+
+    // lane-level accumulators (see VALU kernel)
+    double mshift = INFINITY;
+    double tot_c = 0.0;
+    cd tot_muA[NA];
+    double nu[NA];
+    cd kap = czero();
+    cd tot_mB[NB];
+    double tot_nB[NB];
+    cd tot_kB = czero();
+    cd tot_X[NA][NB];
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+        tot_muA[q] = czero(); nu[q] = 0.0;
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) tot_X[q][bb] = czero();
+    }
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) { tot_mB[bb] = czero(); tot_nB[bb] = 0.0; }
+    double best_d = INFINITY;
+    int best_j = 0x7fffffff;
+
+    const int col = lane & 15;
+    const int rq = lane >> 4;
+    const int nktile = c.JB >> 4;
+    const int ntile_chunk = c.chunk >> 4;
+    bool table_ready = false;
+
+    for (int kt = 0; kt < nktile; ++kt) {
+        const int k = kt * 16 + col;
+        cd xb[NB];
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) xb[bb] = s_cons[(k >> (c.lm * (NB - 1 - bb))) & mask];
+        cd qv[NR];
+        double gam = 0.0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            cd acc = czero();
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb) acc = cfma(acc, H[(NA + bb) * NR + r], xb[bb]);
+            qv[r] = acc;
+            gam += cabs2(acc);
+        }
+        double bop[STEPS];
+#pragma unroll
+        for (int s = 0; s < STEPS; ++s) {
+            const int kk = 4 * s + rq;
+            double v = 0.0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                if (kk == 2 * r) v = qv[r].x;
+                if (kk == 2 * r + 1) v = qv[r].y;
+            }
+            bop[s] = v;
+        }
+        double ck = 0.0;
+        cd mu[NA];
+#pragma unroll
+        for (int q = 0; q < NA; ++q) mu[q] = czero();
+
+        for (int i0 = 0; i0 < c.JA; i0 += c.chunk) {
+            if (!table_ready) {
+                // ---- P' and alpha for entries i0 .. i0+chunk-1 ----
+                wave_sync();
+                cd y[NR];
+#pragma unroll
+                for (int r = 0; r < NR; ++r) y[r] = a.yd[(size_t)gsym * NR + r];
+                for (int e = lane; e < c.chunk; e += 64) {
+                    const int i = i0 + e;
+                    double al = 0.0;
+                    const int tt = e >> 4, ii = e & 15;
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) {
+                        cd pr = y[r];
+#pragma unroll
+                        for (int q = 0; q < NA; ++q) {
+                            const cd x = s_cons[(i >> (c.lm * (NA - 1 - q))) & mask];
+                            pr = csub(pr, cmul(H[q * NR + r], x));
+                        }
+                        al += cabs2(pr);
+                        const int kr = 2 * r, ki = 2 * r + 1;
+                        s_tab[(tt * STEPS + (kr >> 2)) * 64 + ((kr & 3) << 4) + ii] = -2.0 * pr.x;
+                        s_tab[(tt * STEPS + (ki >> 2)) * 64 + ((ki & 3) << 4) + ii] = -2.0 * pr.y;
+                    }
+#pragma unroll
+                    for (int kk = K2; kk < 4 * STEPS; ++kk)
+                        s_tab[(tt * STEPS + (kk >> 2)) * 64 + ((kk & 3) << 4) + ii] = 0.0;
+                    s_al[e] = al;
+                }
+                wave_sync();
+                table_ready = (c.JA == c.chunk);
+            }
+            for (int tt = 0; tt < ntile_chunk; ++tt) {
+                d4v acc;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = s_al[tt * 16 + rq + 4 * j] + gam;
+#pragma unroll
+                for (int s = 0; s < STEPS; ++s)
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(s_tab[(tt * STEPS + s) * 64 + lane],
+                                                              bop[s], acc, 0, 0, 0);
+                const int ibase = i0 + tt * 16 + rq;
+                if (MODE == SBCE_ESTEP_HARD) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int jj = (ibase + 4 * j) * c.JB + k;
+                        const double dv = acc[j];
+                        if (dv < best_d || (dv == best_d && jj < best_j)) { best_d = dv; best_j = jj; }
+                    }
+                    continue;
+                }
+                const double cm = fmin(fmin(acc[0], acc[1]), fmin(acc[2], acc[3]));
+                if (__any(cm < mshift)) {
+                    double mn = fmin(cm, mshift);
+                    for (int off = 32; off >= 1; off >>= 1) mn = fmin(mn, shfl_xor_d(mn, off));
+                    const double f = (mshift == INFINITY) ? 0.0 : fexp_neg((mn - mshift) * inv_s2);
+                    mshift = mn;
+                    tot_c *= f; ck *= f; kap = cscale(kap, f); tot_kB = cscale(tot_kB, f);
+#pragma unroll
+                    for (int q = 0; q < NA; ++q) {
+                        tot_muA[q] = cscale(tot_muA[q], f); nu[q] *= f; mu[q] = cscale(mu[q], f);
+#pragma unroll
+                        for (int bb = 0; bb < NB; ++bb) tot_X[q][bb] = cscale(tot_X[q][bb], f);
+                    }
+#pragma unroll
+                    for (int bb = 0; bb < NB; ++bb) { tot_mB[bb] = cscale(tot_mB[bb], f); tot_nB[bb] *= f; }
+                }
+                if (!__any(cm <= mshift + c.thr_d)) continue;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int i = ibase + 4 * j;
+                    const double w = fexp_neg((mshift - acc[j]) * inv_s2);
+                    cd xa[NA];
+#pragma unroll
+                    for (int q = 0; q < NA; ++q) xa[q] = s_cons[(i >> (c.lm * (NA - 1 - q))) & mask];
+                    ck += w;
+#pragma unroll
+                    for (int q = 0; q < NA; ++q) {
+                        mu[q] = caxpy(mu[q], w, xa[q]);
+                        nu[q] = fma(w, cabs2(xa[q]), nu[q]);
+                    }
+                    if (NPA) kap = caxpy(kap, w, cmulc(xa[0], xa[NA > 1 ? 1 : 0]));
+                }
+            }
+        }
+        if (MODE == SBCE_ESTEP_SOFT) {
+            tot_c += ck;
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb) {
+                tot_mB[bb] = caxpy(tot_mB[bb], ck, xb[bb]);
+                tot_nB[bb] = fma(ck, cabs2(xb[bb]), tot_nB[bb]);
+            }
+            if (NPB) tot_kB = caxpy(tot_kB, ck, cmulc(xb[0], xb[NB > 1 ? 1 : 0]));
+#pragma unroll
+            for (int q = 0; q < NA; ++q) {
+                tot_muA[q] = cadd(tot_muA[q], mu[q]);
+#pragma unroll
+                for (int bb = 0; bb < NB; ++bb) tot_X[q][bb] = cfmac(tot_X[q][bb], mu[q], xb[bb]);
+            }
+        }
+    }
+
+    constexpr int MS = NT + NT * NT;
+    cd* out = a.mom + (size_t)gsym * MS;
+    if (MODE == SBCE_ESTEP_HARD) {
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double od = shfl_xor_d(best_d, off);
+            const int oj = __shfl_xor(best_j, off);
+            if (od < best_d || (od == best_d && oj < best_j)) { best_d = od; best_j = oj; }
+        }
+        if (lane == 0) {
+            cd x[NT];
+#pragma unroll
+            for (int s2 = 0; s2 < NT; ++s2) x[s2] = s_cons[(best_j >> (c.lm * (NT - 1 - s2))) & mask];
+#pragma unroll
+            for (int s2 = 0; s2 < NT; ++s2) {
+                out[s2] = x[s2];
+#pragma unroll
+                for (int s3 = 0; s3 < NT; ++s3) out[NT + s2 * NT + s3] = cmulc(x[s2], x[s3]);
+            }
+        }
+        return;
+    }
+    tot_c = seg_sum(tot_c, 64);
+    kap = seg_sum(kap, 64);
+    tot_kB = seg_sum(tot_kB, 64);
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+        tot_muA[q] = seg_sum(tot_muA[q], 64);
+        nu[q] = seg_sum(nu[q], 64);
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) tot_X[q][bb] = seg_sum(tot_X[q][bb], 64);
+    }
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) { tot_mB[bb] = seg_sum(tot_mB[bb], 64); tot_nB[bb] = seg_sum(tot_nB[bb], 64); }
+    if (lane == 0) {
+        const double iz = 1.0 / tot_c;
+        cd m[NT];
+        cd Sm[NT][NT];
+#pragma unroll
+        for (int q = 0; q < NA; ++q) { m[q] = cscale(tot_muA[q], iz); Sm[q][q] = cmk(nu[q] * iz, 0.0); }
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) {
+            m[NA + bb] = cscale(tot_mB[bb], iz);
+            Sm[NA + bb][NA + bb] = cmk(tot_nB[bb] * iz, 0.0);
+        }
+        if (NPA) { Sm[0][NA > 1 ? 1 : 0] = cscale(kap, iz); Sm[NA > 1 ? 1 : 0][0] = cconj(cscale(kap, iz)); }
+        if (NPB) { Sm[NA][NT - 1] = cscale(tot_kB, iz); Sm[NT - 1][NA] = cconj(cscale(tot_kB, iz)); }
+#pragma unroll
+        for (int q = 0; q < NA; ++q)
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb) {
+                const cd v = cscale(tot_X[q][bb], iz);
+                Sm[q][NA + bb] = v;
+                Sm[NA + bb][q] = cconj(v);
+            }
+#pragma unroll
+        for (int s2 = 0; s2 < NT; ++s2) {
+            out[s2] = m[s2];
+#pragma unroll
+            for (int s3 = 0; s3 < NT; ++s3) out[NT + s2 * NT + s3] = Sm[s2][s3];
+        }
+    }
+}
+
+bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
+    if (pb.NT < 2 || pb.NT > 4 || pb.NR < 1 || pb.NR > 8) return false;
+    if (pb.M < 2 || pb.M > 64 || (pb.M & (pb.M - 1))) return false;
+    int lm = 0;
+    while ((1 << lm) < pb.M) ++lm;
+    const int NA = pb.NT / 2, NB = pb.NT - NA;
+    const long JA = 1L << (lm * NA), JB = 1L << (lm * NB);
+    if (JA < 16 || JB < 16 || JA * JB > (1L << 24)) return false;
+    c.B = pb.B; c.Td = pb.Td; c.P = pb.P; c.M = pb.M; c.lm = lm;
+    c.JA = (int)JA; c.JB = (int)JB;
+    c.chunk = (int)(JA < kChunk ? JA : kChunk);
+    const int NO = pb.NT * pb.NR;
+    c.nparts = NO <= 64 ? 64 / NO : 1;
+    const int steps = (2 * pb.NR + 3) / 4;
+    c.tab_d = 2 * NO + c.chunk + (c.chunk / 16) * steps * 64;
+    c.tab_d = (c.tab_d + 1) / 2 * 2;          // keep 16-B alignment per wave
+    c.inv_s2 = 1.0 / (pb.varn * pb.varn);
+    c.thr_d = kSkipThr * pb.varn * pb.varn;
+    lds = 64 * sizeof(cd) + (size_t)kMfmaWaves * c.tab_d * sizeof(double);
+    const long nsym = (long)pb.B * pb.Td;
+    blocks = (nsym + kMfmaWaves - 1) / kMfmaWaves;
+    return lds <= 160 * 1024;
+}
+
+template <int NT, int NR>
+hipError_t dispatch_mfma_mode(const MfmaConst& c, size_t lds, long blocks, const EstepArgs& a,
+                              int mode, hipStream_t s) {
+    if (mode == SBCE_ESTEP_HARD)
+        hipLaunchKernelGGL((estep_mfma_kernel<NT, NR, SBCE_ESTEP_HARD>), dim3((unsigned)blocks),
+                           dim3(64 * kMfmaWaves), lds, s, a, c);
+    else
+        hipLaunchKernelGGL((estep_mfma_kernel<NT, NR, SBCE_ESTEP_SOFT>), dim3((unsigned)blocks),
+                           dim3(64 * kMfmaWaves), lds, s, a, c);
+    return hipGetLastError();
+}
+
+template <int NT>
+hipError_t dispatch_mfma_nr(int NR, const MfmaConst& c, size_t lds, long blocks,
+                            const EstepArgs& a, int mode, hipStream_t s) {
+    switch (NR) {
+        case 1: return dispatch_mfma_mode<NT, 1>(c, lds, blocks, a, mode, s);
+        case 2: return dispatch_mfma_mode<NT, 2>(c, lds, blocks, a, mode, s);
+        case 3: return dispatch_mfma_mode<NT, 3>(c, lds, blocks, a, mode, s);
+        case 4: return dispatch_mfma_mode<NT, 4>(c, lds, blocks, a, mode, s);
+        case 5: return dispatch_mfma_mode<NT, 5>(c, lds, blocks, a, mode, s);
+        case 6: return dispatch_mfma_mode<NT, 6>(c, lds, blocks, a, mode, s);
+        case 7: return dispatch_mfma_mode<NT, 7>(c, lds, blocks, a, mode, s);
+        case 8: return dispatch_mfma_mode<NT, 8>(c, lds, blocks, a, mode, s);
+    }
+    return hipErrorInvalidValue;
+}
+
 struct Geometry {
     EstepConst c;
     int KP;
@@ -462,6 +821,19 @@ bool estep_supported(const Problem& pb, int mode) {
 }
 
 hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStream_t s) {
+    const char* impl = getenv("SBCE_ESTEP_IMPL");   // "valu" forces the VALU kernel (A/B runs)
+    const bool force_valu = impl && impl[0] == 'v';
+    MfmaConst mc;
+    size_t mlds;
+    long mblocks;
+    if (!force_valu && make_mfma(pb, mc, mlds, mblocks)) {
+        if (mblocks == 0) return hipSuccess;
+        switch (pb.NT) {
+            case 2: return dispatch_mfma_nr<2>(pb.NR, mc, mlds, mblocks, a, mode, s);
+            case 3: return dispatch_mfma_nr<3>(pb.NR, mc, mlds, mblocks, a, mode, s);
+            case 4: return dispatch_mfma_nr<4>(pb.NR, mc, mlds, mblocks, a, mode, s);
+        }
+    }
     Geometry g;
     if (!make_geometry(pb, g)) return hipErrorInvalidValue;
     if (g.blocks == 0) return hipSuccess;
