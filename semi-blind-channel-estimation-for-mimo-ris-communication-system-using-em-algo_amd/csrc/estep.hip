@@ -411,7 +411,7 @@ struct MfmaConst {
     double inv_s2, thr_d;
 };
 
-template <int NT, int NR, int MODE>
+template <int NT, int NR, int MODE, int TU>
 __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst c) {
     constexpr int NA = NT / 2;
     constexpr int NB = NT - NA;
@@ -556,25 +556,34 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
                 wave_sync();
                 table_ready = (c.JA == c.chunk);
             }
-            for (int tt = 0; tt < ntile_chunk; ++tt) {
-                d4v acc;
+            for (int tg = 0; tg < ntile_chunk; tg += TU) {
+                // TU independent 16x16 tiles in flight: STEPS*TU MFMAs per group
+                d4v acc[TU];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] = s_al[tt * 16 + rq + 4 * j] + gam;
+                for (int u = 0; u < TU; ++u)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[u][j] = s_al[(tg + u) * 16 + rq + 4 * j] + gam;
 #pragma unroll
                 for (int s = 0; s < STEPS; ++s)
-                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(s_tab[(tt * STEPS + s) * 64 + lane],
-                                                              bop[s], acc, 0, 0, 0);
-                const int ibase = i0 + tt * 16 + rq;
+#pragma unroll
+                    for (int u = 0; u < TU; ++u)
+                        acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                            s_tab[((tg + u) * STEPS + s) * 64 + lane], bop[s], acc[u], 0, 0, 0);
                 if (MODE == SBCE_ESTEP_HARD) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int jj = (ibase + 4 * j) * c.JB + k;
-                        const double dv = acc[j];
-                        if (dv < best_d || (dv == best_d && jj < best_j)) { best_d = dv; best_j = jj; }
-                    }
+                    for (int u = 0; u < TU; ++u)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int jj = (i0 + (tg + u) * 16 + rq + 4 * j) * c.JB + k;
+                            const double dv = acc[u][j];
+                            if (dv < best_d || (dv == best_d && jj < best_j)) { best_d = dv; best_j = jj; }
+                        }
                     continue;
                 }
-                const double cm = fmin(fmin(acc[0], acc[1]), fmin(acc[2], acc[3]));
+                double cm = fmin(fmin(acc[0][0], acc[0][1]), fmin(acc[0][2], acc[0][3]));
+#pragma unroll
+                for (int u = 1; u < TU; ++u)
+                    cm = fmin(cm, fmin(fmin(acc[u][0], acc[u][1]), fmin(acc[u][2], acc[u][3])));
                 if (__any(cm < mshift)) {
                     double mn = fmin(cm, mshift);
                     for (int off = 32; off >= 1; off >>= 1) mn = fmin(mn, shfl_xor_d(mn, off));
@@ -592,19 +601,24 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
                 }
                 if (!__any(cm <= mshift + c.thr_d)) continue;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int i = ibase + 4 * j;
-                    const double w = fexp_neg((mshift - acc[j]) * inv_s2);
-                    cd xa[NA];
+                for (int u = 0; u < TU; ++u) {
+                    const double cmu = fmin(fmin(acc[u][0], acc[u][1]), fmin(acc[u][2], acc[u][3]));
+                    if (!__any(cmu <= mshift + c.thr_d)) continue;
 #pragma unroll
-                    for (int q = 0; q < NA; ++q) xa[q] = s_cons[(i >> (c.lm * (NA - 1 - q))) & mask];
-                    ck += w;
+                    for (int j = 0; j < 4; ++j) {
+                        const int i = i0 + (tg + u) * 16 + rq + 4 * j;
+                        const double w = fexp_neg((mshift - acc[u][j]) * inv_s2);
+                        cd xa[NA];
 #pragma unroll
-                    for (int q = 0; q < NA; ++q) {
-                        mu[q] = caxpy(mu[q], w, xa[q]);
-                        nu[q] = fma(w, cabs2(xa[q]), nu[q]);
+                        for (int q = 0; q < NA; ++q) xa[q] = s_cons[(i >> (c.lm * (NA - 1 - q))) & mask];
+                        ck += w;
+#pragma unroll
+                        for (int q = 0; q < NA; ++q) {
+                            mu[q] = caxpy(mu[q], w, xa[q]);
+                            nu[q] = fma(w, cabs2(xa[q]), nu[q]);
+                        }
+                        if (NPA) kap = caxpy(kap, w, cmulc(xa[0], xa[NA > 1 ? 1 : 0]));
                     }
-                    if (NPA) kap = caxpy(kap, w, cmulc(xa[0], xa[NA > 1 ? 1 : 0]));
                 }
             }
         }
@@ -702,7 +716,8 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     const int NO = pb.NT * pb.NR;
     c.nparts = NO <= 64 ? 64 / NO : 1;
     const int steps = (2 * pb.NR + 3) / 4;
-    c.tab_d = 2 * NO + c.chunk + (c.chunk / 16) * steps * 64;
+    const int tab = (c.chunk / 16) * steps * 64;
+    c.tab_d = 2 * NO + c.chunk + (tab > 128 ? tab : 128);   // >= 64 cd of H_eff partials
     c.tab_d = (c.tab_d + 1) / 2 * 2;          // keep 16-B alignment per wave
     c.inv_s2 = 1.0 / (pb.varn * pb.varn);
     c.thr_d = kSkipThr * pb.varn * pb.varn;
@@ -715,12 +730,22 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
 template <int NT, int NR>
 hipError_t dispatch_mfma_mode(const MfmaConst& c, size_t lds, long blocks, const EstepArgs& a,
                               int mode, hipStream_t s) {
-    if (mode == SBCE_ESTEP_HARD)
-        hipLaunchKernelGGL((estep_mfma_kernel<NT, NR, SBCE_ESTEP_HARD>), dim3((unsigned)blocks),
-                           dim3(64 * kMfmaWaves), lds, s, a, c);
-    else
-        hipLaunchKernelGGL((estep_mfma_kernel<NT, NR, SBCE_ESTEP_SOFT>), dim3((unsigned)blocks),
-                           dim3(64 * kMfmaWaves), lds, s, a, c);
+    const bool tu4 = (c.chunk / 16) % 4 == 0;
+    if (mode == SBCE_ESTEP_HARD) {
+        if (tu4)
+            hipLaunchKernelGGL((estep_mfma_kernel<NT, NR, SBCE_ESTEP_HARD, 4>), dim3((unsigned)blocks),
+                               dim3(64 * kMfmaWaves), lds, s, a, c);
+        else
+            hipLaunchKernelGGL((estep_mfma_kernel<NT, NR, SBCE_ESTEP_HARD, 1>), dim3((unsigned)blocks),
+                               dim3(64 * kMfmaWaves), lds, s, a, c);
+    } else {
+        if (tu4)
+            hipLaunchKernelGGL((estep_mfma_kernel<NT, NR, SBCE_ESTEP_SOFT, 4>), dim3((unsigned)blocks),
+                               dim3(64 * kMfmaWaves), lds, s, a, c);
+        else
+            hipLaunchKernelGGL((estep_mfma_kernel<NT, NR, SBCE_ESTEP_SOFT, 1>), dim3((unsigned)blocks),
+                               dim3(64 * kMfmaWaves), lds, s, a, c);
+    }
     return hipGetLastError();
 }
 
