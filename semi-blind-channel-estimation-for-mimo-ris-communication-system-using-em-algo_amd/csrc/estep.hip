@@ -396,8 +396,9 @@ __global__ __launch_bounds__(256) void estep_kernel(EstepArgs a, EstepConst c) {
 // per-k posterior sums (c_k, mu_k) are per lane, exactly like the VALU kernel.
 // The VALU only does the running minimum, the skip test and (rarely, at high
 // SNR) the exp/accumulate work, in parallel with the matrix pipe.
-// P' lives in LDS in MFMA-operand order ([tile][step][64 lanes], conflict-free
-// ds_read_b64), 256 i-entries per chunk.
+// The A operand is assembled per tile from two small LDS tables, -2 p_i =
+// U_{s0} + V_{s1} (U_s = -2(y - h_0 x_s), V_s = 2 h_1 x_s, layout [kk][s]:
+// conflict-free ds_read_b64), and alpha_i = ||p_i||^2 is tabulated 256 at a time.
 // ============================================================================
 typedef double d4v __attribute__((ext_vector_type(4)));
 
@@ -429,7 +430,9 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
     double* wbase = reinterpret_cast<double*>(s_cons + 64) + (size_t)wave * c.tab_d;
     cd* s_heff = reinterpret_cast<cd*>(wbase);                 // NO
     double* s_al = wbase + 2 * NO;                             // chunk
-    double* s_tab = s_al + c.chunk;                            // chunk/16 * STEPS * 64
+    double* s_U = s_al + c.chunk;                              // [KPAD][M]
+    double* s_V = s_U + 4 * STEPS * c.M;                       // [KPAD][M]   (NA == 2)
+    double* s_tab = s_V + 4 * STEPS * c.M;                     // scratch: 64 cd
 
     for (int i = threadIdx.x; i < c.M; i += blockDim.x) s_cons[i] = a.cons[i];
     __syncthreads();
@@ -486,6 +489,29 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
     double best_d = INFINITY;
     int best_j = 0x7fffffff;
 
+    // U_s = -2 (y - h_0 x_s),  V_s = 2 h_1 x_s  so that  -2 p_i = U_{s0(i)} + V_{s1(i)}
+    // (NA == 1: -2 p_i = U_{i}).  Layout [kk][s]: conflict-free per-lane reads.
+    {
+        wave_sync();
+        for (int e = lane; e < c.M * 4 * STEPS; e += 64) {
+            const int kk = e / c.M, sx = e - kk * c.M;
+            double u = 0.0, v = 0.0;
+            if (kk < K2) {
+                const int r = kk >> 1;
+                const cd x = s_cons[sx];
+                const cd yv = a.yd[(size_t)gsym * NR + r];
+                const cd pu = csub(yv, cmul(H[0 * NR + r], x));
+                u = -2.0 * ((kk & 1) ? pu.y : pu.x);
+                if (NA == 2) {
+                    const cd hv = cmul(H[1 * NR + r], x);
+                    v = 2.0 * ((kk & 1) ? hv.y : hv.x);
+                }
+            }
+            s_U[e] = u;
+            if (NA == 2) s_V[e] = v;
+        }
+        wave_sync();
+    }
     const int col = lane & 15;
     const int rq = lane >> 4;
     const int nktile = c.JB >> 4;
@@ -526,32 +552,20 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
 
         for (int i0 = 0; i0 < c.JA; i0 += c.chunk) {
             if (!table_ready) {
-                // ---- P' and alpha for entries i0 .. i0+chunk-1 ----
+                // ---- alpha_i = ||p_i||^2 for entries i0 .. i0+chunk-1 from U, V ----
                 wave_sync();
-                cd y[NR];
-#pragma unroll
-                for (int r = 0; r < NR; ++r) y[r] = a.yd[(size_t)gsym * NR + r];
                 for (int e = lane; e < c.chunk; e += 64) {
                     const int i = i0 + e;
+                    const int su = (NA == 2) ? (i >> c.lm) : i;
+                    const int sv = i & mask;
                     double al = 0.0;
-                    const int tt = e >> 4, ii = e & 15;
 #pragma unroll
-                    for (int r = 0; r < NR; ++r) {
-                        cd pr = y[r];
-#pragma unroll
-                        for (int q = 0; q < NA; ++q) {
-                            const cd x = s_cons[(i >> (c.lm * (NA - 1 - q))) & mask];
-                            pr = csub(pr, cmul(H[q * NR + r], x));
-                        }
-                        al += cabs2(pr);
-                        const int kr = 2 * r, ki = 2 * r + 1;
-                        s_tab[(tt * STEPS + (kr >> 2)) * 64 + ((kr & 3) << 4) + ii] = -2.0 * pr.x;
-                        s_tab[(tt * STEPS + (ki >> 2)) * 64 + ((ki & 3) << 4) + ii] = -2.0 * pr.y;
+                    for (int kk = 0; kk < K2; ++kk) {
+                        double v = s_U[kk * c.M + su];
+                        if (NA == 2) v += s_V[kk * c.M + sv];
+                        al = fma(v, v, al);
                     }
-#pragma unroll
-                    for (int kk = K2; kk < 4 * STEPS; ++kk)
-                        s_tab[(tt * STEPS + (kk >> 2)) * 64 + ((kk & 3) << 4) + ii] = 0.0;
-                    s_al[e] = al;
+                    s_al[e] = 0.25 * al;
                 }
                 wave_sync();
                 table_ready = (c.JA == c.chunk);
@@ -566,9 +580,13 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
 #pragma unroll
                 for (int s = 0; s < STEPS; ++s)
 #pragma unroll
-                    for (int u = 0; u < TU; ++u)
-                        acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(
-                            s_tab[((tg + u) * STEPS + s) * 64 + lane], bop[s], acc[u], 0, 0, 0);
+                    for (int u = 0; u < TU; ++u) {
+                        const int ia = i0 + (tg + u) * 16 + col;          // A-operand row
+                        const int kk = 4 * s + rq;
+                        double av = s_U[kk * c.M + ((NA == 2) ? (ia >> c.lm) : ia)];
+                        if (NA == 2) av += s_V[kk * c.M + (ia & mask)];
+                        acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bop[s], acc[u], 0, 0, 0);
+                    }
                 if (MODE == SBCE_ESTEP_HARD) {
 #pragma unroll
                     for (int u = 0; u < TU; ++u)
@@ -716,8 +734,7 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     const int NO = pb.NT * pb.NR;
     c.nparts = NO <= 64 ? 64 / NO : 1;
     const int steps = (2 * pb.NR + 3) / 4;
-    const int tab = (c.chunk / 16) * steps * 64;
-    c.tab_d = 2 * NO + c.chunk + (tab > 128 ? tab : 128);   // >= 64 cd of H_eff partials
+    c.tab_d = 2 * NO + c.chunk + 2 * (4 * steps) * pb.M + 128;   // heff|alpha|U|V|64-cd scratch
     c.tab_d = (c.tab_d + 1) / 2 * 2;          // keep 16-B alignment per wave
     c.inv_s2 = 1.0 / (pb.varn * pb.varn);
     c.thr_d = kSkipThr * pb.varn * pb.varn;
