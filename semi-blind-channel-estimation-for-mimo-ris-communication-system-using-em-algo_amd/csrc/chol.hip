@@ -180,13 +180,19 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
         const int k0 = kb * NB;
         const int w = (L - k0) < NB ? (L - k0) : NB;
         if (wave == 0) {
+            // stage the 16x16 diagonal block of L in LDS (one coalesced pass), then
             // x_c = (y_c - sum_{c'>c} conj(L[c'][c]) x_c') / L[c][c]
+            for (int e = lane; e < NB * NB; e += 64) {
+                const int r2 = e / NB, c2 = e - r2 * NB;
+                D[e] = (r2 < w && c2 <= r2) ? R[(size_t)(k0 + r2) * L + k0 + c2] : czero();
+            }
+            wave_sync();
             if (lane < NR) {
                 for (int c = w - 1; c >= 0; --c) {
                     cd v = y[(k0 + c) * NR + lane];
                     for (int c2 = c + 1; c2 < w; ++c2)
-                        v = csub(v, cmulc(y[(k0 + c2) * NR + lane], R[(size_t)(k0 + c2) * L + k0 + c]));
-                    const double lcc = R[(size_t)(k0 + c) * L + k0 + c].x;
+                        v = csub(v, cmulc(y[(k0 + c2) * NR + lane], D[c2 * NB + c]));
+                    const double lcc = D[c * NB + c].x;
                     y[(k0 + c) * NR + lane] = (lcc > 0.0) ? cscale(v, 1.0 / lcc) : czero();
                 }
             }
