@@ -82,16 +82,22 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
                 const int i = tid + s * nth;
                 if (i < rows) {
                     const cd* Li = R + (size_t)(jb + i) * L + k0;
-                    for (int k = 0; k < kc; ++k) {
-                        const cd lik = Li[k];
+                    // fixed 8-wide k sub-chunks: 8 row loads in flight, then 16 x 8 cMACs
+                    for (int kk = 0; kk < kc; kk += 8) {
+                        cd lik[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) lik[u] = (kk + u < kc) ? Li[kk + u] : czero();
 #pragma unroll
                         for (int c = 0; c < NB; ++c) {
-                            const cd t = T[c * KC + k];
-                            // row[c] -= lik * conj(t)
-                            row[s][c].x = fma(-lik.x, t.x, row[s][c].x);
-                            row[s][c].x = fma(-lik.y, t.y, row[s][c].x);
-                            row[s][c].y = fma(-lik.y, t.x, row[s][c].y);
-                            row[s][c].y = fma(lik.x, t.y, row[s][c].y);
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) {
+                                const cd t = T[c * KC + kk + u];   // zero-padded past kc
+                                // row[c] -= lik * conj(t)
+                                row[s][c].x = fma(-lik[u].x, t.x, row[s][c].x);
+                                row[s][c].x = fma(-lik[u].y, t.y, row[s][c].x);
+                                row[s][c].y = fma(-lik[u].y, t.x, row[s][c].y);
+                                row[s][c].y = fma(lik[u].x, t.y, row[s][c].y);
+                            }
                         }
                     }
                 }
