@@ -16,6 +16,8 @@
 // 2 per column.  The back substitution L^H x = y is blocked by 16 the same way.
 // Pivots <= 1e-14 * max(diag R) are flagged (status bit 0); solve_mode DROP
 // zeroes that direction, CHOL clamps the pivot to the tolerance.
+#include <stdlib.h>
+
 #include "sbce_internal.h"
 
 namespace sbce {
@@ -26,7 +28,9 @@ constexpr int NB = 16;   // panel width (columns)
 constexpr int KC = 32;   // k-chunk of the left-looking update
 
 template <int RPT, bool YLDS>
-__global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int NR) {
+__global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int NR, int skip) {
+    // skip: DIAGNOSTIC phase mask (timing only, results invalid): 1 update, 2 diag factor,
+    // 4 forward y, 8 trsm rows, 16 back substitution
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -69,7 +73,7 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
                 row[s][c] = (i < rows && c < w) ? R[(size_t)(jb + i) * L + jb + c] : czero();
         }
         // ---- left-looking update with the already factored columns 0..jb-1 ----
-        for (int k0 = 0; k0 < jb; k0 += KC) {
+        for (int k0 = 0; k0 < ((skip & 1) ? 0 : jb); k0 += KC) {
             const int kc = (jb - k0) < KC ? (jb - k0) : KC;
             __syncthreads();
             for (int e = tid; e < NB * KC; e += nth) {
@@ -113,7 +117,7 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
             }
         }
         __syncthreads();
-        if (wave == 0) {
+        if (wave == 0 && !(skip & 2)) {
             for (int c = 0; c < w; ++c) {
                 const double dia = D[c * NB + c].x;
                 const bool bad = !(dia > tol);
@@ -137,6 +141,8 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
                 }
                 wave_sync();
             }
+        }
+        if (wave == 0 && !(skip & 4)) {
             // forward-solve the y block: y_c = (y_c - sum_{c'<c} D[c][c'] y_c') * dinv[c]
             if (lane < NR) {
                 for (int c = 0; c < w; ++c) {
@@ -154,7 +160,7 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
             cd* dst = R + (size_t)(jb + i) * L + jb;
             if (i < w) {
                 for (int c = 0; c <= i; ++c) dst[c] = D[i * NB + c];
-            } else if (i < rows) {
+            } else if (i < rows && !(skip & 8)) {
 #pragma unroll
                 for (int c = 0; c < NB; ++c) {
                     if (c < w) {
@@ -182,7 +188,7 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
 
     // ================= blocked back substitution  L^H x = y =================
     const int nblk = (L + NB - 1) / NB;
-    for (int kb = nblk - 1; kb >= 0; --kb) {
+    for (int kb = nblk - 1; kb >= ((skip & 16) ? nblk : 0); --kb) {
         const int k0 = kb * NB;
         const int w = (L - k0) < NB ? (L - k0) : NB;
         if (wave == 0) {
@@ -222,7 +228,10 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
 
 template <int RPT, bool YLDS>
 hipError_t launch_rpt(const Problem& pb, const MstepArgs& a, int nth, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((chol_solve_kernel<RPT, YLDS>), dim3(pb.B), dim3(nth), lds, s, a, pb.L, pb.NR);
+    const char* sk = getenv("SBCE_CHOL_SKIP");      // diagnostic only (see kernel)
+    const int skip = sk ? atoi(sk) : 0;
+    hipLaunchKernelGGL((chol_solve_kernel<RPT, YLDS>), dim3(pb.B), dim3(nth), lds, s, a, pb.L, pb.NR,
+                       skip);
     return hipGetLastError();
 }
 

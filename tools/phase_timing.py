@@ -1,0 +1,36 @@
+"""Diagnostic: time the M-step Cholesky with phases disabled (SBCE_CHOL_SKIP bitmask,
+results invalid) and the E-step per SNR, on cfg1 shapes.  Not part of the product."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import __graft_entry__ as ge  # noqa: E402
+
+pkg = ge.package()
+B = int(os.environ.get("B", "1000"))
+varn = float(pkg.signal_model.snr_to_varn(20.0))
+batch = pkg.signal_model.synthetic_batch(B, 4, 4, 64, 16, 256, 16, varn, seed=0)
+eng = pkg.EMEngine(batch, varn)
+eng.run(2)
+eng.estep()
+torch.cuda.synchronize()
+
+
+def timeit(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+for skip in (0, 1, 2, 4, 8, 16, 2 | 4 | 16, 31):
+    os.environ["SBCE_CHOL_SKIP"] = str(skip)
+    print(f"chol skip={skip:2d}: mstep {timeit(eng.mstep):.3f} ms", flush=True)
+os.environ["SBCE_CHOL_SKIP"] = "0"
