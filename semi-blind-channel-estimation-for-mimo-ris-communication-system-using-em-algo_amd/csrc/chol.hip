@@ -35,8 +35,9 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
     if (a.done && a.done[b]) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     cd* T = reinterpret_cast<cd*>(smem);        // [NB][KC]
-    cd* D = T + NB * KC;                        // [NB][NB]
-    double* dinv = reinterpret_cast<double*>(D + NB * NB);   // [NB]
+    cd* D = T + NB * KC;                        // [NB][NB] factored diagonal block
+    cd* Di = D + NB * NB;                       // [NB][NB] its inverse (lower)
+    double* dinv = reinterpret_cast<double*>(Di + NB * NB);   // [NB]
     double* red = dinv + NB;                    // [16] reduction scratch
     int* flag = reinterpret_cast<int*>(red + 16);
     cd* ylds = reinterpret_cast<cd*>(red + 18);  // [L][NR] when YLDS
@@ -107,53 +108,73 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
                 }
             }
         }
-        // ---- diagonal block -> LDS, factored by wave 0 ----
-#pragma unroll
-        for (int s = 0; s < RPT; ++s) {
-            const int i = tid + s * nth;
-            if (i < w) {
-#pragma unroll
-                for (int c = 0; c < NB; ++c) D[i * NB + c] = row[s][c];
-            }
-        }
-        __syncthreads();
+        // ---- diagonal block: factored in wave-0 REGISTERS (lane r < w holds row r, in place) ----
         if (wave == 0 && !(skip & 2)) {
-            for (int c = 0; c < w; ++c) {
-                const double dia = D[c * NB + c].x;
-                const bool bad = !(dia > tol);
-                const bool drop = bad && a.solve_mode == SBCE_SOLVE_CHOL_DROP;
-                const double piv = sqrt(bad ? tol : dia);
-                const double inv = drop ? 0.0 : 1.0 / piv;
-                wave_sync();
-                if (lane == 0) {
-                    D[c * NB + c] = cmk(drop ? 0.0 : piv, 0.0);
-                    dinv[c] = inv;
-                    if (bad) *flag = 1;
+            cd* dr = row[0];
+            const bool mine = lane < w;
+            cd* colbuf = Di;      // scratch until the inverse is built
+#pragma unroll
+            for (int c = 0; c < NB; ++c) {
+                if (c < w) {
+                    if (lane == c) colbuf[NB] = dr[c];
+                    wave_sync();
+                    const double dia = colbuf[NB].x;
+                    const bool bad = !(dia > tol);
+                    const bool drop = bad && a.solve_mode == SBCE_SOLVE_CHOL_DROP;
+                    const double piv = sqrt(bad ? tol : dia);
+                    const double inv = drop ? 0.0 : 1.0 / piv;
+                    if (lane == 0) { dinv[c] = inv; if (bad) *flag = 1; }
+                    if (lane == c) dr[c] = cmk(drop ? 0.0 : piv, 0.0);
+                    else if (mine && lane > c) dr[c] = cscale(dr[c], inv);
+                    if (mine && lane > c) colbuf[lane] = dr[c];
+                    wave_sync();
+#pragma unroll
+                    for (int c2 = c + 1; c2 < NB; ++c2) {
+                        if (c2 < w && mine && lane >= c2) dr[c2] = csub(dr[c2], cmulc(dr[c], colbuf[c2]));
+                        if ((c2 & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // bound load hoisting
+                    }
+                    wave_sync();
                 }
-                const int r = c + 1 + lane;
-                if (r < w) D[r * NB + c] = cscale(D[r * NB + c], inv);
-                wave_sync();
-                // trailing 16x16 update: D[r][c2] -= D[r][c] conj(D[c2][c]),  c < c2 <= r < w
-                for (int e = lane; e < NB * NB; e += 64) {
-                    const int rr = e / NB, c2 = e - rr * NB;
-                    if (c2 > c && rr >= c2 && rr < w)
-                        D[e] = csub(D[e], cmulc(D[rr * NB + c], D[c2 * NB + c]));
+            }
+            if (lane < NB) {
+#pragma unroll
+                for (int c = 0; c < NB; ++c) D[lane * NB + c] = (c <= lane && mine) ? dr[c] : czero();
+            }
+            wave_sync();
+            // Di = D^{-1}: lane j < w builds column j by forward substitution in LDS
+            if (lane < NB) {
+                const int j = lane;
+                for (int i = 0; i < NB; ++i) {
+                    cd acc = (i == j) ? cmk(1.0, 0.0) : czero();
+                    for (int k = j; k < i; ++k) acc = csub(acc, cmul(D[i * NB + k], Di[k * NB + j]));
+                    Di[i * NB + j] = (i >= j && i < w && j < w) ? cscale(acc, dinv[i]) : czero();
                 }
-                wave_sync();
+            }
+            wave_sync();
+            // conj(Di[c2][c]) (c2 > c) -> R's unused strict upper diagonal block (back substitution)
+            for (int e = lane; e < NB * NB; e += 64) {
+                const int c = e / NB, c2 = e - c * NB;
+                if (c2 > c && c2 < w) R[(size_t)(jb + c) * L + jb + c2] = cconj(Di[c2 * NB + c]);
             }
         }
         if (wave == 0 && !(skip & 4)) {
-            // forward-solve the y block: y_c = (y_c - sum_{c'<c} D[c][c'] y_c') * dinv[c]
-            if (lane < NR) {
-                for (int c = 0; c < w; ++c) {
-                    cd v = y[(jb + c) * NR + lane];
-                    for (int c2 = 0; c2 < c; ++c2) v = csub(v, cmul(D[c * NB + c2], y[(jb + c2) * NR + lane]));
-                    y[(jb + c) * NR + lane] = cscale(v, dinv[c]);
-                }
+            // forward-solve the y block in parallel: y_blk <- Di y_blk  (w*NR <= 128 outputs)
+            const int e0 = lane, e1 = lane + 64;
+            cd t0 = czero(), t1 = czero();
+            if (e0 < w * NR) {
+                const int c = e0 / NR, r = e0 - c * NR;
+                for (int c2 = 0; c2 <= c; ++c2) t0 = cfma(t0, Di[c * NB + c2], y[(jb + c2) * NR + r]);
             }
+            if (e1 < w * NR) {
+                const int c = e1 / NR, r = e1 - c * NR;
+                for (int c2 = 0; c2 <= c; ++c2) t1 = cfma(t1, Di[c * NB + c2], y[(jb + c2) * NR + r]);
+            }
+            wave_sync();
+            if (e0 < w * NR) y[jb * NR + e0] = t0;
+            if (e1 < w * NR) y[jb * NR + e1] = t1;
         }
         __syncthreads();
-        // ---- panel rows: TRSM against the factored diagonal block, y update, write-back ----
+        // ---- panel rows: TRSM L_i = A_i D^{-H} (independent FMAs), y update, write-back ----
 #pragma unroll
         for (int s = 0; s < RPT; ++s) {
             const int i = tid + s * nth;
@@ -161,26 +182,25 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
             if (i < w) {
                 for (int c = 0; c <= i; ++c) dst[c] = D[i * NB + c];
             } else if (i < rows && !(skip & 8)) {
+                // in place, highest column first (row[c2 < c] still holds A_i)
+                cd* xr = row[s];
 #pragma unroll
-                for (int c = 0; c < NB; ++c) {
-                    if (c < w) {
-                        cd v = row[s][c];
+                for (int c = NB - 1; c >= 0; --c) {
+                    cd v = czero();
 #pragma unroll
-                        for (int c2 = 0; c2 < NB; ++c2)
-                            if (c2 < c) v = csub(v, cmulc(row[s][c2], D[c * NB + c2]));
-                        row[s][c] = cscale(v, dinv[c]);
-                    }
+                    for (int c2 = 0; c2 <= c; ++c2) v = cfmac(v, row[s][c2], Di[c * NB + c2]);
+                    xr[c] = v;
                 }
                 for (int r = 0; r < NR; ++r) {
                     cd acc = y[(jb + i) * NR + r];
 #pragma unroll
                     for (int c = 0; c < NB; ++c)
-                        if (c < w) acc = csub(acc, cmul(row[s][c], y[(jb + c) * NR + r]));
+                        if (c < w) acc = csub(acc, cmul(xr[c], y[(jb + c) * NR + r]));
                     y[(jb + i) * NR + r] = acc;
                 }
 #pragma unroll
                 for (int c = 0; c < NB; ++c)
-                    if (c < w) dst[c] = row[s][c];
+                    if (c < w) dst[c] = xr[c];
             }
         }
         __syncthreads();
@@ -192,22 +212,25 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
         const int k0 = kb * NB;
         const int w = (L - k0) < NB ? (L - k0) : NB;
         if (wave == 0) {
-            // stage the 16x16 diagonal block of L in LDS (one coalesced pass), then
-            // x_c = (y_c - sum_{c'>c} conj(L[c'][c]) x_c') / L[c][c]
-            for (int e = lane; e < NB * NB; e += 64) {
-                const int r2 = e / NB, c2 = e - r2 * NB;
-                D[e] = (r2 < w && c2 <= r2) ? R[(size_t)(k0 + r2) * L + k0 + c2] : czero();
-            }
-            wave_sync();
-            if (lane < NR) {
-                for (int c = w - 1; c >= 0; --c) {
-                    cd v = y[(k0 + c) * NR + lane];
-                    for (int c2 = c + 1; c2 < w; ++c2)
-                        v = csub(v, cmulc(y[(k0 + c2) * NR + lane], D[c2 * NB + c]));
-                    const double lcc = D[c * NB + c].x;
-                    y[(k0 + c) * NR + lane] = (lcc > 0.0) ? cscale(v, 1.0 / lcc) : czero();
+            // x_blk = D^{-H} z_blk:  x[c] = z[c] / L[c][c] + sum_{c2>c} conj(Di[c2][c]) z[c2]
+            // (conj(Di[c2][c]) kept in R's strict upper diagonal block); w*NR <= 128 outputs
+            const int e0 = lane, e1 = lane + 64;
+            cd t0 = czero(), t1 = czero();
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int e = h ? e1 : e0;
+                if (e < w * NR) {
+                    const int c = e / NR, r = e - c * NR;
+                    const cd* Rc = R + (size_t)(k0 + c) * L + k0;
+                    const double lcc = Rc[c].x;
+                    cd acc = (lcc > 0.0) ? cscale(y[(k0 + c) * NR + r], 1.0 / lcc) : czero();
+                    for (int c2 = c + 1; c2 < w; ++c2) acc = cfma(acc, Rc[c2], y[(k0 + c2) * NR + r]);
+                    if (h) t1 = acc; else t0 = acc;
                 }
             }
+            wave_sync();
+            if (e0 < w * NR) y[k0 * NR + e0] = t0;
+            if (e1 < w * NR) y[k0 * NR + e1] = t1;
         }
         __syncthreads();
         // y[k] -= sum_c conj(L[k0+c][k]) x[k0+c]   for k < k0
@@ -254,7 +277,7 @@ hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t 
     int nth = (pb.L + 63) / 64 * 64;
     if (nth > 512) nth = 512;
     const int rpt = (pb.L + nth - 1) / nth;
-    const size_t base = (size_t)(NB * KC + NB * NB) * sizeof(cd) + (NB + 18) * sizeof(double);
+    const size_t base = (size_t)(NB * KC + 2 * NB * NB) * sizeof(cd) + (NB + 18) * sizeof(double);
     const size_t ybytes = (size_t)pb.L * pb.NR * sizeof(cd);
     if (ybytes <= 48 * 1024) return launch_y<true>(pb, a, nth, rpt, base + ybytes, s);
     return launch_y<false>(pb, a, nth, rpt, base, s);
