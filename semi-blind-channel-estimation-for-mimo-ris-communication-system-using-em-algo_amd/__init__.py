@@ -6,6 +6,7 @@ the reference's ``em(...)`` operator ("Proposed method/Proposed_method_NMSEvsTp.
 runs as hand-written HIP kernels for gfx950 behind the C-ABI of include/sbce.h.
 """
 from . import _lib, qam, signal_model, layout, distributed  # noqa: F401
+from . import sweeps  # noqa: F401
 from ._lib import SbceUnavailable, SbceError  # noqa: F401
 from .em import (  # noqa: F401
     em, em_ml, em_llf, em_ml_llf, em_zero_init, em_batch, estep_batch, mstep_batch, nmse_batch,

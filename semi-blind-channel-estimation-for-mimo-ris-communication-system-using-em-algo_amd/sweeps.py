@@ -1,0 +1,171 @@
+"""Monte-Carlo sweep drivers: the reference's entry-point scripts, running the GPU
+estimator with every trial of a sweep point batched into ONE sbce_em call.
+
+  nmse_vs_tp   "Proposed method/Proposed_method_NMSEvsTp.py":133-176
+  nmse_vs_td   "Proposed method/Proposed_method_NMSEvsTd.py":121-157
+  nmse_vs_snr  "Proposed method/SNR/all_Detectors.py":331-395 (exact and log-max EMs)
+
+Data generation (host, NumPy):
+  replay=True   the reference's exact legacy-RandomState call order after
+                np.random.seed(seed) (trials generated sequentially, so every rank
+                replays the whole stream and keeps its own trials);
+  replay=False  per-trial numpy Generators seeded (seed, trial): statistical parity,
+                no sequential dependence (large sweeps / many GPUs).
+Multi-GPU: when torch.distributed is initialised, trials are sharded
+(distributed.shard) and the per-point accumulators are all-reduced ONCE at the end.
+"""
+import numpy as np
+
+from . import signal_model as sm
+from .distributed import Accumulators, shard
+from .em import em_batch
+from .qam import qam_constellation
+
+
+def _dist():
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist, dist.get_world_size(), dist.get_rank()
+    except ImportError:
+        pass
+    return None, 1, 0
+
+
+def _trial_rng(seed, trial):
+    return np.random.RandomState(np.random.SeedSequence([seed, trial]).generate_state(1)[0])
+
+
+def _pack(trials, P):
+    """Stack per-trial dicts into the batch-major C-ABI arrays."""
+    return dict(
+        y_d=np.stack([t["Y_d"] for t in trials]),
+        y_p=np.stack([t["Y_p"] for t in trials]),
+        psi_d=np.stack([t["Psi_d"].T for t in trials]),
+        u_p=np.stack([t["U_p"] for t in trials]),
+        theta0=np.stack([t["h0"] for t in trials]),
+        h=np.stack([t["h"] for t in trials]),
+    )
+
+
+def _nmse(theta, h):
+    return np.sum(np.abs(theta - h) ** 2, axis=1) / np.sum(np.abs(h) ** 2, axis=1)
+
+
+def _run_points(points, cons, varns, itera, mode, acc, dist):
+    for pt, (trials, varn) in enumerate(zip(points, varns)):
+        if not trials:
+            continue
+        b = _pack(trials, None)
+        r = em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], cons, varn, itera, b["theta0"],
+                     mode=mode)
+        acc.add(pt, _nmse(r["theta"], b["h"]))
+    return acc
+
+
+def nmse_vs_tp(T_p=(4, 12, 20, 28, 36, 40), T_d=50, N=32, n_rx=4, n_tx=4, itera=3, monte_iter=1,
+               M=4, varn=0.1, seed=0, replay=True, mode="soft", varh=1.0):
+    """Mean NMSE per pilot length (PMd/Proposed_method_NMSEvsTp.py:154-176).
+
+    Reference draw order per trial: channelMatrix, symbols(T_d), pilotSymbols(max T_p),
+    then for each T_p: irsMatrix (T_d uniform draws), receivedSignals (noise)."""
+    dist, world, rank = _dist()
+    mine = set(shard(monte_iter, world, rank).tolist())
+    points = [[] for _ in T_p]
+    if replay:
+        np.random.seed(seed)
+    for i in range(monte_iter):
+        rs = None if replay else _trial_rng(seed, i)
+        if not replay and i not in mine:
+            continue
+        h = sm.channel_matrix(n_tx, n_rx, N, varh, rs=rs)
+        X_d, _ = sm.symbols(n_tx, M, T_d, rs=rs)
+        X_p = sm.pilot_symbols(n_tx, M, max(T_p), rs=rs)
+        for k, tp in enumerate(T_p):
+            Ptp, Ptd = sm.irs_matrix(tp, T_d, N, rs=rs)
+            Ptd = sm.insert_direct(Ptd)
+            Y_p, Y_d, U_p, _, h0 = sm.received_signals(tp, T_d, Ptp, Ptd, n_rx, n_tx, X_d, X_p[:tp],
+                                                       h, varn, rs=rs)
+            if i in mine:
+                points[k].append(dict(Y_d=Y_d, Y_p=Y_p, Psi_d=Ptd, U_p=U_p, h0=h0, h=h))
+    acc = Accumulators(len(T_p))
+    _run_points(points, qam_constellation(M), [varn] * len(T_p), itera, mode, acc, dist)
+    acc.allreduce(dist)
+    return np.asarray(T_p), acc.mean_nmse()
+
+
+def nmse_vs_td(T_d=(20, 30, 40, 50, 60, 70, 80, 90, 100), T_p=16, N=32, n_rx=2, n_tx=2, itera=3,
+               monte_iter=1, M=4, varn=0.1, seed=0, replay=True, mode="soft", varh=1.0):
+    """Mean NMSE per data length (PMd/Proposed_method_NMSEvsTd.py:140-157; C-order h, :15).
+
+    Reference draw order per trial: channelMatrix, pilotSymbols(T_p), then for each T_d:
+    symbols(T_d), irsMatrix, receivedSignals."""
+    dist, world, rank = _dist()
+    mine = set(shard(monte_iter, world, rank).tolist())
+    points = [[] for _ in T_d]
+    if replay:
+        np.random.seed(seed)
+    for i in range(monte_iter):
+        rs = None if replay else _trial_rng(seed, i)
+        if not replay and i not in mine:
+            continue
+        h = sm.channel_matrix(n_tx, n_rx, N, varh, order="C", rs=rs)
+        X_p = sm.pilot_symbols(n_tx, M, T_p, rs=rs)
+        for k, td in enumerate(T_d):
+            X_d, _ = sm.symbols(n_tx, M, td, rs=rs)
+            Ptp, Ptd = sm.irs_matrix(T_p, td, N, rs=rs)
+            Ptd = sm.insert_direct(Ptd)
+            Y_p, Y_d, U_p, _, h0 = sm.received_signals(T_p, td, Ptp, Ptd, n_rx, n_tx, X_d, X_p, h,
+                                                       varn, rs=rs)
+            if i in mine:
+                points[k].append(dict(Y_d=Y_d, Y_p=Y_p, Psi_d=Ptd, U_p=U_p, h0=h0, h=h))
+    acc = Accumulators(len(T_d))
+    _run_points(points, qam_constellation(M), [varn] * len(T_d), itera, mode, acc, dist)
+    acc.allreduce(dist)
+    return np.asarray(T_d), acc.mean_nmse()
+
+
+def gen_snr(SNR=(-5, 0, 5, 10, 15, 20), T_d=50, T_p=12, N=10, n_rx=2, n_tx=2, monte_iter=15, M=4,
+            power=10.0, seed=0, replay=True, varh=1.0, keep=None):
+    """Synthetic data of PMd/SNR/all_Detectors.py:362-370 in the reference draw order:
+    per trial channelMatrix, symbols, pilotSymbols, irsMatrix once, then per SNR
+    receivedSignals.  Returns (points, varns): points[k] = list of per-trial dicts."""
+    varns = sm.snr_to_varn(SNR, power)
+    keep = set(range(monte_iter)) if keep is None else set(keep)
+    points = [[] for _ in SNR]
+    if replay:
+        np.random.seed(seed)
+    for i in range(monte_iter):
+        rs = None if replay else _trial_rng(seed, i)
+        if not replay and i not in keep:
+            continue
+        h = sm.channel_matrix(n_tx, n_rx, N, varh, rs=rs)
+        X_d, _ = sm.symbols(n_tx, M, T_d, rs=rs)
+        X_p = sm.pilot_symbols(n_tx, M, T_p, rs=rs)
+        Ptp, Ptd = sm.irs_matrix(T_p, T_d, N, rs=rs)
+        Ptd = sm.insert_direct(Ptd)
+        for k in range(len(SNR)):
+            Y_p, Y_d, U_p, _, h0 = sm.received_signals(T_p, T_d, Ptp, Ptd, n_rx, n_tx, X_d, X_p, h,
+                                                       varns[k], rs=rs)
+            if i in keep:
+                points[k].append(dict(Y_d=Y_d, Y_p=Y_p, Psi_d=Ptd, U_p=U_p, h0=h0, h=h,
+                                      X_d=np.stack([x.reshape(-1) for x in X_d])))
+    return points, varns
+
+
+def nmse_vs_snr(SNR=(-5, 0, 5, 10, 15, 20), T_d=50, T_p=12, N=10, n_rx=2, n_tx=2, itera=5,
+                monte_iter=15, M=4, power=10.0, seed=0, replay=True, modes=("soft", "hard"),
+                varh=1.0):
+    """Mean NMSE per SNR for the exact ('soft', "Exact") and log-max ('hard') EMs
+    (PMd/SNR/all_Detectors.py:362-395; varn = power / 10^(SNR/10), :351-354)."""
+    dist, world, rank = _dist()
+    mine = shard(monte_iter, world, rank).tolist()
+    points, varns = gen_snr(SNR, T_d, T_p, N, n_rx, n_tx, monte_iter, M, power, seed, replay,
+                            varh, keep=mine)
+    out = {}
+    for mode in modes:
+        acc = Accumulators(len(SNR))
+        _run_points(points, qam_constellation(M), list(varns), itera, mode, acc, dist)
+        acc.allreduce(dist)
+        out[mode] = acc.mean_nmse()
+    return np.asarray(SNR), out

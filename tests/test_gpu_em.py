@@ -219,3 +219,35 @@ def test_mfma_and_valu_estep_agree(sbce, shape, monkeypatch):
     for (m1, S1), (m2, S2) in zip(out["mfma"], out["valu"]):
         assert np.abs(m1 - m2).max() < 1e-11 * scale
         assert np.abs(S1 - S2).max() < 1e-11 * scale
+
+
+def test_snr_sweep_entry_point_reproduces_reference_curve(sbce):
+    """North-star parity through the sweep entry point: sweeps.nmse_vs_snr with the
+    reference's own RNG replay (seed 0, one trial) gives the reference's NMSE-vs-SNR
+    curves (exact EM and log-max EM) of PMd/SNR/all_Detectors.py."""
+    k = golden("kat2_snr")
+    snr, curves = sbce.sweeps.nmse_vs_snr(monte_iter=1, seed=0)
+    assert np.array_equal(snr, k["snr"])
+    assert np.allclose(curves["soft"], k["nmse"], rtol=1e-9, atol=0)
+    assert np.allclose(curves["hard"], k["nmse_ml"], rtol=1e-9, atol=0)
+
+
+@pytest.mark.parametrize("script,args,rows", [
+    ("Proposed_method_NMSEvsTp.py", ["--monte-iter", "2", "--T-p", "8", "40", "--N", "8"], 2),
+    ("Proposed_method_NMSEvsTd.py", ["--monte-iter", "2", "--T-d", "20", "40", "--N", "8"], 2),
+    ("nmse_vs_snr.py", ["--monte-iter", "2", "--SNR", "0", "20"], 2),
+])
+def test_sweep_scripts_run(sbce, script, args, rows, tmp_path):
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT, PKG
+    out = tmp_path / "curve.npz"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, PKG, script), *args, "--out", str(out)],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = np.load(out)
+    assert d["x"].shape == (rows,)
+    for key in d.files:
+        if key != "x":
+            assert np.isfinite(d[key]).all()

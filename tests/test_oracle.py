@@ -214,3 +214,16 @@ def test_device_exp_polynomial_accuracy():
     assert rel_err.max() < 1e-15
     assert _fexp_neg_numpy(np.array([-np.inf]))[0] == 0.0
     assert _fexp_neg_numpy(np.array([0.0]))[0] == 1.0
+
+
+def test_sweep_snr_replay_reproduces_reference_data(sbce):
+    """sweeps.gen_snr replays PMd/SNR/all_Detectors.py's draw order (KAT-2 data)."""
+    k = golden("kat2_snr")
+    pts, varns = sbce.sweeps.gen_snr(monte_iter=1, seed=0)
+    assert np.allclose(varns, k["varn"], rtol=1e-15)
+    for i in range(6):
+        t = pts[i][0]
+        assert np.array_equal(t["h"], k["h"])
+        assert np.array_equal(t["Psi_d"], k["Ptd"])
+        assert rel(t["Y_d"], k["Y_d"][i]) < 1e-14 and rel(t["Y_p"], k["Y_p"][i]) < 1e-14
+        assert rel(t["h0"], k["h0"][i]) < 1e-12
