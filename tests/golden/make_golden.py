@@ -236,6 +236,25 @@ def case_root():
                             theta=np.asarray(th).reshape(-1), nmse=nmse(th, h))
 
 
+def case_pm(name, N, n_tx, n_rx, T_d, T_p, M, varn, itera, seed, r_uniform, r_soft):
+    """PM.em_pm (uniform list, lstsq) and PM_beta.em_pm (posterior list) on north-star data."""
+    ns = load_defs(os.path.join(PMD, "Proposed_method_NMSEvsTp.py"),
+                   N=N, n_tx=n_tx, n_rx=n_rx, beta_min=0.0, beta_max=2 * np.pi)
+    d = _gen_northstar(ns, seed, N, n_tx, n_rx, T_d, T_p, M, varn)
+    cons = _cons(M)
+    ns_pm = load_defs(os.path.join(PMD, "PM.py"), N=N, beta_min=0.0, beta_max=2 * np.pi)
+    th_u = quiet(ns_pm["em_pm"], d["Y_d"], d["Y_p"], T_d, T_p, d["Z_p"], d["Ptd"], d["aps"], M,
+                 varn, itera, d["h0"], d["h"], n_tx, r_uniform, d["X_d"], cons)
+    ns_pmb = load_defs(os.path.join(PMD, "PM_beta.py"), N=N, qamCons=cons, beta_min=0.0,
+                       beta_max=2 * np.pi)
+    th_s = quiet(ns_pmb["em_pm"], d["Y_d"], d["Y_p"], T_d, T_p, d["Z_p"], d["Ptd"], M, varn,
+                 itera, d["h0"], d["h"], n_tx, r_soft, d["X_d"], cons)
+    return name, _pack(d, N=N, n_tx=n_tx, n_rx=n_rx, T_d=T_d, T_p=T_p, M=M, varn=varn,
+                       itera=itera, seed=seed, r_uniform=r_uniform, r_soft=r_soft,
+                       pm_theta=np.asarray(th_u).reshape(-1),
+                       pmbeta_theta=np.asarray(th_s).reshape(-1))
+
+
 def case_qam():
     """Constellation tables of the vendored komm QAM (PMd/QAM.py:320-322)."""
     return "qam", {f"cons{M}": _cons(M) for M in (4, 16, 64, 256)}
@@ -243,6 +262,8 @@ def case_qam():
 
 CASES = {
     "qam": (case_qam, ()),
+    "pm_nt4": (case_pm, ("pm_nt4", 3, 4, 4, 24, 8, 4, 0.1, 3, 12, 0, 2)),
+    "pm_nt3_m16": (case_pm, ("pm_nt3_m16", 4, 3, 3, 24, 10, 16, 0.3, 3, 13, 1, 1)),
     "kat1_s7": (case_kat1, (7,)),
     "kat1_s11": (case_kat1, (11,)),
     "kat2_snr": (case_kat2, ()),

@@ -227,3 +227,24 @@ def test_sweep_snr_replay_reproduces_reference_data(sbce):
         assert np.array_equal(t["Psi_d"], k["Ptd"])
         assert rel(t["Y_d"], k["Y_d"][i]) < 1e-14 and rel(t["Y_p"], k["Y_p"][i]) < 1e-14
         assert rel(t["h0"], k["h0"][i]) < 1e-12
+
+
+PM_CASES = [("kat1_s7", "pm_r0_theta", False, 0, 3), ("kat1_s7", "pmbeta_r1_theta", True, 1, 3),
+            ("pm_nt4", "pm_theta", False, None, None), ("pm_nt4", "pmbeta_theta", True, None, None),
+            ("pm_nt3_m16", "pm_theta", False, None, None),
+            ("pm_nt3_m16", "pmbeta_theta", True, None, None)]
+
+
+@pytest.mark.parametrize("case,key,soft,r,itera", PM_CASES)
+def test_pm_oracle_matches_reference(case, key, soft, r, itera):
+    """PM.em_pm (uniform list) and PM_beta.em_pm (posterior list) incl. the off-by-one
+    list channel, the concatenated stream order and the oracle early stop."""
+    from oracle.pm import em_pm
+    d = golden(case)
+    n_tx, n_rx, M = int(d["n_tx"]), int(d["n_rx"]), int(d["M"])
+    if r is None:
+        r = int(d["r_soft"] if soft else d["r_uniform"])
+        itera = int(d["itera"])
+    th = em_pm(d["Y_d"], d["Y_p"], u_from_zp(d["Z_p"], n_rx), d["Ptd"], float(d["varn"]), itera,
+               d["h0"], n_tx, n_rx, r, cons_from_aps(d["aps"], M), soft=soft, h=d["h"])
+    assert rel(th, d[key]) < 1e-12
