@@ -66,6 +66,10 @@ extern "C" {
                                    Proposed_method_NMSEvsTp.py:61-71 */
 #define SBCE_ESTEP_HARD 1       /* argmax posterior ("log-max"):
                                    ML_detecctor.py:65-77 */
+#define SBCE_ESTEP_PM 2         /* partitioned list detector, every list member
+                                   weight 1: PM.py:57-104 (dims.partition_r) */
+#define SBCE_ESTEP_PM_SOFT 3    /* partitioned list detector, posterior list
+                                   weights: PM_beta.py:55-95 (dims.partition_r) */
 
 /* M-step solve modes (SURVEY.md §7 hard part 3) */
 #define SBCE_SOLVE_CHOL 0       /* Hermitian Cholesky of the reduced L x L system
@@ -79,13 +83,14 @@ extern "C" {
 
 typedef struct sbce_dims {
     int32_t batch;      /* B: independent Monte-Carlo trials */
-    int32_t n_tx;       /* streams (1..4 for the exact E-step) */
+    int32_t n_tx;       /* streams (1..4 exact/hard E-step, 1..8 PM E-steps) */
     int32_t n_rx;       /* receive antennas (1..8) */
     int32_t n_psi;      /* P = rows of PsiTilde_td (N+1 with the direct path) */
     int32_t t_p;        /* pilot symbols */
     int32_t t_d;        /* data symbols */
     int32_t m;          /* constellation size (power of two, 2..64) */
-    int32_t reserved;   /* must be 0 */
+    int32_t partition_r;/* PM modes: list = M^(p+1) with p = int(partition_r /
+                           log2 M) (PM.py:74), at most 64 members; else 0 */
     double varn;        /* noise variance parameter; posterior uses varn^2 */
 } sbce_dims;
 

@@ -59,36 +59,44 @@ def pm_list(y, channel, qamCons, partition_r, M):
     return np.asarray(out)
 
 
+def pm_moments(theta, Y_d, Psi, qamCons, n_tx, n_rx, partition_r, varn, soft):
+    """PM E-step of one trial: m (T,n_tx), S (T,n_tx,n_tx) summed over the list with
+    weight 1 (PM.py:103-104) or posterior weights (PM_beta.py:88-95)."""
+    M = len(qamCons)
+    P, T = Psi.shape
+    N = P - 1
+    theta = np.asarray(theta, dtype=complex).reshape(-1)
+    th = theta.reshape(-1, 1)
+    h_bu = th[:n_tx * n_rx].reshape((n_rx, n_tx), order="F")
+    prod = th[n_tx * n_rx:].reshape((n_tx * n_rx, N), order="F")
+    H3 = theta.reshape(P, n_tx, n_rx)
+    m = np.zeros((T, n_tx), dtype=complex)
+    S = np.zeros((T, n_tx, n_tx), dtype=complex)
+    for t in range(T):
+        channel = h_bu + (prod @ Psi[:N, t]).reshape((n_rx, n_tx), order="F")
+        lst = pm_list(Y_d[t], channel, qamCons, partition_r, M)
+        if soft:
+            Htrue = np.einsum("par,p->ra", H3, Psi[:, t])
+            d = np.sum(np.abs(Y_d[t][None, :] - lst @ Htrue.T) ** 2, axis=1)
+            w = np.exp(-(d - d.min()) / varn ** 2)
+            w /= w.sum()
+        else:
+            w = np.ones(lst.shape[0])
+        m[t] = w @ lst
+        S[t] = np.einsum("j,ja,jb->ab", w, lst, np.conj(lst))
+    return m, S
+
+
 def em_pm(Y_d, Y_p, U_p, Psi, varn, itera, theta0, n_tx, n_rx, partition_r, qamCons,
           soft=False, h=None, return_trace=False):
     """PM EM over one trial, array inputs (Y_d (T_d,n_rx), Psi (N+1,T_d), U_p (T_p,L)).
     Reduced-form M-step; list weights uniform (soft=False, PM.py) or posterior
     (soft=True, PM_beta.py)."""
     from .em_reduced import mstep_build, mstep_solve
-    M = len(qamCons)
-    P, T = Psi.shape
-    N = P - 1
     theta = np.asarray(theta0, dtype=complex).reshape(-1)
     trace = []
     for l in range(itera):
-        th = theta.reshape(-1, 1)
-        h_bu = th[:n_tx * n_rx].reshape((n_rx, n_tx), order="F")
-        prod = th[n_tx * n_rx:].reshape((n_tx * n_rx, N), order="F")
-        H3 = theta.reshape(P, n_tx, n_rx)
-        m = np.zeros((T, n_tx), dtype=complex)
-        S = np.zeros((T, n_tx, n_tx), dtype=complex)
-        for t in range(T):
-            channel = h_bu + (prod @ Psi[:N, t]).reshape((n_rx, n_tx), order="F")
-            lst = pm_list(Y_d[t], channel, qamCons, partition_r, M)
-            if soft:
-                Htrue = np.einsum("par,p->ra", H3, Psi[:, t])
-                d = np.sum(np.abs(Y_d[t][None, :] - lst @ Htrue.T) ** 2, axis=1)
-                w = np.exp(-(d - d.min()) / varn ** 2)
-                w /= w.sum()
-            else:
-                w = np.ones(lst.shape[0])
-            m[t] = w @ lst
-            S[t] = np.einsum("j,ja,jb->ab", w, lst, np.conj(lst))
+        m, S = pm_moments(theta, Y_d, Psi, qamCons, n_tx, n_rx, partition_r, varn, soft)
         R, rhs = mstep_build(U_p, Y_p, Psi, Y_d, m, S)
         theta = mstep_solve(R, rhs)
         trace.append(theta.copy())

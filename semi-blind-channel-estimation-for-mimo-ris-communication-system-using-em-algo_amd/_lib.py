@@ -13,6 +13,8 @@ LIB_PATH = os.path.join(_HERE, "libsbce.so")
 SBCE_ABI_VERSION = 1
 SBCE_ESTEP_SOFT = 0
 SBCE_ESTEP_HARD = 1
+SBCE_ESTEP_PM = 2
+SBCE_ESTEP_PM_SOFT = 3
 SBCE_SOLVE_CHOL = 0
 SBCE_SOLVE_CHOL_DROP = 1
 SBCE_STATUS_NONHPD = 1
@@ -32,7 +34,7 @@ class SbceError(RuntimeError):
 class Dims(ctypes.Structure):
     _fields_ = [("batch", ctypes.c_int32), ("n_tx", ctypes.c_int32), ("n_rx", ctypes.c_int32),
                 ("n_psi", ctypes.c_int32), ("t_p", ctypes.c_int32), ("t_d", ctypes.c_int32),
-                ("m", ctypes.c_int32), ("reserved", ctypes.c_int32), ("varn", ctypes.c_double)]
+                ("m", ctypes.c_int32), ("partition_r", ctypes.c_int32), ("varn", ctypes.c_double)]
 
 
 class Ptrs(ctypes.Structure):

@@ -22,11 +22,11 @@ struct Carve {
 bool make_problem(const sbce_dims* d, Problem& pb) {
     if (!d) return false;
     if (d->batch < 0 || d->n_tx < 1 || d->n_rx < 1 || d->n_psi < 1 || d->t_p < 0 || d->t_d < 1 ||
-        d->m < 2 || d->reserved != 0 || !(d->varn > 0.0))
+        d->m < 2 || d->partition_r < 0 || !(d->varn > 0.0))
         return false;
-    if (d->n_tx > 4 || d->n_rx > 8) return false;
+    if (d->n_tx > 8 || d->n_rx > 8) return false;
     pb.B = d->batch; pb.NT = d->n_tx; pb.NR = d->n_rx; pb.P = d->n_psi;
-    pb.Tp = d->t_p; pb.Td = d->t_d; pb.M = d->m; pb.varn = d->varn;
+    pb.Tp = d->t_p; pb.Td = d->t_d; pb.M = d->m; pb.varn = d->varn; pb.pr = d->partition_r;
     pb.L = pb.P * pb.NT;
     pb.K = pb.L * pb.NR;
     return true;

@@ -1,0 +1,274 @@
+// PM (partitioned-detector) E-step: "Proposed method/PM.py":57-104 (uniform list
+// weights) and "Proposed method/PM_beta.py":55-95 (posterior list weights), the
+// list-based E-step that makes n_tx = 8 (BASELINE cfg 2) tractable.
+//
+// Per data symbol (one wave, n_tx, n_rx <= 8 so one 8x8 matrix = one wave):
+//   1. H_off = H_BU + sum_{n<N} G_{n+1} psi_{n,t}  (the reference's off-by-one
+//      slice PsiTilde_td[:N, t], PM.py:63) builds the list; H_true = sum_p G_p psi_{p,t}
+//      weighs it (PM_beta.py:88-93);
+//   2. greedy stream order: repeatedly drop the column with the largest
+//      diag((A^H A)^{-1}) (PM.py:65-70; Gauss-Jordan inverse, lanes over entries);
+//   3. A = first p+1 streams (p = int(partition_r / log2 M), PM.py:74), B = the rest;
+//      G_B = (B^H B)^{-1} B^H;
+//   4. one lane per candidate a in M^{|A|} (itertools.product order):
+//      z = G_B (y - A a), per-element nearest constellation point (== the exhaustive
+//      argmin over M^{|B|} of ||z - b||^2, PM.py:97-99, which is separable), candidate
+//      x = [a, b] in the CONCATENATED order, used as natural stream order (PM.py:102);
+//   5. weights: 1 (PM) or softmax(-||y - H_true x||^2 / varn^2) (PM_beta);
+//   6. m_t = sum w x, S_t = sum w x x^H (unnormalised for the uniform list, as the
+//      reference sums every list member with weight 1, PM.py:103-104).
+#include "sbce_internal.h"
+
+namespace sbce {
+
+namespace {
+
+constexpr int kPmWaves = 2;
+constexpr int kAugW = 16;          // augmented-matrix row stride ([G | I], G in cols 0..7)
+
+struct PmConst {
+    int B, Td, P, M, lm, NT, NR, NA, JA;
+    double inv_s2;
+};
+
+struct PmLds {                      // per-wave LDS carve (complex doubles unless noted)
+    static constexpr int Ht = 0, Ho = 64, Y = 128, AUG = 136, GB = AUG + 8 * kAugW,
+                         GY = GB + 64, GA = GY + 8, XS = GA + 64, W = XS + 64 * 8,
+                         INTS = W + 32, TOTAL = INTS + 16;
+};
+
+// In-place Gauss-Jordan inverse of the k x k block aug[0:k][0:k] (HPD, no pivoting),
+// with the identity pre-set in aug[0:k][8:8+k]; the inverse ends in aug[0:k][8:8+k].
+__device__ void gj_inverse(cd* aug, int k, int lane) {
+    for (int c = 0; c < k; ++c) {
+        const cd piv = aug[c * kAugW + c];
+        const double den = cabs2(piv);
+        const cd inv = cmk(piv.x / den, -piv.y / den);
+        cd rowc[2], fi[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int e = lane + 64 * h;
+            const int i = e >> 4, j = e & 15;
+            rowc[h] = (i < k) ? aug[c * kAugW + j] : czero();
+            fi[h] = (i < k) ? aug[i * kAugW + c] : czero();
+        }
+        wave_sync();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int e = lane + 64 * h;
+            const int i = e >> 4, j = e & 15;
+            if (i < k) {
+                const cd rs = cmul(rowc[h], inv);
+                aug[i * kAugW + j] = (i == c) ? rs : csub(aug[i * kAugW + j], cmul(fi[h], rs));
+            }
+        }
+        wave_sync();
+    }
+}
+
+// aug[u][v] = sum_r conj(H[col_u][r]) H[col_v][r], identity in cols 8.. (H indexed [a*NR + r])
+__device__ void gram(cd* aug, const cd* H, const int* cols, int k, int NR, int lane) {
+    const int u = lane >> 3, v = lane & 7;
+    if (u < k && v < k) {
+        cd acc = czero();
+        for (int r = 0; r < NR; ++r) acc = cfmac(acc, H[cols[v] * NR + r], H[cols[u] * NR + r]);
+        aug[u * kAugW + v] = acc;
+        aug[u * kAugW + 8 + v] = (u == v) ? cmk(1.0, 0.0) : czero();
+    }
+    wave_sync();
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64 * kPmWaves) void estep_pm_kernel(EstepArgs a, PmConst c) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cd* s_cons = reinterpret_cast<cd*>(smem);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    cd* W = s_cons + 64 + wave * PmLds::TOTAL;
+    cd* Ht = W + PmLds::Ht;
+    cd* Ho = W + PmLds::Ho;
+    cd* yv = W + PmLds::Y;
+    cd* aug = W + PmLds::AUG;
+    cd* GB = W + PmLds::GB;
+    cd* Gy = W + PmLds::GY;
+    cd* GA = W + PmLds::GA;
+    cd* xs = W + PmLds::XS;
+    double* wts = reinterpret_cast<double*>(W + PmLds::W);
+    int* cols = reinterpret_cast<int*>(W + PmLds::INTS);
+    int* ord = cols + 8;
+
+    for (int i = threadIdx.x; i < c.M; i += blockDim.x) s_cons[i] = a.cons[i];
+    __syncthreads();
+    const long nsym = (long)c.B * c.Td;
+    const long gsym = (long)blockIdx.x * kPmWaves + wave;
+    if (gsym >= nsym) return;
+    const int b = (int)(gsym / c.Td);
+    if (a.done && a.done[b]) return;
+    const int NT = c.NT, NR = c.NR, NO = NT * NR, P = c.P, mask = c.M - 1;
+
+    // ---- 1. H_true, H_off (lane = output a*NR + r), y ----
+    if (lane < NO) {
+        const cd* th = a.theta + (size_t)b * P * NO;
+        const cd* ps = a.psid + (size_t)gsym * P;
+        cd ht = czero(), ho = th[lane];
+        for (int p = 0; p < P; ++p) {
+            const cd psi = ps[p];
+            ht = cfma(ht, psi, th[p * NO + lane]);
+            if (p + 1 < P) ho = cfma(ho, psi, th[(p + 1) * NO + lane]);
+        }
+        Ht[lane] = ht;
+        Ho[lane] = ho;
+    }
+    if (lane < NR) yv[lane] = a.yd[(size_t)gsym * NR + lane];
+    if (lane < NT) cols[lane] = lane;
+    wave_sync();
+
+    // ---- 2. greedy stream order on H_off ----
+    for (int step = 0; step < NT; ++step) {
+        const int k = NT - step;
+        int kmax = 0;
+        if (k > 1) {
+            gram(aug, Ho, cols, k, NR, lane);
+            gj_inverse(aug, k, lane);
+            // np.argmax over the complex diagonal: lexicographic (real, imag), first maximum
+            cd best = aug[0 * kAugW + 8];
+            for (int u = 1; u < k; ++u) {
+                const cd v = aug[u * kAugW + 8 + u];
+                if (v.x > best.x || (v.x == best.x && v.y > best.y)) { best = v; kmax = u; }
+            }
+        }
+        wave_sync();
+        if (lane == 0) {
+            ord[step] = cols[kmax];
+            for (int u = kmax; u + 1 < k; ++u) cols[u] = cols[u + 1];
+        }
+        wave_sync();
+    }
+
+    // ---- 3. partition A = ord[0:NA], B = ord[NA:NT]; G_B = (B^H B)^{-1} B^H ----
+    const int NA = c.NA, nB = NT - NA;
+    const int* Bc = ord + NA;
+    if (nB > 0) {
+        gram(aug, Ho, Bc, nB, NR, lane);
+        gj_inverse(aug, nB, lane);
+        {
+            const int bb = lane / NR, r = lane - bb * NR;   // lanes < nB*NR <= 64
+            if (bb < nB) {
+                cd acc = czero();
+                for (int b2 = 0; b2 < nB; ++b2)
+                    acc = cfma(acc, aug[bb * kAugW + 8 + b2], cconj(Ho[Bc[b2] * NR + r]));
+                GB[bb * NR + r] = acc;
+            }
+        }
+        wave_sync();
+        if (lane < nB) {
+            cd acc = czero();
+            for (int r = 0; r < NR; ++r) acc = cfma(acc, GB[lane * NR + r], yv[r]);
+            Gy[lane] = acc;
+        }
+        {
+            const int bb = lane >> 3, q = lane & 7;
+            if (bb < nB && q < NA) {
+                cd acc = czero();
+                for (int r = 0; r < NR; ++r) acc = cfma(acc, GB[bb * NR + r], Ho[ord[q] * NR + r]);
+                GA[bb * 8 + q] = acc;
+            }
+        }
+        wave_sync();
+    }
+
+    // ---- 4./5. candidates (one lane each) and their weights ----
+    const int JA = c.JA;
+    double d = INFINITY;
+    if (lane < JA) {
+        cd* x = xs + lane * 8;      // the candidate lives in LDS (no dynamically indexed registers)
+        for (int q = 0; q < NA; ++q) x[q] = s_cons[(lane >> (c.lm * (NA - 1 - q))) & mask];
+        for (int bb = 0; bb < nB; ++bb) {
+            cd z = Gy[bb];
+            for (int q = 0; q < NA; ++q) z = csub(z, cmul(GA[bb * 8 + q], x[q]));
+            int sbest = 0;
+            double dbest = cabs2(csub(z, s_cons[0]));
+            for (int s2 = 1; s2 < c.M; ++s2) {
+                const double dd = cabs2(csub(z, s_cons[s2]));
+                if (dd < dbest) { dbest = dd; sbest = s2; }
+            }
+            x[NA + bb] = s_cons[sbest];
+        }
+        if (MODE == 3) {
+            d = 0.0;
+            for (int r = 0; r < NR; ++r) {
+                cd res = yv[r];
+                for (int q = 0; q < NT; ++q) res = csub(res, cmul(Ht[q * NR + r], x[q]));
+                d += cabs2(res);
+            }
+        }
+    }
+    double w = (lane < JA) ? 1.0 : 0.0;
+    if (MODE == 3) {
+        double dm = d;
+        for (int off = 32; off >= 1; off >>= 1) dm = fmin(dm, shfl_xor_d(dm, off));
+        w = (lane < JA) ? exp(-(d - dm) * c.inv_s2) : 0.0;
+        double z = w;
+        for (int off = 32; off >= 1; off >>= 1) z += shfl_xor_d(z, off);
+        w /= z;
+    }
+    wts[lane] = w;
+    wave_sync();
+
+    // ---- 6. moments ----
+    const int MS = NT + NT * NT;
+    cd* out = a.mom + (size_t)gsym * MS;
+    {
+        const int ai = lane >> 3, bi = lane & 7;
+        if (ai < NT && bi < NT) {
+            cd acc = czero();
+            for (int i = 0; i < JA; ++i)
+                acc = caxpy(acc, wts[i], cmulc(xs[i * 8 + ai], xs[i * 8 + bi]));
+            out[NT + ai * NT + bi] = acc;
+        }
+        if (lane < NT) {
+            cd acc = czero();
+            for (int i = 0; i < JA; ++i) acc = caxpy(acc, wts[i], xs[i * 8 + lane]);
+            out[lane] = acc;
+        }
+    }
+}
+
+}  // namespace
+
+bool estep_pm_supported(const Problem& pb, int partition_r) {
+    if (pb.NT < 1 || pb.NT > 8 || pb.NR < 1 || pb.NR > 8) return false;
+    if (pb.M < 2 || pb.M > 64 || (pb.M & (pb.M - 1))) return false;
+    if (partition_r < 0) return false;
+    const int p = (int)((double)partition_r / log2((double)pb.M));
+    const int NA = p + 1;
+    if (NA > pb.NT) return false;
+    int lm = 0;
+    while ((1 << lm) < pb.M) ++lm;
+    return lm * NA <= 6;                       // list of M^{|A|} <= 64 candidates
+}
+
+hipError_t launch_estep_pm(const Problem& pb, const EstepArgs& a, int mode, int partition_r,
+                           hipStream_t s) {
+    if (!estep_pm_supported(pb, partition_r)) return hipErrorInvalidValue;
+    PmConst c;
+    c.B = pb.B; c.Td = pb.Td; c.P = pb.P; c.M = pb.M; c.NT = pb.NT; c.NR = pb.NR;
+    int lm = 0;
+    while ((1 << lm) < pb.M) ++lm;
+    c.lm = lm;
+    c.NA = (int)((double)partition_r / log2((double)pb.M)) + 1;
+    c.JA = 1 << (lm * c.NA);
+    c.inv_s2 = 1.0 / (pb.varn * pb.varn);
+    const size_t lds = (64 + (size_t)kPmWaves * PmLds::TOTAL) * sizeof(cd);
+    const long nsym = (long)pb.B * pb.Td;
+    const long blocks = (nsym + kPmWaves - 1) / kPmWaves;
+    if (blocks == 0) return hipSuccess;
+    if (mode == SBCE_ESTEP_PM_SOFT)
+        hipLaunchKernelGGL(estep_pm_kernel<3>, dim3((unsigned)blocks), dim3(64 * kPmWaves), lds, s,
+                           a, c);
+    else
+        hipLaunchKernelGGL(estep_pm_kernel<2>, dim3((unsigned)blocks), dim3(64 * kPmWaves), lds, s,
+                           a, c);
+    return hipGetLastError();
+}
+
+}  // namespace sbce

@@ -69,6 +69,48 @@ __global__ __launch_bounds__(256) void rbuild_kernel(MstepArgs a, int B, int P, 
         }
 }
 
+// Wide variant for NT = 5..8 (PM E-step shapes): one thread per (block pair, row i)
+// keeps NT accumulators instead of NT^2.
+template <int NT>
+__global__ __launch_bounds__(256) void rbuild_wide_kernel(MstepArgs a, int B, int P, int Tp,
+                                                          int Td, int L) {
+    const int b = blockIdx.y;
+    if (a.done && a.done[b]) return;
+    const int npairs = P * (P + 1) / 2;
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int pi = gid / NT, i = gid - pi * NT;
+    if (pi >= npairs) return;
+    int p = (int)((sqrt(8.0 * pi + 1.0) - 1.0) * 0.5);
+    while ((p + 1) * (p + 2) / 2 <= pi) ++p;
+    while (p * (p + 1) / 2 > pi) --p;
+    const int q = pi - p * (p + 1) / 2;
+    constexpr int MS = NT + NT * NT;
+
+    cd acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = czero();
+    const cd* up = a.up + (size_t)b * Tp * L;
+    for (int tp = 0; tp < Tp; ++tp) {
+        const cd ua = up[tp * L + p * NT + i];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[j] = cfmac(acc[j], ua, up[tp * L + q * NT + j]);
+    }
+    const cd* ps = a.psid + (size_t)b * Td * P;
+    const cd* mom = a.mom + (size_t)b * Td * MS;
+    for (int t = 0; t < Td; ++t) {
+        const cd w = cmulc(ps[t * P + p], ps[t * P + q]);
+        const cd* St = mom + t * MS + NT + i * NT;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[j] = cfma(acc[j], w, St[j]);
+    }
+    cd* R = a.R + (size_t)b * L * L;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        R[(size_t)(p * NT + i) * L + q * NT + j] = acc[j];
+        if (p != q) R[(size_t)(q * NT + j) * L + p * NT + i] = cconj(acc[j]);
+    }
+}
+
 // ------------------------------------------------------------------ B^H build
 // One thread per row l = p*NT + a of one trial (L x NR right-hand sides).
 template <int NR>
@@ -202,6 +244,9 @@ hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t
         case 2: hipLaunchKernelGGL(rbuild_kernel<2>, g1, dim3(256), 0, s, a, pb.B, pb.P, pb.Tp, pb.Td, pb.L); break;
         case 3: hipLaunchKernelGGL(rbuild_kernel<3>, g1, dim3(256), 0, s, a, pb.B, pb.P, pb.Tp, pb.Td, pb.L); break;
         case 4: hipLaunchKernelGGL(rbuild_kernel<4>, g1, dim3(256), 0, s, a, pb.B, pb.P, pb.Tp, pb.Td, pb.L); break;
+#define SBCE_RW(n) case n: hipLaunchKernelGGL(rbuild_wide_kernel<n>, dim3((npairs * n + 255) / 256, pb.B), dim3(256), 0, s, a, pb.B, pb.P, pb.Tp, pb.Td, pb.L); break;
+        SBCE_RW(5) SBCE_RW(6) SBCE_RW(7) SBCE_RW(8)
+#undef SBCE_RW
         default: return hipErrorInvalidValue;
     }
     hipError_t e = hipGetLastError();

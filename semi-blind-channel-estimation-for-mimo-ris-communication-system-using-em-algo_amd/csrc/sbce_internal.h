@@ -80,6 +80,7 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) { return __shfl_xo
 // ------------------------------------------------------------------ launch API
 struct Problem {
     int B, NT, NR, P, Tp, Td, M, L, K;
+    int pr;            // partition_r (PM E-step modes)
     double varn;
 };
 
@@ -107,6 +108,9 @@ struct MstepArgs {
 };
 
 hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStream_t s);
+hipError_t launch_estep_pm(const Problem& pb, const EstepArgs& a, int mode, int partition_r,
+                           hipStream_t s);
+bool estep_pm_supported(const Problem& pb, int partition_r);
 bool estep_supported(const Problem& pb, int mode);
 hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s);

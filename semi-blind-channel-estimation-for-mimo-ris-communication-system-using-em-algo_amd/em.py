@@ -14,6 +14,10 @@ Reference operator -> entry point here:
                                                                         -> em_ml_llf(..., Z_d=)
   em(... no h_initial ...)     root Proposed_method_NMSEvsTp.py:43-69 (zero init)
                                                                         -> em_zero_init()
+  em_pm(..., h, n_tx, partition_r, X_d, qamCons)
+                               PM.py:47-116 (uniform list weights)      -> em_pm()
+  em_pm(... no all_possibleSymbols ...)
+                               PM_beta.py:42-112 (posterior list weights) -> em_pm_soft()
 Batched form for sweeps / benchmark: ``em_batch`` (one sbce_em call for all trials).
 
 Semantics kept from the reference: inputs are not mutated, theta is returned
@@ -44,12 +48,13 @@ def _dev(torch, arr, dtype=None):
     return torch.from_numpy(a).to("cuda", non_blocking=False)
 
 
-_MODES = {"soft": _lib.SBCE_ESTEP_SOFT, "hard": _lib.SBCE_ESTEP_HARD}
+_MODES = {"soft": _lib.SBCE_ESTEP_SOFT, "hard": _lib.SBCE_ESTEP_HARD, "pm": _lib.SBCE_ESTEP_PM,
+          "pm_soft": _lib.SBCE_ESTEP_PM_SOFT}
 _SOLVES = {"chol": _lib.SBCE_SOLVE_CHOL, "drop": _lib.SBCE_SOLVE_CHOL_DROP}
 
 
 def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_true=None,
-             h_true=None, solve="chol", return_device=False):
+             h_true=None, solve="chol", return_device=False, partition_r=0):
     """Run ``itera`` EM iterations on a batch of independent trials.
 
     Array layouts (complex128, batch-major, include/sbce.h):
@@ -58,6 +63,7 @@ def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_t
       cons (M,), theta0 (B,K) with K = P*n_tx*n_rx.
     Optional: x_d_true (B,T_d,n_tx) -> per-iteration LLF (IterationsvsLLF.py:76);
     h_true (B,K) -> the reference's oracle early stop (PM.py:110-112).
+    mode: "soft" | "hard" | "pm" | "pm_soft"; partition_r selects the PM list size.
     Inputs may be numpy arrays or CUDA complex128 tensors (used in place).
     Returns dict(theta (B,K), llf (B,itera) or None, status (B,), iters_done (B,)).
     """
@@ -84,7 +90,7 @@ def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_t
     M = Cs.shape[0]
     if th.shape != (B, L * n_rx):
         raise ValueError(f"theta0 shape {tuple(th.shape)} != {(B, L * n_rx)}")
-    dims = _lib.Dims(B, n_tx, n_rx, P, T_p, T_d, M, 0, float(varn))
+    dims = _lib.Dims(B, n_tx, n_rx, P, T_p, T_d, M, int(partition_r), float(varn))
     ws_bytes = _lib.workspace_bytes(dims)
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device="cuda")
     status = torch.zeros(B, dtype=torch.int32, device="cuda")
@@ -107,14 +113,18 @@ def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_t
     return {k: (v.cpu().numpy() if v is not None else None) for k, v in out.items()}
 
 
-def _prepare_single(Y_d, Y_p, Z_p, PsiTilde_td, all_possibleSymbols, M, h_initial):
+def _prepare_single(Y_d, Y_p, Z_p, PsiTilde_td, all_possibleSymbols, M, h_initial, n_tx=None,
+                    cons=None):
     n_rx = np.asarray(Y_d[0]).shape[0]
-    aps = np.asarray(all_possibleSymbols)
-    n_tx = aps.shape[1]
+    aps = None if all_possibleSymbols is None else np.asarray(all_possibleSymbols)
+    if aps is not None:
+        n_tx = aps.shape[1]
+        cons = cons_from_aps(aps, int(M)) if cons is None else np.asarray(cons, dtype=complex)
+    else:
+        cons = np.asarray(cons, dtype=complex).reshape(-1)
     Psi = np.asarray(PsiTilde_td)
     P = Psi.shape[0]
     K = P * n_tx * n_rx
-    cons = cons_from_aps(aps, int(M))
     U_p = u_from_zp(Z_p, n_rx) if len(Z_p) else np.zeros((0, P * n_tx), dtype=complex)
     check_structure(Z_p, U_p, n_rx, aps, cons, K)
     y_d = np.stack([np.asarray(y).reshape(-1) for y in Y_d])[None]
@@ -196,20 +206,61 @@ def em_ml_llf(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn
                   h_initial, n_tx, mode="hard")
 
 
+def _pm(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, aps, M, varn, itera, h_initial, h, n_tx,
+        partition_r, qamCons, mode, solve, verbose):
+    cons = np.asarray(qamCons, dtype=complex).reshape(-1)
+    if cons.size != int(M):
+        raise ValueError("qamCons must hold the M constellation points")
+    d = _prepare_single(Y_d[:T_d], Y_p[:T_p], Z_p[:T_p], np.asarray(PsiTilde_td)[:, :T_d], aps, M,
+                        h_initial, n_tx=int(n_tx), cons=cons)
+    if d["n_tx"] != int(n_tx):
+        raise ValueError("n_tx does not match all_possibleSymbols")
+    hh = None if h is None else np.asarray(h, dtype=complex).reshape(1, -1)
+    res = em_batch(d["y_d"], d["y_p"], d["psi_d"], d["u_p"], cons, varn, itera, d["theta0"],
+                   mode=mode, h_true=hh, solve=solve, partition_r=int(partition_r))
+    return _finish(res, verbose, itera)
+
+
+def em_pm(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera, h_initial, h,
+          n_tx, partition_r, X_d, qamCons, verbose=False, solve="drop"):
+    """Partitioned list-detector EM, every list member weight 1 (PMd/PM.py:47-116).
+
+    The list of M**(p+1) candidates (p = int(partition_r / log2 M)) is built per
+    symbol from the reference's off-by-one channel (PM.py:63) with greedy stream
+    ordering and per-element slicing of the B partition; the candidate vector is
+    the concatenation [x_A, x_B] used in natural stream order (PM.py:101-104).
+    ``h`` drives the reference's oracle early stop (PM.py:110-112) when given;
+    ``X_d`` is accepted for signature parity (the reference only reads its
+    length).  ``all_possibleSymbols`` may be None (n_tx = 8 makes it 4.3e9 rows).
+    The reference solves with lstsq (PM.py:108); solve='drop' is its device
+    counterpart (identical on HPD systems)."""
+    return _pm(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera,
+               h_initial, h, n_tx, partition_r, qamCons, "pm", solve, verbose)
+
+
+def em_pm_soft(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, M, varn, itera, h_initial, h, n_tx,
+               partition_r, X_d, qamCons, verbose=False, solve="chol"):
+    """Partitioned list-detector EM with posterior list weights
+    exp(-||y - H_t x||^2 / varn^2), normalised over the list (PMd/PM_beta.py:42-112;
+    the same signature as PM_beta.em_pm, which takes no all_possibleSymbols)."""
+    return _pm(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, None, M, varn, itera, h_initial, h, n_tx,
+               partition_r, qamCons, "pm_soft", solve, verbose)
+
+
 def em_zero_init(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera):
     """Root-level em() (Proposed_method_NMSEvsTp.py:43-69): theta_0 = 0."""
     return em(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera, None)
 
 
 # ------------------------------------------------------------------ diagnostic stages
-def _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn):
+def _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn, partition_r=0):
     def dev(x):
         return _dev(torch, x, np.complex128)
     Yd, Yp, Ps, Up, Cs, Th = (dev(y_d), dev(y_p), dev(psi_d), dev(u_p), dev(cons), dev(theta))
     B, T_d, n_rx = Yd.shape
     T_p, P, L = Yp.shape[1], Ps.shape[2], Up.shape[2]
     n_tx = L // P
-    dims = _lib.Dims(B, n_tx, n_rx, P, T_p, T_d, Cs.shape[0], 0, float(varn))
+    dims = _lib.Dims(B, n_tx, n_rx, P, T_p, T_d, Cs.shape[0], int(partition_r), float(varn))
     ws = torch.empty(max(_lib.workspace_bytes(dims), 16), dtype=torch.uint8, device="cuda")
     status = torch.zeros(B, dtype=torch.int32, device="cuda")
     ptrs = _lib.Ptrs(Yd.data_ptr(), Yp.data_ptr() if T_p else Yd.data_ptr(), Ps.data_ptr(),
@@ -219,7 +270,7 @@ def _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn):
     return dims, ptrs, keep
 
 
-def estep_batch(y_d, psi_d, cons, theta, varn, n_tx, mode="soft"):
+def estep_batch(y_d, psi_d, cons, theta, varn, n_tx, mode="soft", partition_r=0):
     """One device E-step (sbce_estep): returns m (B,T_d,n_tx), S (B,T_d,n_tx,n_tx)."""
     torch = _torch()
     lib = _lib.load()
@@ -227,7 +278,7 @@ def estep_batch(y_d, psi_d, cons, theta, varn, n_tx, mode="soft"):
     P = np.shape(psi_d)[2]
     y_p = np.zeros((B, 0, n_rx), dtype=complex)
     u_p = np.zeros((B, 0, P * n_tx), dtype=complex)
-    dims, ptrs, keep = _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn)
+    dims, ptrs, keep = _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn, partition_r)
     mom = torch.zeros((B, T_d, n_tx + n_tx * n_tx), dtype=torch.complex128, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
     _lib.check(lib.sbce_estep(dims, ptrs, _MODES[mode], mom.data_ptr(), stream), "sbce_estep")
@@ -282,7 +333,8 @@ class EMEngine:
     synchronised inside ``run()``.
     """
 
-    def __init__(self, batch, varn, mode="soft", solve="chol", x_d_true=None, h_true=None):
+    def __init__(self, batch, varn, mode="soft", solve="chol", x_d_true=None, h_true=None,
+                 partition_r=0):
         torch = _torch()
         self.torch = torch
         self.lib = _lib.load()
@@ -304,7 +356,7 @@ class EMEngine:
         self.n_tx, self.n_rx, self.B, self.T_d, self.T_p, self.P = L // P, n_rx, B, T_d, T_p, P
         self.M = self.cons.shape[0]
         self.varn = float(varn)
-        self.dims = _lib.Dims(B, self.n_tx, n_rx, P, T_p, T_d, self.M, 0, self.varn)
+        self.dims = _lib.Dims(B, self.n_tx, n_rx, P, T_p, T_d, self.M, int(partition_r), self.varn)
         self.ws = torch.empty(max(_lib.workspace_bytes(self.dims), 16), dtype=torch.uint8,
                               device="cuda")
         self.status = torch.zeros(B, dtype=torch.int32, device="cuda")

@@ -20,17 +20,26 @@ def cons_from_aps(all_possibleSymbols, M):
 
 
 def check_structure(Z_p, U_p, n_rx, aps, cons, K):
-    """Reject inputs that the reduced form would silently mis-handle."""
-    aps = np.asarray(aps)
-    n_tx = aps.shape[1]
+    """Reject inputs that the reduced form would silently mis-handle.
+    ``aps`` may be None (list detectors never enumerate M**n_tx hypotheses)."""
     M = cons.size
     if M & (M - 1):
         raise ValueError("constellation size must be a power of two")
+    if aps is not None:
+        _check_aps(np.asarray(aps), cons, M)
+    _check_zp(Z_p, U_p, n_rx, K)
+
+
+def _check_aps(aps, cons, M):
+    n_tx = aps.shape[1]
     if aps.shape[0] != M ** n_tx:
         raise ValueError("all_possibleSymbols must hold all M**n_tx hypotheses")
     idx = np.indices((M,) * n_tx).reshape(n_tx, -1).T
     if not np.array_equal(aps, cons[idx]):
         raise ValueError("all_possibleSymbols is not in itertools.product order of one constellation")
+
+
+def _check_zp(Z_p, U_p, n_rx, K):
     if len(Z_p):
         Z0 = np.asarray(Z_p[0])
         if Z0.shape != (n_rx, K):

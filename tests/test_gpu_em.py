@@ -251,3 +251,79 @@ def test_sweep_scripts_run(sbce, script, args, rows, tmp_path):
     for key in d.files:
         if key != "x":
             assert np.isfinite(d[key]).all()
+
+
+# ---------------------------------------------------------------- PM list detectors
+PM_CASES = [("kat1_s7", "pm_r0_theta", "pm", 0, 3), ("kat1_s7", "pmbeta_r1_theta", "pm_soft", 1, 3),
+            ("pm_nt4", "pm_theta", "pm", None, None), ("pm_nt4", "pmbeta_theta", "pm_soft", None, None),
+            ("pm_nt3_m16", "pm_theta", "pm", None, None),
+            ("pm_nt3_m16", "pmbeta_theta", "pm_soft", None, None)]
+
+
+@pytest.mark.parametrize("case,key,mode,r,itera", PM_CASES)
+def test_em_pm_matches_reference(sbce, case, key, mode, r, itera):
+    """PM.em_pm / PM_beta.em_pm (reference signatures) vs the reference outputs, incl.
+    the oracle early stop on h."""
+    d = golden(case)
+    Y_d, Y_p, Z_p = ref_lists(d)
+    n_tx, M = int(d["n_tx"]), int(d["M"])
+    if r is None:
+        r = int(d["r_soft"] if mode == "pm_soft" else d["r_uniform"])
+        itera = int(d["itera"])
+    cons = cons_from_aps(d["aps"], M)
+    args = (Y_d, Y_p, int(d["T_d"]), int(d["T_p"]), Z_p, d["Ptd"])
+    tail = (float(d["varn"]), itera, d["h0"].reshape(-1, 1), d["h"].reshape(-1, 1), n_tx, r,
+            d["X_d"], cons)
+    if mode == "pm":
+        th = sbce.em_pm(*args, d["aps"], M, *tail)
+    else:
+        th = sbce.em_pm_soft(*args, M, *tail)
+    assert th.shape == (d[key].size, 1)
+    assert rel(th, d[key]) < THETA_TOL
+
+
+@pytest.mark.parametrize("shape", [
+    # (n_tx, n_rx, N, T_p, T_d, M, snr_db, partition_r)
+    (2, 2, 4, 8, 24, 4, 20, 0),
+    (3, 4, 3, 8, 24, 16, 15, 1),
+    (4, 4, 3, 8, 20, 4, 10, 4),       # p = 2: list of 64
+    (5, 6, 2, 12, 16, 4, 20, 2),
+    (6, 6, 2, 12, 16, 16, 20, 4),     # p = 1: a list of 16^2 = 256 > 64 is rejected (EUNSUPPORTED)
+    (8, 8, 2, 24, 16, 16, 20, 1),     # BASELINE cfg 2 list detector (n_tx = n_rx = 8, 16-QAM)
+    (8, 8, 2, 24, 16, 16, 0, 1),
+    (7, 8, 1, 16, 12, 64, 25, 0),
+])
+def test_pm_estep_moments_vs_oracle(sbce, shape):
+    """Device PM E-step (uniform and posterior list weights) vs the oracle's pm_moments."""
+    from oracle.pm import pm_moments
+    n_tx, n_rx, N, T_p, T_d, M, snr, r = shape
+    varn = float(sbce.signal_model.snr_to_varn(snr))
+    b = sbce.signal_model.synthetic_batch(2, n_tx, n_rx, N, T_p, T_d, M, varn, seed=5)
+    lm = int(np.log2(M))
+    if (int(r / np.log2(M)) + 1) * lm > 6:
+        with pytest.raises(sbce.SbceError):
+            sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx, "pm", r)
+        return
+    scale = np.abs(b["cons"]).max() ** 2
+    for mode, soft in (("pm", False), ("pm_soft", True)):
+        m, S = sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx, mode, r)
+        for i in range(2):
+            m0, S0 = pm_moments(b["theta0"][i], b["y_d"][i], b["psi_d"][i].T, b["cons"], n_tx,
+                                n_rx, r, varn, soft)
+            nlist = 1 if soft else M ** (int(r / np.log2(M)) + 1)
+            assert np.abs(m[i] - m0).max() < 1e-11 * scale * nlist
+            assert np.abs(S[i] - S0).max() < 1e-11 * scale * nlist
+
+
+def test_pm_soft_full_em_cfg2_geometry_vs_oracle(sbce):
+    """n_tx = n_rx = 8, 16-QAM, PM_beta r = 1 (the BASELINE cfg 2 estimator) at a small
+    RIS: full EM on the device vs the oracle, batched."""
+    from oracle.pm import em_pm
+    n_tx, n_rx, N, T_p, T_d, M, varn, itera = 8, 8, 4, 48, 64, 16, 0.05, 3
+    b = sbce.signal_model.synthetic_batch(3, n_tx, n_rx, N, T_p, T_d, M, varn, seed=9)
+    res = sbce.em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, itera,
+                        b["theta0"], mode="pm_soft", partition_r=1)
+    for i in range(3):
+        th = em_pm(b["y_d"][i], b["y_p"][i], b["u_p"][i], b["psi_d"][i].T, varn, itera,
+                   b["theta0"][i], n_tx, n_rx, 1, b["cons"], soft=True)
+        assert rel(res["theta"][i], th) < 1e-9
