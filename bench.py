@@ -82,8 +82,12 @@ def cpu_baseline(cfg, varn, seed, iters=2):
     em_reduced(b["y_d"][0], b["y_p"][0], b["u_p"][0], b["psi_d"][0].T, aps, varn, iters,
                b["theta0"][0])
     dt = time.perf_counter() - t0
-    cores = len(os.sched_getaffinity(0))
     threads = os.environ.get("OMP_NUM_THREADS")
+    # threads actually usable by the port: NumPy elementwise work is single-threaded,
+    # BLAS calls use up to OMP_NUM_THREADS (16 on the GPU box), never more than the affinity
+    cores = len(os.sched_getaffinity(0))
+    if threads and threads.isdigit():
+        cores = min(cores, int(threads))
     return {"value": iters / dt, "unit": "EM-iterations/s", "cores": cores,
             "kind": "port",
             "sample": f"1 trial x {iters} EM iterations of the same config, oracle/em_reduced.py "
@@ -207,7 +211,8 @@ def main():
         "nmse_mean": nmse_mean,
         "nonhpd_trials": nonhpd,
         "kernels_ms": {"estep": estep_ms, "mstep_build_plus_solve": mstep_ms},
-        "roofline": {"bound": "fp64", "pipe": "VALU (FP64 vector)", "kernel": "estep_kernel",
+        "roofline": {"bound": "mfma", "pipe": "FP64 MFMA v_mfma_f64_16x16x4f64 (+ FP64 VALU)",
+                     "kernel": "estep_mfma_kernel",
                      "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "algorithmic_bytes": algo_bytes,
