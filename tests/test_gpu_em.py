@@ -327,3 +327,34 @@ def test_pm_soft_full_em_cfg2_geometry_vs_oracle(sbce):
         th = em_pm(b["y_d"][i], b["y_p"][i], b["u_p"][i], b["psi_d"][i].T, varn, itera,
                    b["theta0"][i], n_tx, n_rx, 1, b["cons"], soft=True)
         assert rel(res["theta"][i], th) < 1e-9
+
+
+@pytest.mark.parametrize("shape", [
+    # (n_tx, n_rx, N, T_p, T_d)  ->  L = (N+1) n_tx
+    (2, 2, 8, 12, 40),        # L = 18: one full + one partial panel
+    (3, 5, 20, 16, 60),       # L = 63: partial last panel (w = 15)
+    (4, 4, 64, 16, 256),      # L = 260: BASELINE cfg 1
+    (4, 8, 127, 16, 200),     # L = 512: largest MFMA Cholesky shape, 8 RHS
+    (1, 1, 40, 8, 80),        # L = 41, single RHS
+])
+def test_mfma_and_valu_cholesky_agree(sbce, shape, monkeypatch):
+    """The MFMA and the VALU blocked Cholesky solve the same normal equations, and both
+    match numpy.linalg.solve of the R, rhs the device built."""
+    n_tx, n_rx, N, T_p, T_d = shape
+    b = sbce.signal_model.synthetic_batch(2, n_tx, n_rx, N, T_p, T_d, 4, 0.05, seed=4)
+    x = b["x_d"]
+    m = x
+    S = x[..., :, None] * np.conj(x[..., None, :]) + 0.1 * np.eye(n_tx)
+    out = {}
+    for impl in ("mfma", "valu"):
+        monkeypatch.setenv("SBCE_CHOL_IMPL", impl)
+        out[impl] = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], m, S, 0.05)
+    th_m, R, rhs, st = out["mfma"]
+    th_v = out["valu"][0]
+    assert not st.any()
+    for i in range(2):
+        X = np.linalg.solve(R[i], rhs[i])                     # R X = B^H, theta = conj(X)
+        ref = np.conj(X).reshape(-1)
+        assert rel(th_m[i], ref) < 1e-9
+        assert rel(th_v[i], ref) < 1e-9
+    assert rel(th_m, th_v) < 1e-9
