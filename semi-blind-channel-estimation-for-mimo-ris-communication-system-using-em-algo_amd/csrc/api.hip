@@ -179,6 +179,13 @@ int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int 
     return hip_rc(launch_chol_solve(pb, ma, s));
 }
 
+// Diagnostic, not part of include/sbce.h: per-phase cycle sums (32) of the MFMA Cholesky
+// (SBCE_CHOL_SKIP bit 64); reset != 0 clears them.
+int sbce_debug_chol_clock(unsigned long long* out32, int reset) {
+    if (reset) return hip_rc(chol_debug_clock_reset());
+    return out32 ? hip_rc(chol_debug_clock(out32)) : SBCE_EINVAL;
+}
+
 int sbce_nmse(const sbce_dims* d, const void* theta, const void* h_true, double* nmse_out,
               void* hip_stream) {
     Problem pb;

@@ -163,6 +163,7 @@ __device__ __forceinline__ double prologue(const cd* R, const cd* rhs, cd* y, do
     __syncthreads();
     double tol = 0.0;
     for (int w = 0; w < (nth >> 6); ++w) tol = fmax(tol, red[w]);
+    __syncthreads();                                 // red[] is reused afterwards
     return tol * 1e-14;
 }
 
@@ -281,181 +282,317 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
 // Tile tau (rows jb + 16 tau ..) of panel jb belongs to wave tau % nw, slot tau / nw.
 // Lane l of a 16 x 16 f64 MFMA: A[i = l&15][k = l>>4], B[k = l>>4][j = l&15],
 // C/D value q at row (l>>4) + 4q, column l&15.
-constexpr int KCM = 16;                // k-chunk: A prefetched to registers, B staged in LDS
-constexpr int KCP = KCM + 1;           // padded LDS row (complex) of the B block
+constexpr int KCM = 16;                // k-chunk of the A-operand register pipeline
+
+// 1/sqrt(x) for x > 0 in ~10 dependent VALU ops instead of the ~25 of the IEEE sqrt +
+// division sequences (whose latency sets the pace of the column chain): exponent split,
+// v_rsq_f32 seed on the mantissa, two f64 Newton steps (2^-24 -> 2^-48 -> ~1 ulp).
+__device__ __forceinline__ double fast_rsqrt(double x) {
+    const int e = __builtin_amdgcn_frexp_exp(x);          // x = m 2^e, m in [0.5, 1)
+    const int h = e >> 1;
+    const double xs = __builtin_amdgcn_ldexp(x, -2 * h);  // in [0.5, 2)
+    double y = (double)__builtin_amdgcn_rsqf((float)xs);
+    double r = fma(-xs * y, y, 1.0);
+    y = fma(0.5 * y, r, y);
+    r = fma(-xs * y, y, 1.0);
+    y = fma(0.5 * y, r, y);
+    return __builtin_amdgcn_ldexp(y, -h);
+}
 
 // One-wave factorisation of the w x w diagonal block held in LDS A[16][16] (lower part
-// valid; lane l owns entries (row (l>>4) + 4h, col l&15), h < 4 -- few registers, so the
-// MFMA update loop keeps its occupancy), then Di = D^{-1} by columns (lane j < 16, forward
-// substitution from LDS).  Writes Di to LDS and the factor rows + conj(Di) (strict upper)
-// into R's diagonal block.
+// valid).  Lane l owns entries (row (l>>4) + 4h, col l&15), h < 4.  Column c costs ONE
+// LDS round trip: every lane reads the pivot and the column entries it needs, then
+//   L[r][c] = A[r][c] / p,   A[r][c2] -= A[r][c] conj(A[c2][c]) / p^2   (r >= c2 > c)
+// are written together (the trailing update uses the unscaled column, so no second
+// pass).  Di = D^{-1} then goes row by row, four lanes per column j splitting the
+// sum over m (reduced by two xor-shuffles): 16 dependent steps of one round trip each.
+// Few registers, so the MFMA update loop keeps its occupancy.  Writes Di to LDS and the
+// factor rows + conj(Di) (strict upper) into R's diagonal block.
 __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double tol,
-                                                int solve_mode, cd* Di, int* flag, cd* Rdiag,
-                                                int L) {
+                                                int solve_mode, cd* Di, double* dinv, int* flag,
+                                                cd* Rdiag, int L,
+                                                unsigned long long* clk = nullptr) {
     const int col = lane & 15, r0 = lane >> 4;
+    unsigned long long tc = clk ? __builtin_amdgcn_s_memtime() : 0;
     bool bad_any = false;
+    // Branch-free: every entry (r, col) has exactly one owner lane, which rewrites it each
+    // column (unchanged entries get their old value back); divergent branches in this
+    // single-wave dependent chain cost more than the arithmetic.
 #pragma unroll 1
     for (int c = 0; c < w; ++c) {
         const double dia = A[c * NB + c].x;
+        const cd lc = A[col * NB + c];                      // A[col][c] (unscaled)
+        cd arc[4], arx[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const int r = r0 + 4 * h;
+            arc[h] = A[r * NB + c];
+            arx[h] = A[r * NB + col];
+        }
         const bool bad = !(dia > tol);
         bad_any |= bad;
         const bool drop = bad && solve_mode == SBCE_SOLVE_CHOL_DROP;
-        const double piv = sqrt(bad ? tol : dia);
-        const double inv = drop ? 0.0 : 1.0 / piv;
-        wave_sync();
-        if (col == c) {
+        const double pv = bad ? tol : dia;
+        const double rs = fast_rsqrt(pv);
+        const double piv = drop ? 0.0 : pv * rs;
+        const double inv = drop ? 0.0 : rs;
+        const cd lcs = cscale(cconj(lc), inv * inv);
+        if (clk && lane == 0) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); clk[9] += t2 - tc; tc = t2; }
+        wave_sync();                                         // all reads of column c done
+        dinv[c] = inv;                                       // same value from every lane
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                const int r = r0 + 4 * h;
-                if (r == c) A[c * NB + c] = cmk(drop ? 0.0 : piv, 0.0);
-                else if (r > c && r < w) A[r * NB + c] = cscale(A[r * NB + c], inv);
-            }
+        for (int h = 0; h < 4; ++h) {
+            const int r = r0 + 4 * h;
+            const bool isdiag = col == c && r == c;
+            const bool iscol = col == c && r > c && r < w;
+            const bool istrail = col > c && col < w && r >= col && r < w;
+            const cd upd = csub(arx[h], cmul(arc[h], lcs));
+            const cd scl = cscale(arc[h], inv);
+            cd v = csel(istrail, upd, arx[h]);
+            v = csel(iscol, scl, v);
+            v = csel(isdiag, cmk(piv, 0.0), v);
+            A[r * NB + col] = v;
         }
         wave_sync();
-        if (col > c && col < w) {
-            const cd lc = cconj(A[col * NB + c]);            // conj(L[col][c])
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                const int r = r0 + 4 * h;
-                if (r >= col && r < w) A[r * NB + col] = csub(A[r * NB + col], cmul(A[r * NB + c], lc));
-            }
-        }
-        wave_sync();
+        if (clk && lane == 0) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); clk[10] += t2 - tc; tc = t2; }
     }
-    if (bad_any && lane == 0) *flag = 1;
-    // Di[k][j] = (delta_kj - sum_{j<=m<k} L[k][m] Di[m][j]) / L[k][k]   (lane j, rows in order)
-    if (lane < NB) {
-        const int j = lane;
+    if (bad_any) *flag = 1;
+    if (clk && lane == 0) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); clk[0] += t2 - tc; tc = t2; }
+    // Di[k][j] = (delta_kj - sum_{j<=m<k} L[k][m] Di[m][j]) / L[k][k]; lane = (j, part)
+    {
+        const int j = lane & 15, part = lane >> 4;
 #pragma unroll 1
         for (int k = 0; k < NB; ++k) {
-            cd acc = (k == j) ? cmk(1.0, 0.0) : czero();
-#pragma unroll 4
-            for (int m = j; m < k; ++m) acc = csub(acc, cmul(A[k * NB + m], Di[m * NB + j]));
-            const double lkk = (k < w) ? A[k * NB + k].x : 0.0;
-            const double inv = lkk > 0.0 ? 1.0 / lkk : 0.0;
-            Di[k * NB + j] = (k < w && j <= k && j < w) ? cscale(acc, inv) : czero();
+            cd acc = czero();
+#pragma unroll
+            for (int mm = 0; mm < 4; ++mm) {
+                const int m = part + 4 * mm;
+                const bool on = m >= j && m < k;
+                const cd lkm = A[k * NB + m], dmj = Di[m * NB + j];
+                acc = cfma(acc, csel(on, lkm, czero()), csel(on, dmj, czero()));
+            }
+            acc.x += shfl_xor_d(acc.x, 16); acc.y += shfl_xor_d(acc.y, 16);
+            acc.x += shfl_xor_d(acc.x, 32); acc.y += shfl_xor_d(acc.y, 32);
+            const double inv = (k < w) ? dinv[k] : 0.0;     // 0 for dropped directions
+            const cd v = csel(k == j, cmk(1.0, 0.0), cmk(-acc.x, -acc.y));
+            Di[k * NB + j] = csel(k < w && j <= k && j < w, cscale(v, inv), czero());   // 4 lanes, same value
+            wave_sync();
         }
     }
-    wave_sync();
+    if (clk && lane == 0) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); clk[1] += t2 - tc; tc = t2; }
     // factor rows (c <= r) and conj(Di[c][r]) (c > r) into R's diagonal block
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
         const int r = r0 + 4 * h;
         if (r < w && col < w)
-            Rdiag[(size_t)r * L + col] = (col <= r) ? A[r * NB + col] : cconj(Di[col * NB + r]);
+            Rdiag[(size_t)r * L + col] = csel(col <= r, A[r * NB + col], cconj(Di[col * NB + r]));
+    }
+    if (clk && lane == 0) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); clk[8] += t2 - tc; }
+}
+
+// Blocked back substitution L^H x = y for the MFMA kernel: every thread owns column
+// k = tid (+ nth) of the update and loads its 16 factor entries BEFORE the barrier that
+// publishes the block solution, so each block pays one memory latency, not three.
+__device__ __forceinline__ void back_substitute_pf(const cd* R, cd* y, int L, int NR, int tid,
+                                                   int nth, int lane, int wave, int kb_stop) {
+    const int nblk = (L + NB - 1) / NB;
+    for (int kb = nblk - 1; kb >= kb_stop; --kb) {
+        const int k0 = kb * NB;
+        const int w = (L - k0) < NB ? (L - k0) : NB;
+        // prefetch: conj(L[k0+c][k]) for this thread's columns k < k0
+        cd lv[2][NB];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int k = tid + h * nth;
+#pragma unroll
+            for (int c = 0; c < NB; ++c)
+                lv[h][c] = (k < k0 && c < w) ? R[(size_t)(k0 + c) * L + k] : czero();
+        }
+        if (wave == 0) {
+            // x_blk = D^{-H} z_blk:  x[c] = z[c] / L[c][c] + sum_{c2>c} conj(Di[c2][c]) z[c2]
+            const int e0 = lane, e1 = lane + 64;
+            cd t0 = czero(), t1 = czero();
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int e = h ? e1 : e0;
+                if (e < w * NR) {
+                    const int c = e / NR, r = e - c * NR;
+                    const cd* Rc = R + (size_t)(k0 + c) * L + k0;
+                    const double lcc = Rc[c].x;
+                    cd acc = (lcc > 0.0) ? cscale(y[(k0 + c) * NR + r], 1.0 / lcc) : czero();
+                    for (int c2 = c + 1; c2 < w; ++c2) acc = cfma(acc, Rc[c2], y[(k0 + c2) * NR + r]);
+                    if (h) t1 = acc; else t0 = acc;
+                }
+            }
+            wave_sync();
+            if (e0 < w * NR) y[k0 * NR + e0] = t0;
+            if (e1 < w * NR) y[k0 * NR + e1] = t1;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int k = tid + h * nth;
+            if (k < k0) {
+                for (int r = 0; r < NR; ++r) {
+                    cd acc = y[k * NR + r];
+#pragma unroll
+                    for (int c = 0; c < NB; ++c)
+                        if (c < w) acc = csub(acc, cmulc(y[(k0 + c) * NR + r], lv[h][c]));
+                    y[k * NR + r] = acc;
+                }
+            }
+        }
+        __syncthreads();
     }
 }
 
-template <int MAXT, bool YLDS>
-__global__ __launch_bounds__(512) void chol_mfma_kernel(MstepArgs a, int L, int NR) {
+// DIAGNOSTIC (skip & 64): per-phase s_memtime sums of waves 0 and 1 of block 0
+__device__ unsigned long long g_chol_clk[32];
+
+template <int MAXT, bool YLDS, int NWB, int KB>
+__global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(2)))
+void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip) {
+    constexpr int KBP = KB + 1;                 // padded LDS row (complex) of the panel block
+    // skip: DIAGNOSTIC phase mask (timing only, results invalid): 1 update, 2 diag factor,
+    // 8 trsm tiles, 16 back substitution
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, nth = blockDim.x;
     const int lane = tid & 63, nw = nth >> 6;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR) tile ids
-    cd* Bt = reinterpret_cast<cd*>(smem);       // [NB][KCP]  top block of the k-chunk
-    cd* Di = Bt + NB * KCP;                     // [NB][NB]
-    cd* Xd = Di + NB * NB;                      // [NB][NB]   diagonal tile hand-off
-    double* red = reinterpret_cast<double*>(Xd + NB * NB);   // [16]
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform tile ids
+    cd* Bp = reinterpret_cast<cd*>(smem);       // [NB][KBP]  panel top rows, one k-block
+    cd* Di = Bp + NB * KBP;                     // [NB][NB]
+    cd* Xs = Di + NB * NB;                      // [nw][NB][NB] per-wave tile scratch
+    double* red = reinterpret_cast<double*>(Xs + nw * NB * NB);   // [16]
     int* flag = reinterpret_cast<int*>(red + 16);
     cd* ylds = reinterpret_cast<cd*>(red + 18);
     cd* R = a.R + (size_t)b * L * L;
     cd* y = YLDS ? ylds : a.rhs + (size_t)b * L * NR;
+    cd* X = Xs + wave * NB * NB;
     const double tol = prologue<YLDS>(R, a.rhs + (size_t)b * L * NR, y, red, flag, L, NR, tid,
                                       nth, lane, wave);
     const int li = lane & 15, lk = lane >> 4;
+    const bool clk = (skip & 64) && b == 0 && wave < 2 && lane == 0;
+    unsigned long long tclk = clk ? __builtin_amdgcn_s_memtime() : 0;
+#define SBCE_CLK(ph)                                                          \
+    if (clk) {                                                                \
+        const unsigned long long t2 = __builtin_amdgcn_s_memtime();           \
+        g_chol_clk[wave * 8 + (ph)] += t2 - tclk;                             \
+        tclk = t2;                                                            \
+    }
 
     for (int jb = 0; jb < L; jb += NB) {
         const int w = (L - jb) < NB ? (L - jb) : NB;
         const int ntile = (L - jb + NB - 1) / NB;
-        // ---- update of this wave's tiles, written back in place (R[rows, jb:jb+16]) ----
-        if (jb > 0) {
-            d4v cre[MAXT], cim[MAXT];
+        const int nact = (ntile - wave + nw - 1) / nw;     // active tile slots of this wave
+        // A-operand rows of this wave's tiles (rows past L read row L-1: harmless)
+        const cd* arow[MAXT];
 #pragma unroll
-            for (int u = 0; u < MAXT; ++u) {
-                const int tau = wave + u * nw;
+        for (int u = 0; u < MAXT; ++u) {
+            int r = jb + (wave + u * nw) * NB + li;
+            r = r < L ? r : L - 1;
+            arow[u] = R + (size_t)r * L + lk;
+        }
+        // ---- C tiles <- A[rows, jb:jb+16] (C layout) ----
+        d4v cre[MAXT], cim[MAXT];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int r = jb + tau * NB + lk + 4 * q;
-                    cd v = czero();
-                    if (tau < ntile && r < L && li < w) v = R[(size_t)r * L + jb + li];
-                    cre[u][q] = v.x;
-                    cim[u][q] = v.y;
-                }
+        for (int u = 0; u < MAXT; ++u) {
+            const int tau = wave + u * nw;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int r = jb + tau * NB + lk + 4 * q;
+                cd v = czero();
+                if (tau < ntile && r < L && li < w) v = R[(size_t)r * L + jb + li];
+                cre[u][q] = v.x;
+                cim[u][q] = v.y;
             }
-            for (int k0 = 0; k0 < jb; k0 += KCM) {
-                cd av[MAXT][KCM / 4];
+        }
+        // ---- left-looking update over k-blocks of KBMAX columns: the panel's top rows
+        //      are staged once per block; each wave streams its tiles' rows with the next
+        //      16-column chunk's loads in flight while the current chunk's MFMAs run ----
+        for (int kb0 = 0; kb0 < ((skip & 1) ? 0 : jb); kb0 += KB) {
+            const int kbs = (jb - kb0) < KB ? (jb - kb0) : KB;         // multiple of 16
+            cd av[MAXT][4];
 #pragma unroll
-                for (int u = 0; u < MAXT; ++u) {
-                    int r = jb + (wave + u * nw) * NB + li;
-                    r = r < L ? r : L - 1;                // rows past L: harmless duplicates
-                    const cd* ar = R + (size_t)r * L + k0 + lk;
+            for (int u = 0; u < MAXT; ++u)
 #pragma unroll
-                    for (int s = 0; s < KCM / 4; ++s)
-                        av[u][s] = (wave + u * nw < ntile) ? ar[4 * s] : czero();
+                for (int s2 = 0; s2 < 4; ++s2) av[u][s2] = arow[u][kb0 + 4 * s2];
+            __syncthreads();
+            for (int e = tid; e < NB * kbs; e += nth) {
+                const int c = e / kbs, k = e - c * kbs;
+                Bp[c * KBP + k] = (c < w) ? R[(size_t)(jb + c) * L + kb0 + k] : czero();
+            }
+            __syncthreads();
+            for (int k0 = 0; k0 < kbs; k0 += KCM) {
+                // register pipeline (next chunk's loads in flight) only where the registers
+                // allow it; MAXT >= 4 relies on the second resident workgroup instead
+                constexpr bool PIPE = MAXT <= 3;
+                cd an[PIPE ? MAXT : 1][4];
+                const bool more = k0 + KCM < kbs;
+                if (PIPE) {
+#pragma unroll
+                    for (int u = 0; u < MAXT; ++u)
+#pragma unroll
+                        for (int s2 = 0; s2 < 4; ++s2)
+                            an[PIPE ? u : 0][s2] = more ? arow[u][kb0 + k0 + KCM + 4 * s2] : czero();
+                } else if (k0 > 0) {
+#pragma unroll
+                    for (int u = 0; u < MAXT; ++u)
+#pragma unroll
+                        for (int s2 = 0; s2 < 4; ++s2) av[u][s2] = arow[u][kb0 + k0 + 4 * s2];
                 }
-                __syncthreads();
-                for (int e = tid; e < NB * KCM; e += nth) {
-                    const int c = e / KCM, k = e - c * KCM;
-                    Bt[c * KCP + k] = (c < w) ? R[(size_t)(jb + c) * L + k0 + k] : czero();
-                }
-                __syncthreads();
 #pragma unroll
-                for (int s = 0; s < KCM / 4; ++s) {
-                    const cd t = Bt[li * KCP + 4 * s + lk];
+                for (int s2 = 0; s2 < 4; ++s2) {
+                    const cd t = Bp[li * KBP + k0 + 4 * s2 + lk];
 #pragma unroll
                     for (int u = 0; u < MAXT; ++u) {
-                        // unconditional (idle slots multiply zeros): a branch around an MFMA
-                        // chain makes the compiler copy the accumulators at every join
+                        if (u >= nact) break;          // wave-uniform (SGPR) bound: no exec masking
                         // re -= ar tr + ai ti ;  im -= ai tr - ar ti
-                        const cd v = av[u][s];
+                        const cd v = av[u][s2];
                         cre[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre[u], 0, 0, 0);
                         cre[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre[u], 0, 0, 0);
                         cim[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim[u], 0, 0, 0);
                         cim[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim[u], 0, 0, 0);
                     }
                 }
-            }
-            __syncthreads();    // every wave is done reading R[jb.., 0:jb] and R[jb..jb+16, ..]
+                if (PIPE) {
 #pragma unroll
-            for (int u = 0; u < MAXT; ++u) {
-                const int tau = wave + u * nw;
+                    for (int u = 0; u < MAXT; ++u)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int r = jb + tau * NB + lk + 4 * q;
-                    if (tau < ntile && r < L && li < w)
-                        R[(size_t)r * L + jb + li] = cmk(cre[u][q], cim[u][q]);
+                        for (int s2 = 0; s2 < 4; ++s2) av[u][s2] = an[PIPE ? u : 0][s2];
                 }
             }
-            __syncthreads();
         }
-        // ---- diagonal tile: wave 0 ----
+        SBCE_CLK(0)
+        // ---- diagonal tile (tau = 0: wave 0, slot 0), factored in LDS ----
         if (wave == 0) {
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                const int r = lk + 4 * h;
-                Xd[r * NB + li] = (r < w && li < w) ? R[(size_t)(jb + r) * L + jb + li] : czero();
-            }
+            for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = cmk(cre[0][q], cim[0][q]);
             wave_sync();
-            factor_diag_lds(Xd, w, lane, tol, a.solve_mode, Di, flag, R + (size_t)jb * L + jb, L);
+            if (!(skip & 2))
+                factor_diag_lds(X, w, lane, tol, a.solve_mode, Di, red, flag,
+                                R + (size_t)jb * L + jb, L, clk ? g_chol_clk + 6 : nullptr);
             forward_y_block(Di, y + jb * NR, w, NR, lane);
         }
+        SBCE_CLK(1)
         __syncthreads();
-        // ---- TRSM X = C D^{-H} for the other tiles, computed as X^T = conj(Di) C^T so the
-        //      C operand loads straight from R; lane (li, lk) ends with X[li][lk + 4q] ----
+        SBCE_CLK(2)
+        // ---- TRSM X = C D^{-H} for the other tiles, as X^T = conj(Di) C^T (C transposed
+        //      through the wave's LDS scratch); lane (li, lk) ends with X[li][lk + 4q] ----
 #pragma unroll
         for (int u = 0; u < MAXT; ++u) {
             const int tau = wave + u * nw;
-            if (tau == 0 || tau >= ntile) continue;
+            if (tau == 0 || tau >= ntile || (skip & 8)) continue;
             const int row0 = jb + tau * NB;
-            const int ri = row0 + li < L ? row0 + li : L - 1;
-            cd* crow = R + (size_t)ri * L + jb;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = cmk(cre[u][q], cim[u][q]);
+            wave_sync();
             d4v xre = {0.0, 0.0, 0.0, 0.0}, xim = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int s = 0; s < NB / 4; ++s) {
-                const cd d = Di[li * NB + 4 * s + lk];     // A[j][k] = conj(Di[j][4s+k])
-                const cd c = crow[4 * s + lk];             // B[k][i] = C[i][4s+k]
+            for (int s2 = 0; s2 < NB / 4; ++s2) {
+                const cd d = Di[li * NB + 4 * s2 + lk];    // A[j][k] = conj(Di[j][4s+k])
+                const cd c = X[li * NB + 4 * s2 + lk];     // B[k][i] = C[i][4s+k]
                 // X^T = conj(Di) C^T:  re += dr cr + di ci ;  im += dr ci - di cr
                 xre = __builtin_amdgcn_mfma_f64_16x16x4f64(d.x, c.x, xre, 0, 0, 0);
                 xre = __builtin_amdgcn_mfma_f64_16x16x4f64(d.y, c.y, xre, 0, 0, 0);
@@ -463,6 +600,7 @@ __global__ __launch_bounds__(512) void chol_mfma_kernel(MstepArgs a, int L, int 
                 xim = __builtin_amdgcn_mfma_f64_16x16x4f64(-d.y, c.x, xim, 0, 0, 0);
             }
             const bool live = row0 + li < L;
+            cd* crow = R + (size_t)(live ? row0 + li : L - 1) * L + jb;
             cd xv[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -482,10 +620,15 @@ __global__ __launch_bounds__(512) void chol_mfma_kernel(MstepArgs a, int L, int 
                 p.x += shfl_xor_d(p.x, 32); p.y += shfl_xor_d(p.y, 32);
                 if (lk == 0 && live) y[(row0 + li) * NR + r] = csub(y[(row0 + li) * NR + r], p);
             }
+            wave_sync();
         }
+        SBCE_CLK(3)
         __syncthreads();
+        SBCE_CLK(4)
     }
-    back_substitute(R, y, L, NR, tid, nth, lane, wave, 0);
+    back_substitute_pf(R, y, L, NR, tid, nth, lane, wave, (skip & 16) ? (L + NB - 1) / NB : 0);
+    SBCE_CLK(5)
+#undef SBCE_CLK
     cd* th = a.theta + (size_t)b * L * NR;
     for (int e = tid; e < L * NR; e += nth) th[e] = cconj(y[e]);
     if (tid == 0 && a.status) a.status[b] |= *flag ? SBCE_STATUS_NONHPD : 0;
@@ -510,21 +653,51 @@ hipError_t launch_y(const Problem& pb, const MstepArgs& a, int nth, int rpt, siz
     return hipErrorInvalidValue;
 }
 
-template <bool YLDS>
-hipError_t launch_mfma_y(const Problem& pb, const MstepArgs& a, int nw, int maxt, size_t lds,
-                         hipStream_t s) {
+template <bool YLDS, int NWB, int KB>
+hipError_t launch_mfma_cfg(const Problem& pb, const MstepArgs& a, int nw, int maxt, size_t lds,
+                           hipStream_t s) {
+    const char* sk = getenv("SBCE_CHOL_SKIP");      // diagnostic only (see kernel)
+    const int skip = sk ? atoi(sk) : 0;
     const dim3 g(pb.B), blk(64 * nw);
+#define SBCE_CM(t)                                                                                \
+    case t:                                                                                       \
+        hipLaunchKernelGGL((chol_mfma_kernel<t, YLDS, NWB, KB>), g, blk, lds, s, a, pb.L, pb.NR,  \
+                           skip);                                                                 \
+        break;
     switch (maxt) {
-        case 1: hipLaunchKernelGGL((chol_mfma_kernel<1, YLDS>), g, blk, lds, s, a, pb.L, pb.NR); break;
-        case 2: hipLaunchKernelGGL((chol_mfma_kernel<2, YLDS>), g, blk, lds, s, a, pb.L, pb.NR); break;
-        case 3: hipLaunchKernelGGL((chol_mfma_kernel<3, YLDS>), g, blk, lds, s, a, pb.L, pb.NR); break;
-        case 4: hipLaunchKernelGGL((chol_mfma_kernel<4, YLDS>), g, blk, lds, s, a, pb.L, pb.NR); break;
+        SBCE_CM(1) SBCE_CM(2) SBCE_CM(3) SBCE_CM(4) SBCE_CM(5)
         default: return hipErrorInvalidValue;
     }
+#undef SBCE_CM
     return hipGetLastError();
 }
 
+// Geometry: L <= 320 -> 4-wave workgroups (two trials resident per CU, so one trial's serial
+// diagonal-block phase overlaps the other's MFMA update), up to 5 tiles per wave, 128-column
+// k-blocks; 320 < L <= 512 -> 8 waves, up to 4 tiles per wave, 256-column k-blocks.
+template <bool YLDS>
+hipError_t launch_mfma(const Problem& pb, const MstepArgs& a, size_t ybytes, hipStream_t s) {
+    const int ntile = (pb.L + NB - 1) / NB;
+    const bool small = ntile <= 20;
+    const int nwb = small ? 4 : 8, kb = small ? 128 : 256;
+    const int nw = ntile < nwb ? ntile : nwb;
+    const int maxt = (ntile + nw - 1) / nw;
+    const size_t lds = (size_t)(NB * (kb + 1) + NB * NB + nw * NB * NB) * sizeof(cd) +
+                       18 * sizeof(double) + (YLDS ? ybytes : 0);
+    if (small) return launch_mfma_cfg<YLDS, 4, 128>(pb, a, nw, maxt, lds, s);
+    return launch_mfma_cfg<YLDS, 8, 256>(pb, a, nw, maxt, lds, s);
+}
+
 }  // namespace
+
+hipError_t chol_debug_clock(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chol_clk), sizeof(g_chol_clk), 0,
+                               hipMemcpyDeviceToHost);
+}
+hipError_t chol_debug_clock_reset() {
+    static const unsigned long long z[32] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_chol_clk), z, sizeof(z), 0, hipMemcpyHostToDevice);
+}
 
 bool chol_supported(const Problem& pb) { return pb.L >= 1 && pb.L <= 1024; }
 
@@ -534,12 +707,8 @@ hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t 
     const char* impl = getenv("SBCE_CHOL_IMPL");    // "valu" forces the VALU kernel (A/B runs)
     const bool force_valu = impl && impl[0] == 'v';
     if (!force_valu && pb.L <= 512) {
-        const int ntile = (pb.L + NB - 1) / NB;
-        const int nw = ntile < 8 ? ntile : 8;
-        const int maxt = (ntile + nw - 1) / nw;
-        const size_t base = (size_t)(NB * KCP + 2 * NB * NB) * sizeof(cd) + 18 * sizeof(double);
-        if (ybytes <= 48 * 1024) return launch_mfma_y<true>(pb, a, nw, maxt, base + ybytes, s);
-        return launch_mfma_y<false>(pb, a, nw, maxt, base, s);
+        if (ybytes <= 24 * 1024) return launch_mfma<true>(pb, a, ybytes, s);
+        return launch_mfma<false>(pb, a, ybytes, s);
     }
     int nth = (pb.L + 63) / 64 * 64;
     if (nth > 512) nth = 512;

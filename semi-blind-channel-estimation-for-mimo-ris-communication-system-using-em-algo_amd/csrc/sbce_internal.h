@@ -42,6 +42,8 @@ __device__ __forceinline__ cd caxpy(cd acc, double s, cd a) {
     acc.x = fma(s, a.x, acc.x); acc.y = fma(s, a.y, acc.y); return acc;
 }
 __device__ __forceinline__ double cabs2(cd a) { return fma(a.x, a.x, a.y * a.y); }
+// c ? a : b per component (a ternary on the HIP vector struct can go through scratch)
+__device__ __forceinline__ cd csel(bool c, cd a, cd b) { return cmk(c ? a.x : b.x, c ? a.y : b.y); }
 
 // exp(z) for z <= ~0 (z may be -inf).  Cody-Waite reduction z = k ln2 + r,
 // |r| <= ln2/2, degree-12 Taylor polynomial in Horner form (truncation
@@ -115,6 +117,8 @@ bool estep_supported(const Problem& pb, int mode);
 hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s);
 bool chol_supported(const Problem& pb);
+hipError_t chol_debug_clock(unsigned long long* out);   // diagnostic (SBCE_CHOL_SKIP & 64)
+hipError_t chol_debug_clock_reset();
 hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* out,
                        hipStream_t s);
 hipError_t launch_llf(const Problem& pb, const cd* theta, const cd* yp, const cd* up,

@@ -30,7 +30,29 @@ def timeit(fn, reps=5):
     return e0.elapsed_time(e1) / reps
 
 
-for skip in (0, 1, 2, 4, 8, 16, 2 | 4 | 16, 31):
-    os.environ["SBCE_CHOL_SKIP"] = str(skip)
-    print(f"chol skip={skip:2d}: mstep {timeit(eng.mstep):.3f} ms", flush=True)
+for impl in ("mfma", "valu"):
+    os.environ["SBCE_CHOL_IMPL"] = impl
+    for skip in (0, 1, 2, 8, 16, 1 | 2 | 8 | 16):
+        os.environ["SBCE_CHOL_SKIP"] = str(skip)
+        print(f"chol {impl} skip={skip:2d}: mstep {timeit(eng.mstep):.3f} ms", flush=True)
 os.environ["SBCE_CHOL_SKIP"] = "0"
+os.environ["SBCE_CHOL_IMPL"] = "mfma"
+
+# per-phase s_memtime sums (block 0, waves 0/1) of one MFMA Cholesky launch
+import ctypes  # noqa: E402
+lib = pkg._lib.load()
+buf = (ctypes.c_ulonglong * 32)()
+lib.sbce_debug_chol_clock(buf, 1)
+os.environ["SBCE_CHOL_SKIP"] = "64"
+eng.mstep()
+torch.cuda.synchronize()
+os.environ["SBCE_CHOL_SKIP"] = "0"
+lib.sbce_debug_chol_clock(buf, 0)
+names = ["C init+update", "diag factor", "barrier after diag", "trsm tiles", "end barrier",
+         "back substitution"]
+for wv in range(2):
+    tot = sum(buf[wv * 8 + i] for i in range(6))
+    print(f"wave {wv}: " + ", ".join(f"{n} {buf[wv * 8 + i]}" for i, n in enumerate(names)) +
+          f"  total {tot} cycles", flush=True)
+print(f"wave 0 diag detail: column loop {buf[6]} (reads+pivot {buf[15]}, writes {buf[16]}), "
+      f"inverse {buf[7]}, R writes {buf[14]}", flush=True)
