@@ -42,7 +42,33 @@ CONFIGS = {
     # name: (n_tx, n_rx, N_RIS, T_p, T_d, M, trials per GPU, EM iterations)
     "cfg1": (4, 4, 64, 16, 256, 16, 1000, 20),
     "plumbing": (2, 2, 16, 16, 50, 4, 10, 10),
+    # BASELINE configs[2]: 10k trials over 8 GPUs; PM_beta list E-step r = 1
+    "cfg2": (8, 8, 256, 32, 1024, 16, 1250, 5),
+    # BASELINE configs[3]: T_p unstated -> 16, 16-QAM assumed (SURVEY §8 sizes table)
+    "cfg4": (4, 4, 1024, 16, 512, 16, 100, 5),
 }
+# E-step (mode, partition_r) and M-step solve of each workload.  cfg 2 / cfg 4 have
+# L > T_d + T_p (rank-deficient normal equations at high SNR): they use the drop
+# (lstsq-like, PM.py:108) solve; cfg 4 is a throughput-only workload.
+ESTEP = {"cfg1": ("soft", 0, "chol"), "plumbing": ("soft", 0, "chol"),
+         "cfg2": ("pm_soft", 1, "drop"), "cfg4": ("soft", 0, "drop")}
+
+
+def mstep_flops_per_trial_iter(n_tx, n_rx, N, T_p, T_d):
+    """Minimal M-step work: R build 4 P^2 n_tx^2 (T_d + T_p) (Hermitian half),
+    B^H 8 n_rx L (T_d + T_p), Cholesky (4/3) L^3, triangular solves 8 n_rx L^2."""
+    P = N + 1
+    L = P * n_tx
+    return (4 * P * P * n_tx * n_tx * (T_d + T_p) + 8 * n_rx * L * (T_d + T_p) + 4 * L ** 3 / 3
+            + 8 * n_rx * L * L)
+
+
+def mstep_bytes_per_trial_iter(n_tx, n_rx, N, T_p, T_d):
+    """Minimal HBM bytes of one M-step per trial: R written once and read once (Hermitian
+    half), psi / moments / pilots read once, theta written."""
+    P = N + 1
+    L = P * n_tx
+    return 16 * (L * L + T_d * P + T_d * (n_tx + n_tx * n_tx) + T_p * L + L * n_rx)
 
 
 def estep_flops_per_trial_iter(n_tx, n_rx, T_d, M):
@@ -68,19 +94,24 @@ def load_pmc_traffic(path):
         return None
 
 
-def cpu_baseline(cfg, varn, seed, iters=2):
-    """Oracle port (vectorised float64 NumPy reduced form) on 1 trial x `iters` EM
-    iterations of the same configuration: ~10-30 s of CPU work."""
+def cpu_baseline(cfg, varn, seed, iters=2, mode="soft", part_r=0):
+    """Oracle port (vectorised float64 NumPy reduced form, or the PM list oracle) on
+    1 trial x `iters` EM iterations of the same configuration: ~10-30 s of CPU work."""
     import importlib
     from oracle.em_reduced import em_reduced
+    from oracle.pm import em_pm
     pkg = importlib.import_module(
         "semi-blind-channel-estimation-for-mimo-ris-communication-system-using-em-algo_amd")
     n_tx, n_rx, N, T_p, T_d, M, _, _ = cfg
     b = pkg.signal_model.synthetic_batch(1, n_tx, n_rx, N, T_p, T_d, M, varn, seed=seed + 12345)
-    aps = pkg.qam.all_possible_symbols(b["cons"], n_tx)
     t0 = time.perf_counter()
-    em_reduced(b["y_d"][0], b["y_p"][0], b["u_p"][0], b["psi_d"][0].T, aps, varn, iters,
-               b["theta0"][0])
+    if mode.startswith("pm"):
+        em_pm(b["y_d"][0], b["y_p"][0], b["u_p"][0], b["psi_d"][0].T, varn, iters,
+              b["theta0"][0], n_tx, n_rx, part_r, b["cons"], soft=mode == "pm_soft")
+    else:
+        aps = pkg.qam.all_possible_symbols(b["cons"], n_tx)
+        em_reduced(b["y_d"][0], b["y_p"][0], b["u_p"][0], b["psi_d"][0].T, aps, varn, iters,
+                   b["theta0"][0], mode=mode)
     dt = time.perf_counter() - t0
     threads = os.environ.get("OMP_NUM_THREADS")
     # threads actually usable by the port: NumPy elementwise work is single-threaded,
@@ -90,7 +121,8 @@ def cpu_baseline(cfg, varn, seed, iters=2):
         cores = min(cores, int(threads))
     return {"value": iters / dt, "unit": "EM-iterations/s", "cores": cores,
             "kind": "port",
-            "sample": f"1 trial x {iters} EM iterations of the same config, oracle/em_reduced.py "
+            "sample": f"1 trial x {iters} EM iterations of the same config, "
+                      f"{'oracle/pm.py' if mode.startswith('pm') else 'oracle/em_reduced.py'} "
                       f"(NumPy float64, BLAS threads={threads or 'default'}), {dt:.2f} s"}
 
 
@@ -103,7 +135,9 @@ def main():
     ap.add_argument("--trials", type=int, default=None, help="trials per GPU")
     ap.add_argument("--iters", type=int, default=None, help="EM iterations per step")
     ap.add_argument("--snr", type=float, default=20.0)
-    ap.add_argument("--mode", default="soft", choices=["soft", "hard"])
+    ap.add_argument("--mode", default=None, choices=["soft", "hard", "pm", "pm_soft"],
+                    help="E-step (default: the workload's, ESTEP)")
+    ap.add_argument("--partition-r", type=int, default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
@@ -130,12 +164,16 @@ def main():
     if args.iters:
         cfg[7] = args.iters
     n_tx, n_rx, N, T_p, T_d, M, B, iters = cfg
+    mode, part_r, solve = ESTEP[args.config]
+    mode = args.mode or mode
+    part_r = part_r if args.partition_r is None else args.partition_r
     varn = float(pkg.signal_model.snr_to_varn(args.snr))
 
     # ---- synthetic inputs for this rank's trials, resident in HBM before timing ----
     batch = pkg.signal_model.synthetic_batch(B, n_tx, n_rx, N, T_p, T_d, M, varn,
                                              seed=args.seed * 1000003 + rank)
-    eng = pkg.EMEngine(batch, varn, mode=args.mode)
+    eng = pkg.EMEngine(batch, varn, mode=mode, partition_r=part_r, solve=solve)
+    del batch
     torch.cuda.synchronize()
 
     def barrier():
@@ -183,13 +221,34 @@ def main():
     mstep_ms = e0.elapsed_time(e1) / args.kernel_reps
 
     P = N + 1
-    flops = estep_flops_per_trial_iter(n_tx, n_rx, T_d, M) * B
-    algo_bytes = estep_bytes_per_trial_iter(n_tx, n_rx, P, T_d) * B
-    achieved_tf = flops / (estep_ms * 1e-3) / 1e12
     pmc = load_pmc_traffic(args.pmc)
     traffic = None
-    if pmc and pmc.get("config") == args.config and pmc.get("trials") == B:
-        traffic = pmc.get("hbm_bytes_per_launch")
+    mflops = mstep_flops_per_trial_iter(n_tx, n_rx, N, T_p, T_d) * B
+    mbytes = mstep_bytes_per_trial_iter(n_tx, n_rx, N, T_p, T_d) * B
+    mstep_roof = {"kernel": "M-step (R build + Cholesky + solves)", "ms": mstep_ms,
+                  "achieved": mflops / (mstep_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
+                  "unit": "TFLOP/s", "frac": mflops / (mstep_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                  "algorithmic_bytes": mbytes,
+                  "hbm_frac_algorithmic": mbytes / (mstep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                  "flops_per_launch": mflops}
+    if mode in ("soft", "hard"):
+        flops = estep_flops_per_trial_iter(n_tx, n_rx, T_d, M) * B
+        algo_bytes = estep_bytes_per_trial_iter(n_tx, n_rx, P, T_d) * B
+        achieved_tf = flops / (estep_ms * 1e-3) / 1e12
+        if pmc and pmc.get("config") == args.config and pmc.get("trials") == B:
+            traffic = pmc.get("hbm_bytes_per_launch")
+        roofline = {"bound": "mfma", "pipe": "FP64 MFMA v_mfma_f64_16x16x4f64 (+ FP64 VALU)",
+                    "kernel": "estep_mfma_kernel",
+                    "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                    "algorithmic_bytes": algo_bytes,
+                    "hbm_GBps_algorithmic": algo_bytes / (estep_ms * 1e-3) / 1e9,
+                    "hbm_frac_algorithmic": algo_bytes / (estep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    "flops_per_launch": flops}
+    else:
+        # list-detector workloads: the M-step (MFMA tile build + blocked Cholesky) dominates
+        roofline = dict(mstep_roof, bound="mfma", traffic=None,
+                        pipe="FP64 MFMA v_mfma_f64_16x16x4f64")
 
     value = world * B * iters * args.steps / elapsed
     line = {
@@ -207,21 +266,18 @@ def main():
         "data": "synthetic (Rayleigh channels, 16-QAM, uniform RIS phases, CN noise; numpy Generator)",
         "config": {"workload": args.config, "n_tx": n_tx, "n_rx": n_rx, "N_RIS": N, "T_p": T_p,
                    "T_d": T_d, "M": M, "trials_per_gpu": B, "em_iters": iters,
-                   "snr_db": args.snr, "estep": args.mode, "parallelism": f"trials-sharded x{world}"},
+                   "snr_db": args.snr, "estep": mode, "partition_r": part_r, "solve": solve,
+                   "parallelism": f"trials-sharded x{world}"},
         "nmse_mean": nmse_mean,
         "nonhpd_trials": nonhpd,
         "kernels_ms": {"estep": estep_ms, "mstep_build_plus_solve": mstep_ms},
-        "roofline": {"bound": "mfma", "pipe": "FP64 MFMA v_mfma_f64_16x16x4f64 (+ FP64 VALU)",
-                     "kernel": "estep_mfma_kernel",
-                     "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "algorithmic_bytes": algo_bytes,
-                     "hbm_GBps_algorithmic": algo_bytes / (estep_ms * 1e-3) / 1e9,
-                     "hbm_frac_algorithmic": algo_bytes / (estep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "flops_per_launch": flops},
+        "roofline": roofline,
+        "mstep_roofline": mstep_roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(cfg, varn, args.seed)
+        line["cpu_baseline"] = cpu_baseline(cfg, varn, args.seed,
+                                            iters=2 if args.config in ("cfg1", "plumbing") else 1,
+                                            mode=mode, part_r=part_r)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

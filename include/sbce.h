@@ -80,6 +80,8 @@ extern "C" {
 
 /* per-trial status bits */
 #define SBCE_STATUS_NONHPD 1
+#define SBCE_STATUS_PILOT 2     /* L > 512 path: u_p is not a Kronecker product
+                                   psi_p (x) x_p (PM.py:119-130); R's pilot term invalid */
 
 typedef struct sbce_dims {
     int32_t batch;      /* B: independent Monte-Carlo trials */

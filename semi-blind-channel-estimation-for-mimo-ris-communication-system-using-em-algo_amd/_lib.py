@@ -18,6 +18,7 @@ SBCE_ESTEP_PM_SOFT = 3
 SBCE_SOLVE_CHOL = 0
 SBCE_SOLVE_CHOL_DROP = 1
 SBCE_STATUS_NONHPD = 1
+SBCE_STATUS_PILOT = 2
 
 EXPORTED = ("sbce_abi_version", "sbce_strerror", "sbce_workspace_bytes", "sbce_em",
             "sbce_estep", "sbce_mstep", "sbce_nmse")

@@ -16,7 +16,7 @@ constexpr size_t kAlign = 256;
 size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 struct Carve {
-    size_t mom, R, rhs, done, total;
+    size_t mom, R, rhs, done, tol, winv, ppsi, pS, total;
 };
 
 bool make_problem(const sbce_dims* d, Problem& pb) {
@@ -39,11 +39,26 @@ Carve carve(const Problem& pb) {
     c.R = align_up(c.mom + (size_t)pb.B * pb.Td * MS * sizeof(cd));
     c.rhs = align_up(c.R + (size_t)pb.B * pb.L * pb.L * sizeof(cd));
     c.done = align_up(c.rhs + (size_t)pb.B * pb.L * pb.NR * sizeof(cd));
-    c.total = align_up(c.done + (size_t)pb.B * sizeof(int32_t));
+    c.tol = align_up(c.done + (size_t)pb.B * sizeof(int32_t));
+    c.winv = c.ppsi = c.pS = c.tol;
+    c.total = c.tol;
+    if (pb.L > kLargeL) {                    // tiled large-L M-step (mstep_large.hip)
+        c.winv = align_up(c.tol + (size_t)pb.B * sizeof(double));
+        c.ppsi = align_up(c.winv + (size_t)pb.B * 64 * 64 * sizeof(cd));
+        c.pS = align_up(c.ppsi + (size_t)pb.B * pb.Tp * pb.P * sizeof(cd));
+        c.total = align_up(c.pS + (size_t)pb.B * pb.Tp * pb.NT * pb.NT * sizeof(cd));
+    }
     return c;
 }
 
 int hip_rc(hipError_t e) { return e == hipSuccess ? SBCE_OK : SBCE_EHIP; }
+
+void set_large(MstepArgs& ma, char* ws, const Carve& c) {
+    ma.tol = (double*)(ws + c.tol);
+    ma.winv = (cd*)(ws + c.winv);
+    ma.ppsi = (cd*)(ws + c.ppsi);
+    ma.pS = (cd*)(ws + c.pS);
+}
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -110,6 +125,7 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     ma.yd = ea.yd; ma.yp = (const cd*)p->y_p; ma.psid = ea.psid; ma.up = (const cd*)p->u_p;
     ma.mom = ea.mom; ma.R = (cd*)(ws + c.R); ma.rhs = (cd*)(ws + c.rhs); ma.theta = (cd*)p->theta;
     ma.status = p->status; ma.done = ea.done; ma.solve_mode = solve_mode;
+    set_large(ma, ws, c);
 
     for (int it = 0; it < iters; ++it) {
         if ((rc = hip_rc(launch_estep(pb, ea, estep_mode, s)))) return rc;
@@ -167,6 +183,7 @@ int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int 
     ma.up = (const cd*)p->u_p; ma.mom = (const cd*)moments; ma.R = (cd*)(ws + c.R);
     ma.rhs = (cd*)(ws + c.rhs); ma.theta = (cd*)p->theta; ma.status = p->status; ma.done = nullptr;
     ma.solve_mode = solve_mode;
+    set_large(ma, ws, c);
     if ((rc = hip_rc(launch_mstep_build(pb, ma, s)))) return rc;
     if (r_out &&
         hipMemcpyAsync(r_out, ma.R, (size_t)pb.B * pb.L * pb.L * sizeof(cd), hipMemcpyDeviceToDevice,

@@ -394,7 +394,8 @@ __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double t
 // k = tid (+ nth) of the update and loads its 16 factor entries BEFORE the barrier that
 // publishes the block solution, so each block pays one memory latency, not three.
 __device__ __forceinline__ void back_substitute_pf(const cd* R, cd* y, int L, int NR, int tid,
-                                                   int nth, int lane, int wave, int kb_stop) {
+                                                   int nth, int lane, int wave, int kb_stop,
+                                                   int ld) {
     const int nblk = (L + NB - 1) / NB;
     for (int kb = nblk - 1; kb >= kb_stop; --kb) {
         const int k0 = kb * NB;
@@ -406,7 +407,7 @@ __device__ __forceinline__ void back_substitute_pf(const cd* R, cd* y, int L, in
             const int k = tid + h * nth;
 #pragma unroll
             for (int c = 0; c < NB; ++c)
-                lv[h][c] = (k < k0 && c < w) ? R[(size_t)(k0 + c) * L + k] : czero();
+                lv[h][c] = (k < k0 && c < w) ? R[(size_t)(k0 + c) * ld + k] : czero();
         }
         if (wave == 0) {
             // x_blk = D^{-H} z_blk:  x[c] = z[c] / L[c][c] + sum_{c2>c} conj(Di[c2][c]) z[c2]
@@ -417,7 +418,7 @@ __device__ __forceinline__ void back_substitute_pf(const cd* R, cd* y, int L, in
                 const int e = h ? e1 : e0;
                 if (e < w * NR) {
                     const int c = e / NR, r = e - c * NR;
-                    const cd* Rc = R + (size_t)(k0 + c) * L + k0;
+                    const cd* Rc = R + (size_t)(k0 + c) * ld + k0;
                     const double lcc = Rc[c].x;
                     cd acc = (lcc > 0.0) ? cscale(y[(k0 + c) * NR + r], 1.0 / lcc) : czero();
                     for (int c2 = c + 1; c2 < w; ++c2) acc = cfma(acc, Rc[c2], y[(k0 + c2) * NR + r]);
@@ -449,10 +450,20 @@ __device__ __forceinline__ void back_substitute_pf(const cd* R, cd* y, int L, in
 // DIAGNOSTIC (skip & 64): per-phase s_memtime sums of waves 0 and 1 of block 0
 __device__ unsigned long long g_chol_clk[32];
 
-template <int MAXT, bool YLDS, int NWB, int KB>
+// Geometry of one chol_mfma_kernel launch: the factored L x L matrix starts at row/col
+// `off` of trial b's matrix (a.R + b*stride), leading dimension ld.  SOLVE = false
+// factors in place only (a diagonal tile of the large-L path, tol from tolp[b]).
+struct CholGeom {
+    int ld, off;
+    size_t stride;
+    const double* tolp;
+};
+
+template <int MAXT, bool YLDS, int NWB, int KB, bool SOLVE = true>
 __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(2)))
-void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip) {
+void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip, CholGeom g) {
     constexpr int KBP = KB + 1;                 // padded LDS row (complex) of the panel block
+    const int ld = g.ld;
     // skip: DIAGNOSTIC phase mask (timing only, results invalid): 1 update, 2 diag factor,
     // 8 trsm tiles, 16 back substitution
     const int b = blockIdx.x;
@@ -467,11 +478,18 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip) {
     double* red = reinterpret_cast<double*>(Xs + nw * NB * NB);   // [16]
     int* flag = reinterpret_cast<int*>(red + 16);
     cd* ylds = reinterpret_cast<cd*>(red + 18);
-    cd* R = a.R + (size_t)b * L * L;
-    cd* y = YLDS ? ylds : a.rhs + (size_t)b * L * NR;
+    cd* R = a.R + (size_t)b * g.stride + (size_t)g.off * ld + g.off;
+    cd* y = SOLVE ? (YLDS ? ylds : a.rhs + (size_t)b * L * NR) : nullptr;
     cd* X = Xs + wave * NB * NB;
-    const double tol = prologue<YLDS>(R, a.rhs + (size_t)b * L * NR, y, red, flag, L, NR, tid,
-                                      nth, lane, wave);
+    double tol;
+    if (SOLVE) {
+        tol = prologue<YLDS>(R, a.rhs + (size_t)b * L * NR, y, red, flag, L, NR, tid, nth, lane,
+                             wave);
+    } else {
+        tol = g.tolp[b];
+        if (tid == 0) *flag = 0;
+        __syncthreads();
+    }
     const int li = lane & 15, lk = lane >> 4;
     const bool clk = (skip & 64) && b == 0 && wave < 2 && lane == 0;
     unsigned long long tclk = clk ? __builtin_amdgcn_s_memtime() : 0;
@@ -492,7 +510,7 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip) {
         for (int u = 0; u < MAXT; ++u) {
             int r = jb + (wave + u * nw) * NB + li;
             r = r < L ? r : L - 1;
-            arow[u] = R + (size_t)r * L + lk;
+            arow[u] = R + (size_t)r * ld + lk;
         }
         // ---- C tiles <- A[rows, jb:jb+16] (C layout) ----
         d4v cre[MAXT], cim[MAXT];
@@ -503,7 +521,7 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip) {
             for (int q = 0; q < 4; ++q) {
                 const int r = jb + tau * NB + lk + 4 * q;
                 cd v = czero();
-                if (tau < ntile && r < L && li < w) v = R[(size_t)r * L + jb + li];
+                if (tau < ntile && r < L && li < w) v = R[(size_t)r * ld + jb + li];
                 cre[u][q] = v.x;
                 cim[u][q] = v.y;
             }
@@ -521,7 +539,7 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip) {
             __syncthreads();
             for (int e = tid; e < NB * kbs; e += nth) {
                 const int c = e / kbs, k = e - c * kbs;
-                Bp[c * KBP + k] = (c < w) ? R[(size_t)(jb + c) * L + kb0 + k] : czero();
+                Bp[c * KBP + k] = (c < w) ? R[(size_t)(jb + c) * ld + kb0 + k] : czero();
             }
             __syncthreads();
             for (int k0 = 0; k0 < kbs; k0 += KCM) {
@@ -572,8 +590,8 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip) {
             wave_sync();
             if (!(skip & 2))
                 factor_diag_lds(X, w, lane, tol, a.solve_mode, Di, red, flag,
-                                R + (size_t)jb * L + jb, L, clk ? g_chol_clk + 6 : nullptr);
-            forward_y_block(Di, y + jb * NR, w, NR, lane);
+                                R + (size_t)jb * ld + jb, ld, clk ? g_chol_clk + 6 : nullptr);
+            if (SOLVE) forward_y_block(Di, y + jb * NR, w, NR, lane);
         }
         SBCE_CLK(1)
         __syncthreads();
@@ -600,7 +618,7 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip) {
                 xim = __builtin_amdgcn_mfma_f64_16x16x4f64(-d.y, c.x, xim, 0, 0, 0);
             }
             const bool live = row0 + li < L;
-            cd* crow = R + (size_t)(live ? row0 + li : L - 1) * L + jb;
+            cd* crow = R + (size_t)(live ? row0 + li : L - 1) * ld + jb;
             cd xv[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -609,7 +627,7 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip) {
                 if (live && j < w) crow[j] = xv[q];
             }
             // y[row0+li] -= sum_j X[li][j] y_blk[j]: 4 columns per lane, reduced over lk
-            for (int r = 0; r < NR; ++r) {
+            for (int r = 0; r < (SOLVE ? NR : 0); ++r) {
                 cd p = czero();
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -626,11 +644,14 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip) {
         __syncthreads();
         SBCE_CLK(4)
     }
-    back_substitute_pf(R, y, L, NR, tid, nth, lane, wave, (skip & 16) ? (L + NB - 1) / NB : 0);
-    SBCE_CLK(5)
+    if (SOLVE) {
+        back_substitute_pf(R, y, L, NR, tid, nth, lane, wave, (skip & 16) ? (L + NB - 1) / NB : 0,
+                           ld);
+        SBCE_CLK(5)
+        cd* th = a.theta + (size_t)b * L * NR;
+        for (int e = tid; e < L * NR; e += nth) th[e] = cconj(y[e]);
+    }
 #undef SBCE_CLK
-    cd* th = a.theta + (size_t)b * L * NR;
-    for (int e = tid; e < L * NR; e += nth) th[e] = cconj(y[e]);
     if (tid == 0 && a.status) a.status[b] |= *flag ? SBCE_STATUS_NONHPD : 0;
 }
 
@@ -659,10 +680,12 @@ hipError_t launch_mfma_cfg(const Problem& pb, const MstepArgs& a, int nw, int ma
     const char* sk = getenv("SBCE_CHOL_SKIP");      // diagnostic only (see kernel)
     const int skip = sk ? atoi(sk) : 0;
     const dim3 g(pb.B), blk(64 * nw);
+    CholGeom geo;
+    geo.ld = pb.L; geo.off = 0; geo.stride = (size_t)pb.L * pb.L; geo.tolp = nullptr;
 #define SBCE_CM(t)                                                                                \
     case t:                                                                                       \
         hipLaunchKernelGGL((chol_mfma_kernel<t, YLDS, NWB, KB>), g, blk, lds, s, a, pb.L, pb.NR,  \
-                           skip);                                                                 \
+                           skip, geo);                                                            \
         break;
     switch (maxt) {
         SBCE_CM(1) SBCE_CM(2) SBCE_CM(3) SBCE_CM(4) SBCE_CM(5)
@@ -699,10 +722,24 @@ hipError_t chol_debug_clock_reset() {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_chol_clk), z, sizeof(z), 0, hipMemcpyHostToDevice);
 }
 
-bool chol_supported(const Problem& pb) { return pb.L >= 1 && pb.L <= 1024; }
+bool chol_supported(const Problem& pb) { return pb.L >= 1 && (pb.L <= 1024 || pb.NR <= 8); }
+
+// Factor the w x w diagonal tile at (k0, k0) of every trial's R in place (large-L path).
+hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w, hipStream_t s) {
+    const int ntile = (w + NB - 1) / NB;             // <= 4 -> one 16-row tile per wave
+    CholGeom geo;
+    geo.ld = pb.L; geo.off = k0; geo.stride = (size_t)pb.L * pb.L; geo.tolp = a.tol;
+    const size_t lds = (size_t)(NB * (128 + 1) + NB * NB + ntile * NB * NB) * sizeof(cd) +
+                       18 * sizeof(double);
+    hipLaunchKernelGGL((chol_mfma_kernel<1, false, 4, 128, false>), dim3(pb.B), dim3(64 * ntile),
+                       lds, s, a, w, pb.NR, 0, geo);
+    return hipGetLastError();
+}
 
 hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s) {
     if (!chol_supported(pb)) return hipErrorInvalidValue;
+    const char* impl0 = getenv("SBCE_CHOL_IMPL");
+    if (pb.L > kLargeL && !(impl0 && impl0[0] == 'v' && pb.L <= 1024)) return launch_chol_large(pb, a, s);
     const size_t ybytes = (size_t)pb.L * pb.NR * sizeof(cd);
     const char* impl = getenv("SBCE_CHOL_IMPL");    // "valu" forces the VALU kernel (A/B runs)
     const bool force_valu = impl && impl[0] == 'v';

@@ -238,8 +238,15 @@ __global__ __launch_bounds__(256) void early_stop_kernel(const cd* theta, const 
 
 hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t s) {
     const int npairs = pb.P * (pb.P + 1) / 2;
+    const bool tiles = pb.L > kLargeL && rbuild_tile_supported(pb);
+    if (tiles) {
+        hipError_t e0 = launch_pilot_factor(pb, a, s);
+        if (e0 == hipSuccess) e0 = launch_rbuild_tiles(pb, a, s);
+        if (e0 != hipSuccess) return e0;
+    }
     dim3 g1((npairs + 255) / 256, pb.B);
-    switch (pb.NT) {
+    switch (tiles ? 0 : pb.NT) {
+        case 0: break;
         case 1: hipLaunchKernelGGL(rbuild_kernel<1>, g1, dim3(256), 0, s, a, pb.B, pb.P, pb.Tp, pb.Td, pb.L); break;
         case 2: hipLaunchKernelGGL(rbuild_kernel<2>, g1, dim3(256), 0, s, a, pb.B, pb.P, pb.Tp, pb.Td, pb.L); break;
         case 3: hipLaunchKernelGGL(rbuild_kernel<3>, g1, dim3(256), 0, s, a, pb.B, pb.P, pb.Tp, pb.Td, pb.L); break;

@@ -107,6 +107,11 @@ struct MstepArgs {
     int32_t* status;   // [B] or null
     const int32_t* done;
     int solve_mode;
+    // large-L path (L > 512) workspace
+    double* tol;       // [B]     pivot threshold
+    cd* winv;          // [B][64][64] inverse of the current diagonal tile
+    cd* ppsi;          // [B][Tp][P]  pilot phases psi' (Kronecker factor of u_p)
+    cd* pS;            // [B][Tp][NT*NT] pilot x' x'^H
 };
 
 hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStream_t s);
@@ -117,6 +122,12 @@ bool estep_supported(const Problem& pb, int mode);
 hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s);
 bool chol_supported(const Problem& pb);
+constexpr int kLargeL = 512;   // L above this: tiled build + blocked right-looking Cholesky
+bool rbuild_tile_supported(const Problem& pb);
+hipError_t launch_pilot_factor(const Problem& pb, const MstepArgs& a, hipStream_t s);
+hipError_t launch_rbuild_tiles(const Problem& pb, const MstepArgs& a, hipStream_t s);
+hipError_t launch_chol_large(const Problem& pb, const MstepArgs& a, hipStream_t s);
+hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w, hipStream_t s);
 hipError_t chol_debug_clock(unsigned long long* out);   // diagnostic (SBCE_CHOL_SKIP & 64)
 hipError_t chol_debug_clock_reset();
 hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* out,

@@ -358,3 +358,55 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape, monkeypatch):
         assert rel(th_m[i], ref) < 1e-9
         assert rel(th_v[i], ref) < 1e-9
     assert rel(th_m, th_v) < 1e-9
+
+
+# ---------------------------------------------------------------- large-L M-step (L > 512)
+@pytest.mark.parametrize("shape", [
+    # (n_tx, n_rx, N, T_p, T_d)       L = (N+1) n_tx
+    (4, 4, 149, 16, 200),             # L = 600: MFMA tile build (NT = 4), 10 column blocks
+    (8, 8, 80, 32, 100),              # L = 648: MFMA tile build (NT = 8), BASELINE cfg 2 geometry
+    (3, 2, 200, 12, 260),             # L = 603: VALU build, partial last tile (w = 27)
+])
+def test_large_l_mstep_vs_numpy(sbce, shape):
+    """Tiled R build (pilots through the Kronecker factorisation) and the blocked
+    right-looking Cholesky + triangular solves vs the oracle's R and numpy.linalg.solve."""
+    n_tx, n_rx, N, T_p, T_d = shape
+    b = sbce.signal_model.synthetic_batch(2, n_tx, n_rx, N, T_p, T_d, 4, 0.05, seed=8)
+    x = b["x_d"]
+    m = x
+    S = x[..., :, None] * np.conj(x[..., None, :]) + 0.1 * np.eye(n_tx)
+    th, R, rhs, st = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], m, S,
+                                      0.05)
+    assert not st.any()
+    for i in range(2):
+        R0, rhs0 = mstep_build(b["u_p"][i], b["y_p"][i], b["psi_d"][i].T, b["y_d"][i], m[i], S[i])
+        lo = np.tril_indices(R0.shape[0])
+        assert rel(R[i][lo], R0[lo]) < 1e-12
+        assert rel(rhs[i], rhs0) < 1e-12
+        assert rel(th[i], mstep_solve(R0, rhs0)) < 1e-9
+
+
+def test_large_l_pilot_not_kronecker_is_flagged(sbce):
+    n_tx, n_rx, N, T_p, T_d = 4, 2, 140, 8, 150
+    b = sbce.signal_model.synthetic_batch(1, n_tx, n_rx, N, T_p, T_d, 4, 0.05, seed=3)
+    rng = np.random.default_rng(0)
+    u_p = b["u_p"] + 0.1 * (rng.standard_normal(b["u_p"].shape) + 1j * rng.standard_normal(b["u_p"].shape))
+    x = b["x_d"]
+    S = x[..., :, None] * np.conj(x[..., None, :]) + 0.1 * np.eye(n_tx)
+    _, _, _, st = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], u_p, b["cons"], x, S, 0.05)
+    assert st[0] & sbce._lib.SBCE_STATUS_PILOT
+
+
+def test_large_l_full_em_pm_soft_vs_oracle(sbce):
+    """BASELINE cfg 2 estimator (n_tx = n_rx = 8, 16-QAM, PM_beta r = 1) at L = 648: the
+    whole device EM (PM E-step + tiled M-step) vs the oracle."""
+    from oracle.pm import em_pm
+    n_tx, n_rx, N, T_p, T_d, M, varn, itera = 8, 8, 80, 32, 720, 16, 0.05, 2   # T_d > L: well posed
+    b = sbce.signal_model.synthetic_batch(2, n_tx, n_rx, N, T_p, T_d, M, varn, seed=12)
+    res = sbce.em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, itera,
+                        b["theta0"], mode="pm_soft", partition_r=1)
+    assert not res["status"].any()
+    for i in range(2):
+        th = em_pm(b["y_d"][i], b["y_p"][i], b["u_p"][i], b["psi_d"][i].T, varn, itera,
+                   b["theta0"][i], n_tx, n_rx, 1, b["cons"], soft=True)
+        assert rel(res["theta"][i], th) < 1e-8
