@@ -44,13 +44,10 @@ def _read(d, counter):
 
 
 def _short(name):
-    base = name.replace("(anonymous namespace)", "").split("(")[0]
-    for key in ("estep_mfma_kernel", "estep_pm_kernel", "estep_kernel", "rbuild_wide_kernel",
-                "rbuild_kernel", "rhs_kernel", "chol_solve_kernel", "nmse_kernel", "llf_kernel",
-                "early_stop_kernel"):
-        if key + "<" in base or base.endswith(key):
-            return key
-    return base[:60]
+    """Kernel identifier: last scope component before the template / argument list."""
+    base = name.replace("(anonymous namespace)", "")
+    base = base.split("(")[0].split("<")[0]
+    return base.replace("void ", "").split("::")[-1].strip()[:60]
 
 
 def main():

@@ -20,10 +20,11 @@ def main():
     w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage"])
     for f in dbs:
         con = sqlite3.connect(f)
-        for name, calls, tot, avg, pct in con.execute(
-                "select name, total_calls, total_duration, average, percentage from top_kernels "
-                "order by total_duration desc"):
-            w.writerow([name, calls, f"{tot:.0f}", f"{avg:.1f}", f"{pct:.2f}"])
+        rows = con.execute("select name, count(*), sum(duration), avg(duration) from kernels "
+                           "group by name order by sum(duration) desc").fetchall()
+        total = sum(r[2] for r in rows) or 1
+        for name, calls, tot, avg in rows:
+            w.writerow([name, calls, f"{tot:.0f}", f"{avg:.1f}", f"{100.0 * tot / total:.2f}"])
 
 
 if __name__ == "__main__":
