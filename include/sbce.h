@@ -70,6 +70,9 @@ extern "C" {
                                    weight 1: PM.py:57-104 (dims.partition_r) */
 #define SBCE_ESTEP_PM_SOFT 3    /* partitioned list detector, posterior list
                                    weights: PM_beta.py:55-95 (dims.partition_r) */
+#define SBCE_ESTEP_ZF 4         /* zero-forcing hard decision (n_rx >= n_tx):
+                                   all_detectorsvsTd.py:98-133 */
+#define SBCE_ESTEP_MMSE 5       /* MMSE hard decision: all_detectorsvsTd.py:54-96 */
 
 /* M-step solve modes (SURVEY.md §7 hard part 3) */
 #define SBCE_SOLVE_CHOL 0       /* Hermitian Cholesky of the reduced L x L system
@@ -82,10 +85,13 @@ extern "C" {
 #define SBCE_STATUS_NONHPD 1
 #define SBCE_STATUS_PILOT 2     /* L > 512 path: u_p is not a Kronecker product
                                    psi_p (x) x_p (PM.py:119-130); R's pilot term invalid */
+#define SBCE_STATUS_DETECTOR 4  /* ZF/MMSE: the reference's flattened argmin indexed past
+                                   all_possibleSymbols (IndexError at
+                                   all_detectorsvsTd.py:52); row flat mod M^n_tx used */
 
 typedef struct sbce_dims {
     int32_t batch;      /* B: independent Monte-Carlo trials */
-    int32_t n_tx;       /* streams (1..4 exact/hard E-step, 1..8 PM E-steps) */
+    int32_t n_tx;       /* streams (1..4 exact/hard E-step, 1..8 PM/ZF/MMSE E-steps) */
     int32_t n_rx;       /* receive antennas (1..8) */
     int32_t n_psi;      /* P = rows of PsiTilde_td (N+1 with the direct path) */
     int32_t t_p;        /* pilot symbols */

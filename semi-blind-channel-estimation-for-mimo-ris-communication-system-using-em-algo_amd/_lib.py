@@ -15,10 +15,13 @@ SBCE_ESTEP_SOFT = 0
 SBCE_ESTEP_HARD = 1
 SBCE_ESTEP_PM = 2
 SBCE_ESTEP_PM_SOFT = 3
+SBCE_ESTEP_ZF = 4
+SBCE_ESTEP_MMSE = 5
 SBCE_SOLVE_CHOL = 0
 SBCE_SOLVE_CHOL_DROP = 1
 SBCE_STATUS_NONHPD = 1
 SBCE_STATUS_PILOT = 2
+SBCE_STATUS_DETECTOR = 4
 
 EXPORTED = ("sbce_abi_version", "sbce_strerror", "sbce_workspace_bytes", "sbce_em",
             "sbce_estep", "sbce_mstep", "sbce_nmse")

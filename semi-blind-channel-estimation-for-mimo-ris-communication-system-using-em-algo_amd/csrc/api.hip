@@ -121,6 +121,7 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     EstepArgs ea;
     ea.yd = (const cd*)p->y_d; ea.psid = (const cd*)p->psi_d; ea.theta = (const cd*)p->theta;
     ea.cons = (const cd*)p->cons; ea.mom = (cd*)(ws + c.mom); ea.done = early ? done : nullptr;
+    ea.status = p->status;
     MstepArgs ma;
     ma.yd = ea.yd; ma.yp = (const cd*)p->y_p; ma.psid = ea.psid; ma.up = (const cd*)p->u_p;
     ma.mom = ea.mom; ma.R = (cd*)(ws + c.R); ma.rhs = (cd*)(ws + c.rhs); ma.theta = (cd*)p->theta;
@@ -161,6 +162,7 @@ int sbce_estep(const sbce_dims* d, const sbce_ptrs* p, int estep_mode, void* mom
     EstepArgs ea;
     ea.yd = (const cd*)p->y_d; ea.psid = (const cd*)p->psi_d; ea.theta = (const cd*)p->theta;
     ea.cons = (const cd*)p->cons; ea.mom = (cd*)moments; ea.done = nullptr;
+    ea.status = p->status;
     return hip_rc(launch_estep(pb, ea, estep_mode, (hipStream_t)hip_stream));
 }
 

@@ -1,3 +1,5 @@
+// List / linear-detector E-steps.  MODE 4/5: ZF / MMSE hard decisions of
+// "Proposed method/all_detectorsvsTd.py":98-133 / :54-96 (see the MODE >= 4 branch).
 // PM (partitioned-detector) E-step: "Proposed method/PM.py":57-104 (uniform list
 // weights) and "Proposed method/PM_beta.py":55-95 (posterior list weights), the
 // list-based E-step that makes n_tx = 8 (BASELINE cfg 2) tractable.
@@ -28,7 +30,7 @@ constexpr int kAugW = 16;          // augmented-matrix row stride ([G | I], G in
 
 struct PmConst {
     int B, Td, P, M, lm, NT, NR, NA, JA;
-    double inv_s2;
+    double inv_s2, s2;
 };
 
 struct PmLds {                      // per-wave LDS carve (complex doubles unless noted)
@@ -121,6 +123,60 @@ __global__ __launch_bounds__(64 * kPmWaves) void estep_pm_kernel(EstepArgs a, Pm
     if (lane < NR) yv[lane] = a.yd[(size_t)gsym * NR + lane];
     if (lane < NT) cols[lane] = lane;
     wave_sync();
+
+    if (MODE >= 4) {
+        // ---- ZF / MMSE hard decision (all_detectorsvsTd.py:70-72, :111-113) ----
+        // z = (H^H H [+ varn^2 I])^{-1} H^H y on the off-by-one channel, then the
+        // flattened-argmin nearest_symbol_ecul (:49-52) in closed form: the global minimum
+        // is min_a dist(z_a, cons); its first flat index is a* NT (s* = 0) or
+        // s* NT^2 + a* NT + NT - 1, which selects ROW `flat` of the itertools.product table.
+        gram(aug, Ho, cols, NT, NR, lane);
+        if (MODE == 5 && lane < NT) aug[lane * kAugW + lane].x += c.s2;
+        wave_sync();
+        gj_inverse(aug, NT, lane);
+        {
+            const int aa = lane / NR, r = lane - aa * NR;   // lanes < NT*NR <= 64
+            if (aa < NT) {
+                cd acc = czero();
+                for (int b2 = 0; b2 < NT; ++b2)
+                    acc = cfma(acc, aug[aa * kAugW + 8 + b2], cconj(Ho[b2 * NR + r]));
+                GB[aa * NR + r] = acc;
+            }
+        }
+        wave_sync();
+        if (lane < NT) {
+            cd z = czero();
+            for (int r = 0; r < NR; ++r) z = cfma(z, GB[lane * NR + r], yv[r]);
+            int sbest = 0;
+            double dbest = cabs2(csub(z, s_cons[0]));
+            for (int s2 = 1; s2 < c.M; ++s2) {
+                const double dd = cabs2(csub(z, s_cons[s2]));
+                if (dd < dbest) { dbest = dd; sbest = s2; }
+            }
+            wts[lane] = dbest;
+            cols[8 + lane] = sbest;
+        }
+        wave_sync();
+        int as = 0;
+        for (int q = 1; q < NT; ++q)
+            if (wts[q] < wts[as]) as = q;
+        const int ss = cols[8 + as];
+        long long flat = ss == 0 ? (long long)as * NT : (long long)ss * NT * NT + as * NT + NT - 1;
+        if (c.lm * NT < 62 && flat >= (1LL << (c.lm * NT))) {
+            // the reference raises IndexError here (all_possibleSymbols[flat], :52)
+            if (lane == 0 && a.status) atomicOr(&a.status[b], SBCE_STATUS_DETECTOR);
+            flat %= (1LL << (c.lm * NT));
+        }
+        cd* out = a.mom + (size_t)gsym * (NT + NT * NT);
+        const int ai = lane >> 3, bi = lane & 7;
+        if (ai < NT && bi < NT) {
+            const cd xa = s_cons[(flat >> (c.lm * (NT - 1 - ai))) & mask];
+            const cd xb = s_cons[(flat >> (c.lm * (NT - 1 - bi))) & mask];
+            out[NT + ai * NT + bi] = cmulc(xa, xb);
+            if (bi == 0) out[ai] = xa;
+        }
+        return;
+    }
 
     // ---- 2. greedy stream order on H_off ----
     for (int step = 0; step < NT; ++step) {
@@ -235,9 +291,11 @@ __global__ __launch_bounds__(64 * kPmWaves) void estep_pm_kernel(EstepArgs a, Pm
 
 }  // namespace
 
-bool estep_pm_supported(const Problem& pb, int partition_r) {
+bool estep_pm_supported(const Problem& pb, int partition_r, int mode) {
     if (pb.NT < 1 || pb.NT > 8 || pb.NR < 1 || pb.NR > 8) return false;
     if (pb.M < 2 || pb.M > 64 || (pb.M & (pb.M - 1))) return false;
+    if (mode == SBCE_ESTEP_ZF) return pb.NR >= pb.NT;     // pinv = (H^H H)^{-1} H^H
+    if (mode == SBCE_ESTEP_MMSE) return true;
     if (partition_r < 0) return false;
     const int p = (int)((double)partition_r / log2((double)pb.M));
     const int NA = p + 1;
@@ -249,25 +307,29 @@ bool estep_pm_supported(const Problem& pb, int partition_r) {
 
 hipError_t launch_estep_pm(const Problem& pb, const EstepArgs& a, int mode, int partition_r,
                            hipStream_t s) {
-    if (!estep_pm_supported(pb, partition_r)) return hipErrorInvalidValue;
+    if (!estep_pm_supported(pb, partition_r, mode)) return hipErrorInvalidValue;
     PmConst c;
     c.B = pb.B; c.Td = pb.Td; c.P = pb.P; c.M = pb.M; c.NT = pb.NT; c.NR = pb.NR;
     int lm = 0;
     while ((1 << lm) < pb.M) ++lm;
     c.lm = lm;
-    c.NA = (int)((double)partition_r / log2((double)pb.M)) + 1;
+    const bool det = mode == SBCE_ESTEP_ZF || mode == SBCE_ESTEP_MMSE;
+    c.NA = det ? 1 : (int)((double)partition_r / log2((double)pb.M)) + 1;
     c.JA = 1 << (lm * c.NA);
     c.inv_s2 = 1.0 / (pb.varn * pb.varn);
+    c.s2 = pb.varn * pb.varn;
     const size_t lds = (64 + (size_t)kPmWaves * PmLds::TOTAL) * sizeof(cd);
     const long nsym = (long)pb.B * pb.Td;
     const long blocks = (nsym + kPmWaves - 1) / kPmWaves;
     if (blocks == 0) return hipSuccess;
-    if (mode == SBCE_ESTEP_PM_SOFT)
-        hipLaunchKernelGGL(estep_pm_kernel<3>, dim3((unsigned)blocks), dim3(64 * kPmWaves), lds, s,
-                           a, c);
-    else
-        hipLaunchKernelGGL(estep_pm_kernel<2>, dim3((unsigned)blocks), dim3(64 * kPmWaves), lds, s,
-                           a, c);
+    const dim3 g((unsigned)blocks), blk(64 * kPmWaves);
+    switch (mode) {
+        case SBCE_ESTEP_PM: hipLaunchKernelGGL(estep_pm_kernel<2>, g, blk, lds, s, a, c); break;
+        case SBCE_ESTEP_PM_SOFT: hipLaunchKernelGGL(estep_pm_kernel<3>, g, blk, lds, s, a, c); break;
+        case SBCE_ESTEP_ZF: hipLaunchKernelGGL(estep_pm_kernel<4>, g, blk, lds, s, a, c); break;
+        case SBCE_ESTEP_MMSE: hipLaunchKernelGGL(estep_pm_kernel<5>, g, blk, lds, s, a, c); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -93,6 +93,7 @@ struct EstepArgs {
     const cd* cons;    // [M]
     cd* mom;           // [B][Td][NT + NT*NT]
     const int32_t* done;  // [B] or null
+    int32_t* status;   // [B] or null (detector index flag)
 };
 
 struct MstepArgs {
@@ -117,7 +118,7 @@ struct MstepArgs {
 hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStream_t s);
 hipError_t launch_estep_pm(const Problem& pb, const EstepArgs& a, int mode, int partition_r,
                            hipStream_t s);
-bool estep_pm_supported(const Problem& pb, int partition_r);
+bool estep_pm_supported(const Problem& pb, int partition_r, int mode);
 bool estep_supported(const Problem& pb, int mode);
 hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s);

@@ -18,6 +18,8 @@ Reference operator -> entry point here:
                                PM.py:47-116 (uniform list weights)      -> em_pm()
   em_pm(... no all_possibleSymbols ...)
                                PM_beta.py:42-112 (posterior list weights) -> em_pm_soft()
+  em_zf / em_mmse(..., h_initial, h)
+                               all_detectorsvsTd.py:98-133 / :54-96      -> em_zf(), em_mmse()
 Batched form for sweeps / benchmark: ``em_batch`` (one sbce_em call for all trials).
 
 Semantics kept from the reference: inputs are not mutated, theta is returned
@@ -49,7 +51,8 @@ def _dev(torch, arr, dtype=None):
 
 
 _MODES = {"soft": _lib.SBCE_ESTEP_SOFT, "hard": _lib.SBCE_ESTEP_HARD, "pm": _lib.SBCE_ESTEP_PM,
-          "pm_soft": _lib.SBCE_ESTEP_PM_SOFT}
+          "pm_soft": _lib.SBCE_ESTEP_PM_SOFT, "zf": _lib.SBCE_ESTEP_ZF,
+          "mmse": _lib.SBCE_ESTEP_MMSE}
 _SOLVES = {"chol": _lib.SBCE_SOLVE_CHOL, "drop": _lib.SBCE_SOLVE_CHOL_DROP}
 
 
@@ -245,6 +248,36 @@ def em_pm_soft(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, M, varn, itera, h_initial, 
     the same signature as PM_beta.em_pm, which takes no all_possibleSymbols)."""
     return _pm(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, None, M, varn, itera, h_initial, h, n_tx,
                partition_r, qamCons, "pm_soft", solve, verbose)
+
+
+def _detector(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera,
+              h_initial, h, mode, solve, verbose):
+    d = _prepare_single(Y_d[:T_d], Y_p[:T_p], Z_p[:T_p], np.asarray(PsiTilde_td)[:, :T_d],
+                        all_possibleSymbols, M, h_initial)
+    hh = None if h is None else np.asarray(h, dtype=complex).reshape(1, -1)
+    res = em_batch(d["y_d"], d["y_p"], d["psi_d"], d["u_p"], d["cons"], varn, itera, d["theta0"],
+                   mode=mode, h_true=hh, solve=solve)
+    return _finish(res, verbose, itera)
+
+
+def em_zf(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera, h_initial, h,
+          verbose=False, solve="chol"):
+    """Zero-forcing detector EM (PMd/all_detectorsvsTd.py:98-133): per symbol
+    z = pinv(H_off) y on the reference's off-by-one channel (:111), the flattened-argmin
+    nearest_symbol_ecul decision (:49-52) as a weight-1 hypothesis, np.linalg.solve M-step,
+    oracle early stop on h.  Where the reference's flat index runs past the hypothesis
+    table (an IndexError there) the trial is flagged SBCE_STATUS_DETECTOR (last_status)."""
+    return _detector(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera,
+                     h_initial, h, "zf", solve, verbose)
+
+
+def em_mmse(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera, h_initial,
+            h, verbose=False, solve="chol"):
+    """MMSE detector EM (PMd/all_detectorsvsTd.py:54-96): z = (H^H H + varn^2 I)^{-1} H^H y
+    (:71), otherwise as em_zf.  (The reference's per-iteration LLF there reads a global
+    Z_d and is never returned; it is not part of the result.)"""
+    return _detector(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera,
+                     h_initial, h, "mmse", solve, verbose)
 
 
 def em_zero_init(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera):

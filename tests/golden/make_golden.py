@@ -255,6 +255,24 @@ def case_pm(name, N, n_tx, n_rx, T_d, T_p, M, varn, itera, seed, r_uniform, r_so
                        pmbeta_theta=np.asarray(th_s).reshape(-1))
 
 
+def case_det(name, N, n_tx, n_rx, T_d, T_p, M, varn, itera, seed):
+    """all_detectorsvsTd.em_zf / em_mmse (off-by-one list channel, flattened-argmin
+    nearest_symbol_ecul, oracle early stop) on north-star data."""
+    ns = load_defs(os.path.join(PMD, "Proposed_method_NMSEvsTp.py"),
+                   N=N, n_tx=n_tx, n_rx=n_rx, beta_min=0.0, beta_max=2 * np.pi)
+    d = _gen_northstar(ns, seed, N, n_tx, n_rx, T_d, T_p, M, varn)
+    cons = _cons(M)
+    ns_all = load_defs(os.path.join(PMD, "all_detectorsvsTd.py"), N=N, n_tx=n_tx, qamCons=cons,
+                       h=d["h"], Z_d=d["Z_d"], beta_min=0.0, beta_max=2 * np.pi)
+    th_z = quiet(ns_all["em_zf"], d["Y_d"], d["Y_p"], T_d, T_p, d["Z_p"], d["Ptd"], d["aps"], M,
+                 varn, itera, d["h0"], d["h"])
+    th_m = quiet(ns_all["em_mmse"], d["Y_d"], d["Y_p"], T_d, T_p, d["Z_p"], d["Ptd"], d["aps"],
+                 M, varn, itera, d["h0"], d["h"])
+    return name, _pack(d, N=N, n_tx=n_tx, n_rx=n_rx, T_d=T_d, T_p=T_p, M=M, varn=varn,
+                       itera=itera, seed=seed, zf_theta=np.asarray(th_z).reshape(-1),
+                       mmse_theta=np.asarray(th_m).reshape(-1))
+
+
 def case_qam():
     """Constellation tables of the vendored komm QAM (PMd/QAM.py:320-322)."""
     return "qam", {f"cons{M}": _cons(M) for M in (4, 16, 64, 256)}
@@ -264,6 +282,8 @@ CASES = {
     "qam": (case_qam, ()),
     "pm_nt4": (case_pm, ("pm_nt4", 3, 4, 4, 24, 8, 4, 0.1, 3, 12, 0, 2)),
     "pm_nt3_m16": (case_pm, ("pm_nt3_m16", 4, 3, 3, 24, 10, 16, 0.3, 3, 13, 1, 1)),
+    "det_nt3": (case_det, ("det_nt3", 4, 3, 4, 30, 10, 4, 0.2, 3, 21)),
+    "det_nt2_m16": (case_det, ("det_nt2_m16", 5, 2, 3, 30, 12, 16, 0.3, 3, 22)),
     "kat1_s7": (case_kat1, (7,)),
     "kat1_s11": (case_kat1, (11,)),
     "kat2_snr": (case_kat2, ()),

@@ -410,3 +410,36 @@ def test_large_l_full_em_pm_soft_vs_oracle(sbce):
         th = em_pm(b["y_d"][i], b["y_p"][i], b["u_p"][i], b["psi_d"][i].T, varn, itera,
                    b["theta0"][i], n_tx, n_rx, 1, b["cons"], soft=True)
         assert rel(res["theta"][i], th) < 1e-8
+
+
+# ---------------------------------------------------------------- ZF / MMSE detector EMs
+@pytest.mark.parametrize("case,itera", [("kat1_s7", 3), ("det_nt3", None), ("det_nt2_m16", None)])
+@pytest.mark.parametrize("kind", ["zf", "mmse"])
+def test_em_detector_matches_reference(sbce, case, itera, kind):
+    d = golden(case)
+    Y_d, Y_p, Z_p = ref_lists(d)
+    fn = sbce.em_zf if kind == "zf" else sbce.em_mmse
+    th = fn(Y_d, Y_p, int(d["T_d"]), int(d["T_p"]), Z_p, d["Ptd"], d["aps"], int(d["M"]),
+            float(d["varn"]), itera or int(d["itera"]), d["h0"].reshape(-1, 1),
+            d["h"].reshape(-1, 1))
+    assert rel(th, d[kind + "_theta"]) < THETA_TOL
+
+
+@pytest.mark.parametrize("shape", [(2, 2, 6, 8, 30, 4, 10), (3, 4, 4, 8, 30, 16, 20),
+                                   (8, 8, 2, 24, 20, 16, 20), (4, 6, 3, 12, 24, 64, 25)])
+def test_detector_estep_vs_oracle(sbce, shape):
+    """Device ZF / MMSE decisions (closed-form flat argmin) vs the oracle, incl. n_tx = 8."""
+    from oracle.detectors import detector_moments
+    n_tx, n_rx, N, T_p, T_d, M, snr = shape
+    varn = float(sbce.signal_model.snr_to_varn(snr))
+    b = sbce.signal_model.synthetic_batch(2, n_tx, n_rx, N, T_p, T_d, M, varn, seed=31)
+    for kind in ("zf", "mmse"):
+        m, S = sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx, kind)
+        for i in range(2):
+            try:
+                m0, S0 = detector_moments(b["theta0"][i], b["y_d"][i], b["psi_d"][i].T, None,
+                                          varn, n_tx, n_rx, kind, cons=b["cons"])
+            except IndexError:
+                continue          # the reference would raise; the device flags the trial
+            assert np.array_equal(m[i], m0)
+            assert np.allclose(S[i], S0, rtol=0, atol=1e-12)

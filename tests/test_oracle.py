@@ -248,3 +248,40 @@ def test_pm_oracle_matches_reference(case, key, soft, r, itera):
     th = em_pm(d["Y_d"], d["Y_p"], u_from_zp(d["Z_p"], n_rx), d["Ptd"], float(d["varn"]), itera,
                d["h0"], n_tx, n_rx, r, cons_from_aps(d["aps"], M), soft=soft, h=d["h"])
     assert rel(th, d[key]) < 1e-12
+
+
+DET_CASES = [("kat1_s7", 3), ("det_nt3", None), ("det_nt2_m16", None)]
+
+
+@pytest.mark.parametrize("case,itera", DET_CASES)
+@pytest.mark.parametrize("kind", ["zf", "mmse"])
+def test_detector_oracle_matches_reference(case, itera, kind):
+    """all_detectorsvsTd.em_zf / em_mmse: off-by-one channel, flattened-argmin decision,
+    oracle early stop."""
+    from oracle.detectors import em_detector
+    d = golden(case)
+    n_tx, n_rx = int(d["n_tx"]), int(d["n_rx"])
+    th = em_detector(d["Y_d"], d["Y_p"], u_from_zp(d["Z_p"], n_rx), d["Ptd"], d["aps"],
+                     float(d["varn"]), itera or int(d["itera"]), d["h0"], n_tx, n_rx, kind,
+                     h=d["h"])
+    assert rel(th, d[kind + "_theta"]) < 1e-12
+
+
+def test_flattened_argmin_closed_form():
+    """nearest_symbol_ecul's flat argmin over (J, n_tx, n_tx) (all_detectorsvsTd.py:49-52)
+    equals the closed form the device kernel uses, incl. the IndexError cases."""
+    import itertools
+    from oracle.detectors import ecul_literal, ecul_index
+    q = golden("qam")
+    rng = np.random.default_rng(0)
+    for M, nt in ((4, 2), (4, 3), (16, 2), (64, 2)):
+        cons = q[f"cons{M}"]
+        aps = np.array(list(itertools.product(*([cons] * nt))))
+        for _ in range(300):
+            z = (rng.standard_normal(nt) + 1j * rng.standard_normal(nt)) * np.abs(cons).max()
+            f = ecul_index(z, aps, M)
+            if f >= len(aps):
+                with pytest.raises(IndexError):
+                    ecul_literal(z, aps)
+            else:
+                assert np.array_equal(ecul_literal(z, aps), aps[f])
