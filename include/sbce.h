@@ -40,7 +40,8 @@
  *   h_true   [B][K]                  optional: enables the reference's oracle
  *                                    early stop (PM.py:110-112)
  *   iters_done [B] int32             optional output: iterations performed
- *   status   [B] int32               per-trial flags (bit 0: non-HPD pivot)
+ *   status   [B] int32               per-trial flags (SBCE_STATUS_*)
+ *   x_dest   [B][T_d][n_tx]          optional output: last-iteration decisions
  */
 #ifndef SBCE_H_
 #define SBCE_H_
@@ -52,7 +53,7 @@
 extern "C" {
 #endif
 
-#define SBCE_ABI_VERSION 1
+#define SBCE_ABI_VERSION 2
 
 /* return codes */
 #define SBCE_OK 0
@@ -116,6 +117,9 @@ typedef struct sbce_ptrs {
     int32_t* status;        /* may be NULL */
     void* workspace;
     size_t workspace_bytes;
+    void* x_dest;           /* may be NULL; hard E-step modes only (HARD/ZF/MMSE):
+                               [B][T_d][n_tx] decisions of the last E-step
+                               (SER/log_max_SER.py:77-78) */
 } sbce_ptrs;
 
 /* ABI version (SBCE_ABI_VERSION). */
@@ -147,6 +151,12 @@ int sbce_estep(const sbce_dims* d, const sbce_ptrs* p, int estep_mode,
  * [B][L][n_rx] complex) are copied there before the solve. */
 int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments,
                int solve_mode, void* r_out, void* rhs_out, void* hip_stream);
+
+/* Per-trial symbol error rates of decisions x_dest against x_d_true ([B][T_d][n_tx]):
+ * ser_out[2b] = the SER expression of SER/log_max_SER.py:162 (count_nonzero of the
+ * (T_d,n_tx,1) - (T_d,1,n_tx) broadcast, / (T_d n_tx)); ser_out[2b+1] = element-wise SER. */
+int sbce_ser(const sbce_dims* d, const void* x_dest, const void* x_d_true, double* ser_out,
+             void* hip_stream);
 
 /* Per-trial NMSE ||theta - h||^2 / ||h||^2 (Proposed_method_NMSEvsTp.py:172). */
 int sbce_nmse(const sbce_dims* d, const void* theta, const void* h_true,

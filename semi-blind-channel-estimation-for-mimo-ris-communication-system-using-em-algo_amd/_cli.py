@@ -25,14 +25,15 @@ def init_distributed():
     return 0
 
 
-def report(xname, xs, curves, out=None, title=""):
+def report(xname, xs, curves, out=None, title="", ylabel="NMSE", logy=True):
     rank = int(os.environ.get("RANK", "0"))
     if rank != 0:
         return
     names = list(curves)
-    print(f"{xname:>8} " + " ".join(f"{n:>14}" for n in names))
+    w = max([14] + [len(n) for n in names])
+    print(f"{xname:>8} " + " ".join(f"{n:>{w}}" for n in names))
     for i, x in enumerate(xs):
-        print(f"{x:>8} " + " ".join(f"{curves[n][i]:14.6e}" for n in names))
+        print(f"{x:>8} " + " ".join(f"{curves[n][i]:{w}.6e}" for n in names))
     if out:
         import numpy as np
         np.savez(out, x=xs, **{k: v for k, v in curves.items()})
@@ -42,7 +43,9 @@ def report(xname, xs, curves, out=None, title=""):
             import matplotlib.pyplot as plt
             for n in names:
                 plt.plot(xs, curves[n], label=n)
-            plt.yscale("log"); plt.xlabel(xname); plt.ylabel("NMSE"); plt.title(title)
+            if logy:
+                plt.yscale("log")
+            plt.xlabel(xname); plt.ylabel(ylabel); plt.title(title)
             plt.grid(True); plt.legend(loc="best")
             plt.savefig(os.path.splitext(out)[0] + ".png")
         except ImportError:

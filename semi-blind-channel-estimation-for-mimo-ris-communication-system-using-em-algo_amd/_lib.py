@@ -10,7 +10,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsbce.so")
 
-SBCE_ABI_VERSION = 1
+SBCE_ABI_VERSION = 2
 SBCE_ESTEP_SOFT = 0
 SBCE_ESTEP_HARD = 1
 SBCE_ESTEP_PM = 2
@@ -24,7 +24,7 @@ SBCE_STATUS_PILOT = 2
 SBCE_STATUS_DETECTOR = 4
 
 EXPORTED = ("sbce_abi_version", "sbce_strerror", "sbce_workspace_bytes", "sbce_em",
-            "sbce_estep", "sbce_mstep", "sbce_nmse")
+            "sbce_estep", "sbce_mstep", "sbce_ser", "sbce_nmse")
 
 
 class SbceUnavailable(RuntimeError):
@@ -47,7 +47,7 @@ class Ptrs(ctypes.Structure):
                 ("x_d_true", ctypes.c_void_p), ("llf", ctypes.c_void_p),
                 ("h_true", ctypes.c_void_p), ("iters_done", ctypes.c_void_p),
                 ("status", ctypes.c_void_p), ("workspace", ctypes.c_void_p),
-                ("workspace_bytes", ctypes.c_size_t)]
+                ("workspace_bytes", ctypes.c_size_t), ("x_dest", ctypes.c_void_p)]
 
 
 _lib = None
@@ -77,6 +77,9 @@ def load(path=None):
     lib.sbce_mstep.restype = ctypes.c_int
     lib.sbce_mstep.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Ptrs), ctypes.c_void_p,
                                ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.sbce_ser.restype = ctypes.c_int
+    lib.sbce_ser.argtypes = [ctypes.POINTER(Dims), ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_void_p, ctypes.c_void_p]
     lib.sbce_nmse.restype = ctypes.c_int
     lib.sbce_nmse.argtypes = [ctypes.POINTER(Dims), ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_void_p, ctypes.c_void_p]

@@ -108,6 +108,9 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     if (!estep_supported(pb, estep_mode) || !chol_supported(pb)) return SBCE_EUNSUPPORTED;
     if (solve_mode != SBCE_SOLVE_CHOL && solve_mode != SBCE_SOLVE_CHOL_DROP) return SBCE_EINVAL;
     if (p->llf && !p->x_d_true) return SBCE_EINVAL;
+    const bool hard = estep_mode == SBCE_ESTEP_HARD || estep_mode == SBCE_ESTEP_ZF ||
+                      estep_mode == SBCE_ESTEP_MMSE;
+    if (p->x_dest && (!hard || !aligned16(p->x_dest))) return SBCE_EINVAL;
     if (pb.B == 0 || iters == 0) return SBCE_OK;
     hipStream_t s = (hipStream_t)hip_stream;
     const Carve c = carve(pb);
@@ -141,6 +144,7 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
                                            it, s))))
             return rc;
     }
+    if (p->x_dest && (rc = hip_rc(launch_decisions(pb, ea.mom, (cd*)p->x_dest, s)))) return rc;
     if (!early && p->iters_done) {
         // every trial ran all iterations: fill with `iters` via a tiny host-free memset pattern
         // (int32 fill is done on device by hipMemsetD32Async)
@@ -203,6 +207,15 @@ int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int 
 int sbce_debug_chol_clock(unsigned long long* out32, int reset) {
     if (reset) return hip_rc(chol_debug_clock_reset());
     return out32 ? hip_rc(chol_debug_clock(out32)) : SBCE_EINVAL;
+}
+
+int sbce_ser(const sbce_dims* d, const void* x_dest, const void* x_d_true, double* ser_out,
+             void* hip_stream) {
+    Problem pb;
+    if (!make_problem(d, pb) || !x_dest || !x_d_true || !ser_out) return SBCE_EINVAL;
+    if (pb.B == 0) return SBCE_OK;
+    return hip_rc(launch_ser(pb, (const cd*)x_dest, (const cd*)x_d_true, ser_out,
+                             (hipStream_t)hip_stream));
 }
 
 int sbce_nmse(const sbce_dims* d, const void* theta, const void* h_true, double* nmse_out,

@@ -171,6 +171,42 @@ __global__ __launch_bounds__(256) void nmse_kernel(const cd* theta, const cd* h,
     if (threadIdx.x == 0) out[b] = num / den;
 }
 
+// Last-iteration hard decisions (PMd/SER/log_max_SER.py:77-78): for the hard E-step modes
+// m_t IS the decided hypothesis (weight 1), so x_dest[b][t] = m_t of the final E-step.
+__global__ __launch_bounds__(256) void decisions_kernel(const cd* mom, cd* xdest, long n, int NT) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const long t = e / NT;
+    xdest[e] = mom[t * (NT + NT * NT) + (e - t * NT)];
+}
+
+// Per-trial SER of the decisions (PMd/SER/log_max_SER.py:162):
+//   out[b][0] = count_nonzero(array(X_d) - array(X_dest)) / (T_d n_tx) with the script's
+//               shapes (T_d, n_tx, 1) - (T_d, 1, n_tx): every (a, a') pair of a symbol is
+//               compared (the reference's broadcast), so it is not 0 for exact decisions;
+//   out[b][1] = the element-wise symbol error rate.
+__global__ __launch_bounds__(256) void ser_kernel(const cd* xdest, const cd* xtrue, double* out,
+                                                  int Td, int NT) {
+    __shared__ double sh[4];
+    const int b = blockIdx.x;
+    double pairs = 0.0, elem = 0.0;
+    const cd* xd = xdest + (size_t)b * Td * NT;
+    const cd* xt = xtrue + (size_t)b * Td * NT;
+    for (int e = threadIdx.x; e < Td * NT * NT; e += blockDim.x) {
+        const int t = e / (NT * NT), r = e - t * NT * NT, a = r / NT, a2 = r - a * NT;
+        const cd u = xt[t * NT + a], v = xd[t * NT + a2];
+        const bool ne = u.x != v.x || u.y != v.y;
+        pairs += ne ? 1.0 : 0.0;
+        if (a == a2) elem += ne ? 1.0 : 0.0;
+    }
+    pairs = block_sum(pairs, sh);
+    elem = block_sum(elem, sh);
+    if (threadIdx.x == 0) {
+        out[2 * b] = pairs / ((double)Td * NT);
+        out[2 * b + 1] = elem / ((double)Td * NT);
+    }
+}
+
 // LLF of "Proposed method/IterationsvsLLF.py":49-50,76:
 //   -T_d n_tx ln M - (T_d+T_p) ln(pi varn^2) - (||Y_p - Z_p th|| + ||Y_d - Z_d th||)/varn^2
 // with Z_d built from the TRUE symbols (genie) and UNsquared norms.
@@ -270,6 +306,20 @@ hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t
 
 hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* out, hipStream_t s) {
     hipLaunchKernelGGL(nmse_kernel, dim3(pb.B), dim3(256), 0, s, theta, h, out, pb.K);
+    return hipGetLastError();
+}
+
+hipError_t launch_decisions(const Problem& pb, const cd* mom, cd* xdest, hipStream_t s) {
+    const long n = (long)pb.B * pb.Td * pb.NT;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(decisions_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, mom,
+                       xdest, n, pb.NT);
+    return hipGetLastError();
+}
+
+hipError_t launch_ser(const Problem& pb, const cd* xdest, const cd* xtrue, double* out,
+                      hipStream_t s) {
+    hipLaunchKernelGGL(ser_kernel, dim3(pb.B), dim3(256), 0, s, xdest, xtrue, out, pb.Td, pb.NT);
     return hipGetLastError();
 }
 

@@ -131,6 +131,9 @@ hipError_t launch_chol_large(const Problem& pb, const MstepArgs& a, hipStream_t 
 hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w, hipStream_t s);
 hipError_t chol_debug_clock(unsigned long long* out);   // diagnostic (SBCE_CHOL_SKIP & 64)
 hipError_t chol_debug_clock_reset();
+hipError_t launch_decisions(const Problem& pb, const cd* mom, cd* xdest, hipStream_t s);
+hipError_t launch_ser(const Problem& pb, const cd* xdest, const cd* xtrue, double* out,
+                      hipStream_t s);
 hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* out,
                        hipStream_t s);
 hipError_t launch_llf(const Problem& pb, const cd* theta, const cd* yp, const cd* up,

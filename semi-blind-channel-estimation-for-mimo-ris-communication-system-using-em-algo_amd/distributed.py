@@ -25,29 +25,35 @@ def shard(n_trials, world, rank):
 class Accumulators:
     """Per-sweep-point sums, packed into one float64 vector for a single all-reduce."""
 
-    def __init__(self, n_points, n_iters=0):
+    def __init__(self, n_points, n_iters=0, n_extra=0):
         self.n_points = n_points
         self.n_iters = n_iters
+        self.n_extra = n_extra
         self.nmse = np.zeros(n_points)
         self.count = np.zeros(n_points)
         self.llf = np.zeros((n_points, n_iters))
+        self.extra = np.zeros((n_points, n_extra))    # e.g. SER sums (sweeps.ser_vs_snr)
 
-    def add(self, point, nmse_values, llf_values=None):
+    def add(self, point, nmse_values, llf_values=None, extra_values=None):
         v = np.sort(np.asarray(nmse_values, dtype=float).reshape(-1))   # order-independent
         self.nmse[point] += float(np.sum(v))
         self.count[point] += v.size
         if llf_values is not None and self.n_iters:
             self.llf[point] += np.sum(np.asarray(llf_values, dtype=float).reshape(-1, self.n_iters),
                                       axis=0)
+        if extra_values is not None and self.n_extra:
+            e = np.asarray(extra_values, dtype=float).reshape(-1, self.n_extra)
+            self.extra[point] += np.sort(e, axis=0).sum(axis=0)
 
     def pack(self):
-        return np.concatenate([self.nmse, self.count, self.llf.reshape(-1)])
+        return np.concatenate([self.nmse, self.count, self.llf.reshape(-1), self.extra.reshape(-1)])
 
     def unpack(self, vec):
-        P, I = self.n_points, self.n_iters
+        P, I, E = self.n_points, self.n_iters, self.n_extra
         self.nmse = vec[:P].copy()
         self.count = vec[P:2 * P].copy()
-        self.llf = vec[2 * P:].reshape(P, I).copy()
+        self.llf = vec[2 * P:2 * P + P * I].reshape(P, I).copy()
+        self.extra = vec[2 * P + P * I:].reshape(P, E).copy()
         return self
 
     def allreduce(self, dist=None, device=None):
@@ -66,3 +72,6 @@ class Accumulators:
 
     def mean_llf(self):
         return self.llf / np.maximum(self.count, 1)[:, None]
+
+    def mean_extra(self):
+        return self.extra / np.maximum(self.count, 1)[:, None]

@@ -57,7 +57,8 @@ _SOLVES = {"chol": _lib.SBCE_SOLVE_CHOL, "drop": _lib.SBCE_SOLVE_CHOL_DROP}
 
 
 def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_true=None,
-             h_true=None, solve="chol", return_device=False, partition_r=0):
+             h_true=None, solve="chol", return_device=False, partition_r=0,
+             return_decisions=False):
     """Run ``itera`` EM iterations on a batch of independent trials.
 
     Array layouts (complex128, batch-major, include/sbce.h):
@@ -66,7 +67,9 @@ def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_t
       cons (M,), theta0 (B,K) with K = P*n_tx*n_rx.
     Optional: x_d_true (B,T_d,n_tx) -> per-iteration LLF (IterationsvsLLF.py:76);
     h_true (B,K) -> the reference's oracle early stop (PM.py:110-112).
-    mode: "soft" | "hard" | "pm" | "pm_soft"; partition_r selects the PM list size.
+    mode: "soft" | "hard" | "pm" | "pm_soft" | "zf" | "mmse"; partition_r selects the PM
+    list size.  return_decisions (hard modes): x_dest (B,T_d,n_tx), the last E-step's
+    decisions (SER/log_max_SER.py:77-78).
     Inputs may be numpy arrays or CUDA complex128 tensors (used in place).
     Returns dict(theta (B,K), llf (B,itera) or None, status (B,), iters_done (B,)).
     """
@@ -101,15 +104,20 @@ def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_t
     Xd = dev(x_d_true)
     Ht = dev(h_true)
     llf = torch.zeros((B, max(itera, 1)), dtype=torch.float64, device="cuda") if Xd is not None else None
+    xdest = (torch.zeros((B, T_d, n_tx), dtype=torch.complex128, device="cuda")
+             if return_decisions else None)
     ptrs = _lib.Ptrs(Yd.data_ptr(), Yp.data_ptr() if T_p else Yd.data_ptr(), Ps.data_ptr(),
                      Up.data_ptr() if T_p else Yd.data_ptr(), Cs.data_ptr(), th.data_ptr(),
                      Xd.data_ptr() if Xd is not None else None,
                      llf.data_ptr() if llf is not None else None,
                      Ht.data_ptr() if Ht is not None else None, iters_done.data_ptr(),
-                     status.data_ptr(), ws.data_ptr(), ws.numel())
+                     status.data_ptr(), ws.data_ptr(), ws.numel(),
+                     xdest.data_ptr() if xdest is not None else None)
     stream = torch.cuda.current_stream().cuda_stream
     _lib.check(lib.sbce_em(dims, ptrs, int(itera), _MODES[mode], _SOLVES[solve], stream), "sbce_em")
     out = dict(theta=th, llf=llf, status=status, iters_done=iters_done)
+    if xdest is not None:
+        out["x_dest"] = xdest
     if return_device:
         return out
     torch.cuda.current_stream().synchronize()
@@ -278,6 +286,34 @@ def em_mmse(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, 
     Z_d and is never returned; it is not part of the result.)"""
     return _detector(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera,
                      h_initial, h, "mmse", solve, verbose)
+
+
+def em_ml_ser(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera,
+              h_initial, verbose=False, solve="chol"):
+    """Log-max EM of PMd/SER/log_max_SER.py:51-84: returns (theta (K,1), X_dest) with
+    X_dest the list of (1, n_tx) argmax decisions of the last iteration (:77-78)."""
+    d = _prepare_single(Y_d[:T_d], Y_p[:T_p], Z_p[:T_p], np.asarray(PsiTilde_td)[:, :T_d],
+                        all_possibleSymbols, M, h_initial)
+    res = em_batch(d["y_d"], d["y_p"], d["psi_d"], d["u_p"], d["cons"], varn, itera, d["theta0"],
+                   mode="hard", solve=solve, return_decisions=True)
+    th = _finish(res, verbose, itera)
+    return th, [x[None, :] for x in res["x_dest"][0]]
+
+
+def ser_batch(x_dest, x_d_true):
+    """Per-trial SER on the device (sbce_ser): (ser_reference, ser_elementwise), the first
+    being the expression of PMd/SER/log_max_SER.py:162."""
+    torch = _torch()
+    lib = _lib.load()
+    xd = x_dest if isinstance(x_dest, torch.Tensor) else _dev(torch, x_dest, np.complex128)
+    xt = x_d_true if isinstance(x_d_true, torch.Tensor) else _dev(torch, x_d_true, np.complex128)
+    B, T_d, n_tx = xd.shape
+    dims = _lib.Dims(B, n_tx, 1, 1, 0, T_d, 2, 0, 1.0)
+    out = torch.zeros((B, 2), dtype=torch.float64, device="cuda")
+    _lib.check(lib.sbce_ser(dims, xd.contiguous().data_ptr(), xt.contiguous().data_ptr(),
+                            out.data_ptr(), torch.cuda.current_stream().cuda_stream), "sbce_ser")
+    out = out.cpu().numpy()
+    return out[:, 0], out[:, 1]
 
 
 def em_zero_init(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera):

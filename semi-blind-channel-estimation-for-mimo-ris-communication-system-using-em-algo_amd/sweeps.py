@@ -4,6 +4,7 @@ estimator with every trial of a sweep point batched into ONE sbce_em call.
   nmse_vs_tp   "Proposed method/Proposed_method_NMSEvsTp.py":133-176
   nmse_vs_td   "Proposed method/Proposed_method_NMSEvsTd.py":121-157
   nmse_vs_snr  "Proposed method/SNR/all_Detectors.py":331-395 (exact and log-max EMs)
+  ser_vs_snr   "Proposed method/SER/log_max_SER.py":124-167 (log-max EM decisions)
 
 Data generation (host, NumPy):
   replay=True   the reference's exact legacy-RandomState call order after
@@ -18,7 +19,7 @@ import numpy as np
 
 from . import signal_model as sm
 from .distributed import Accumulators, shard
-from .em import em_batch
+from .em import em_batch, ser_batch
 from .qam import qam_constellation
 
 
@@ -169,3 +170,62 @@ def nmse_vs_snr(SNR=(-5, 0, 5, 10, 15, 20), T_d=50, T_p=12, N=10, n_rx=2, n_tx=2
         acc.allreduce(dist)
         out[mode] = acc.mean_nmse()
     return np.asarray(SNR), out
+
+
+def gen_ser(SNR=(-5, 0, 5, 10, 15, 20), T_d=50, T_p=20, N=30, n_rx=2, n_tx=2, monte_iter=75, M=4,
+            power=10.0, seed=0, replay=True, varh=1.0, keep=None):
+    """Synthetic data of PMd/SER/log_max_SER.py:150-160 in the reference draw order: per
+    trial channelMatrix, symbols(T_d), irsMatrix (pilot phases (N+1) x T_p with a zero last
+    row; ones row inserted into the data phases), pilotSymbols, then per SNR
+    receivedSignals."""
+    varns = sm.snr_to_varn(SNR, power)
+    keep = set(range(monte_iter)) if keep is None else set(keep)
+    points = [[] for _ in SNR]
+    if replay:
+        np.random.seed(seed)
+    for i in range(monte_iter):
+        rs = None if replay else _trial_rng(seed, i)
+        if not replay and i not in keep:
+            continue
+        h = sm.channel_matrix(n_tx, n_rx, N, varh, rs=rs)
+        X_d, _ = sm.symbols(n_tx, M, T_d, rs=rs)
+        Ptp, Ptd = sm.irs_matrix(T_p, T_d, N, pilot="dft_n", rs=rs)
+        Ptd = sm.insert_direct(Ptd)
+        X_p = sm.pilot_symbols(n_tx, M, T_p, rs=rs)
+        for k in range(len(SNR)):
+            Y_p, Y_d, U_p, _, h0 = sm.received_signals(T_p, T_d, Ptp, Ptd, n_rx, n_tx, X_d, X_p, h,
+                                                       varns[k], rs=rs)
+            if i in keep:
+                points[k].append(dict(Y_d=Y_d, Y_p=Y_p, Psi_d=Ptd, U_p=U_p, h0=h0, h=h,
+                                      X_d=np.stack([x.reshape(-1) for x in X_d])))
+    return points, varns
+
+
+def ser_vs_snr(SNR=(-5, 0, 5, 10, 15, 20), T_d=50, T_p=20, N=30, n_rx=2, n_tx=2, itera=5,
+               monte_iter=75, M=4, power=10.0, seed=0, replay=True, varh=1.0):
+    """SER per SNR of the log-max EM's last-iteration decisions (PMd/SER/log_max_SER.py:
+    constants :124-147, driver :150-167).  Returns (SNR, ser_reference, ser_elementwise,
+    nmse): ser_reference is the script's own expression (:162, a (T_d, n_tx, n_tx)
+    broadcast count), ser_elementwise the per-symbol-entry error rate.
+
+    Reference draw order per trial: channelMatrix, symbols(T_d), irsMatrix (ones row
+    inserted, pilot phases (N+1) x T_p with a zero last row), pilotSymbols, then per SNR
+    receivedSignals (gen_ser)."""
+    dist, world, rank = _dist()
+    mine = shard(monte_iter, world, rank).tolist()
+    points, varns = gen_ser(SNR, T_d, T_p, N, n_rx, n_tx, monte_iter, M, power, seed, replay,
+                            varh, keep=mine)
+    acc = Accumulators(len(SNR), n_extra=2)
+    cons = qam_constellation(M)
+    for pt, trials in enumerate(points):
+        if not trials:
+            continue
+        b = _pack(trials, None)
+        r = em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], cons, varns[pt], itera,
+                     b["theta0"], mode="hard", return_decisions=True)
+        x_true = np.stack([t["X_d"] for t in trials])
+        s_ref, s_el = ser_batch(r["x_dest"], x_true)
+        acc.add(pt, _nmse(r["theta"], b["h"]), extra_values=np.stack([s_ref, s_el], axis=1))
+    acc.allreduce(dist)
+    ser = acc.mean_extra()
+    return np.asarray(SNR), ser[:, 0], ser[:, 1], acc.mean_nmse()

@@ -273,6 +273,36 @@ def case_det(name, N, n_tx, n_rx, T_d, T_p, M, varn, itera, seed):
                        mmse_theta=np.asarray(th_m).reshape(-1))
 
 
+def case_ser():
+    """PMd/SER/log_max_SER.py: log-max em (:51-84) returning the last iteration's argmax
+    decisions X_dest, and the script's SER expression (:162), on the script's own data
+    helpers and draw order (:150-160), one trial, two SNR points."""
+    N, n_tx, n_rx, T_d, T_p, M, itera, SNR = 6, 2, 2, 30, 20, 4, 3, (0, 10)
+    ns = load_defs(os.path.join(PMD, "SER", "log_max_SER.py"), N=N, n_tx=n_tx, n_rx=n_rx,
+                   beta_min=0.0, beta_max=2 * np.pi, varh=1.0, amp=1)
+    np.random.seed(5)
+    h = quiet(ns["channelMatrix"], n_tx, n_rx, N, 1.0)
+    X_d, aps = ns["symbols"](n_tx, M, T_d)
+    Ptp, Ptd = ns["irsMatrix"](T_p, T_d, N, 0.0, 1)
+    Ptd = np.insert(Ptd, 0, np.ones((1, T_d), dtype="complex128"), axis=0)
+    X_p = ns["pilotSymbols"](n_tx, M, T_p)
+    out = dict(N=N, n_tx=n_tx, n_rx=n_rx, T_d=T_d, T_p=T_p, M=M, itera=itera,
+               snr=np.asarray(SNR), h=h, X_d=np.stack(X_d)[..., 0], aps=aps, Ptp=Ptp, Ptd=Ptd,
+               X_p=np.stack(X_p)[..., 0])
+    for k, snr in enumerate(SNR):
+        varn = 10 / np.power(10, snr / 10)
+        Y_p, Y_d, Z_p, Z_d, h0 = ns["receivedSignals"](T_p, T_d, Ptp, Ptd, n_rx, n_tx, X_d, X_p,
+                                                       h, varn, M)
+        ns["Z_d"] = Z_d                      # em's LLF line (:83) reads the global Z_d
+        th, X_dest = quiet(ns["em"], Y_d, Y_p, T_d, T_p, Z_p, Ptd, aps, M, varn, itera, h0)
+        ser = np.count_nonzero(np.array(X_d) - np.array(X_dest)) / (T_d * n_tx)
+        out.update({f"varn{k}": varn, f"Y_p{k}": np.stack(Y_p)[..., 0],
+                    f"Y_d{k}": np.stack(Y_d)[..., 0], f"Z_p{k}": np.stack(Z_p),
+                    f"h0{k}": np.asarray(h0).reshape(-1), f"theta{k}": np.asarray(th).reshape(-1),
+                    f"X_dest{k}": np.stack(X_dest)[:, 0, :], f"ser{k}": ser})
+    return "ser_logmax", out
+
+
 def case_qam():
     """Constellation tables of the vendored komm QAM (PMd/QAM.py:320-322)."""
     return "qam", {f"cons{M}": _cons(M) for M in (4, 16, 64, 256)}
@@ -282,6 +312,7 @@ CASES = {
     "qam": (case_qam, ()),
     "pm_nt4": (case_pm, ("pm_nt4", 3, 4, 4, 24, 8, 4, 0.1, 3, 12, 0, 2)),
     "pm_nt3_m16": (case_pm, ("pm_nt3_m16", 4, 3, 3, 24, 10, 16, 0.3, 3, 13, 1, 1)),
+    "ser_logmax": (case_ser, ()),
     "det_nt3": (case_det, ("det_nt3", 4, 3, 4, 30, 10, 4, 0.2, 3, 21)),
     "det_nt2_m16": (case_det, ("det_nt2_m16", 5, 2, 3, 30, 12, 16, 0.3, 3, 22)),
     "kat1_s7": (case_kat1, (7,)),

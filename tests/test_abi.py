@@ -38,8 +38,9 @@ def test_struct_layout_matches_c(sbce, tmp_path):
 #include <stddef.h>
 #include "sbce.h"
 int main(void) {
-  printf("%zu %zu %zu %zu\n", sizeof(sbce_dims), offsetof(sbce_dims, varn),
-         sizeof(sbce_ptrs), offsetof(sbce_ptrs, workspace_bytes));
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(sbce_dims), offsetof(sbce_dims, varn),
+         sizeof(sbce_ptrs), offsetof(sbce_ptrs, workspace_bytes), offsetof(sbce_ptrs, x_dest),
+         offsetof(sbce_dims, partition_r));
   return 0;
 }''')
     exe = tmp_path / "probe"
@@ -48,7 +49,8 @@ int main(void) {
     out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
     L = sbce._lib
     assert [int(v) for v in out] == [ctypes.sizeof(L.Dims), L.Dims.varn.offset,
-                                     ctypes.sizeof(L.Ptrs), L.Ptrs.workspace_bytes.offset]
+                                     ctypes.sizeof(L.Ptrs), L.Ptrs.workspace_bytes.offset,
+                                     L.Ptrs.x_dest.offset, L.Dims.partition_r.offset]
 
 
 def test_workspace_and_validation_without_gpu(sbce):
@@ -59,7 +61,7 @@ def test_workspace_and_validation_without_gpu(sbce):
     Lw = 65 * 4
     expect = 1000 * 256 * 20 * 16 + 1000 * Lw * Lw * 16 + 1000 * Lw * 4 * 16
     assert expect <= n <= expect + 4 * 256 + 4000
-    bad = L.Dims(1, 9, 4, 65, 16, 256, 16, 0, 0.1)     # n_tx > 4
+    bad = L.Dims(1, 9, 4, 65, 16, 256, 16, 0, 0.1)     # n_tx > 8
     nb = ctypes.c_size_t(0)
     assert lib.sbce_workspace_bytes(ctypes.byref(bad), ctypes.byref(nb)) == -1
     bad2 = L.Dims(1, 2, 2, 5, 4, 8, 4, 0, 0.0)         # varn must be > 0

@@ -443,3 +443,31 @@ def test_detector_estep_vs_oracle(sbce, shape):
                 continue          # the reference would raise; the device flags the trial
             assert np.array_equal(m[i], m0)
             assert np.allclose(S[i], S0, rtol=0, atol=1e-12)
+
+
+# ---------------------------------------------------------------- SER path
+def test_em_ml_ser_matches_reference(sbce):
+    """log_max_SER.em: theta and the last iteration's decisions X_dest; device SER."""
+    d = golden("ser_logmax")
+    for k in range(2):
+        Y_d = [y[:, None] for y in d[f"Y_d{k}"]]
+        Y_p = [y[:, None] for y in d[f"Y_p{k}"]]
+        th, X_dest = sbce.em_ml_ser(Y_d, Y_p, int(d["T_d"]), int(d["T_p"]), list(d[f"Z_p{k}"]),
+                                    d["Ptd"], d["aps"], int(d["M"]), float(d[f"varn{k}"]),
+                                    int(d["itera"]), d[f"h0{k}"].reshape(-1, 1))
+        assert rel(th, d[f"theta{k}"]) < THETA_TOL
+        assert len(X_dest) == int(d["T_d"]) and X_dest[0].shape == (1, int(d["n_tx"]))
+        assert np.array_equal(np.concatenate(X_dest), d[f"X_dest{k}"])
+        s_ref, s_el = sbce.ser_batch(np.concatenate(X_dest)[None], d["X_d"][None])
+        assert s_ref[0] == float(d[f"ser{k}"])
+        assert s_el[0] == np.count_nonzero(d["X_d"] != d[f"X_dest{k}"]) / d["X_d"].size
+
+
+def test_ser_sweep_entry_point(sbce):
+    d = golden("ser_logmax")
+    snr, s_ref, s_el, nm = sbce.sweeps.ser_vs_snr(tuple(int(x) for x in d["snr"]), int(d["T_d"]),
+                                                  int(d["T_p"]), int(d["N"]), int(d["n_rx"]),
+                                                  int(d["n_tx"]), int(d["itera"]), 1, int(d["M"]),
+                                                  10.0, 5)
+    assert list(s_ref) == [float(d["ser0"]), float(d["ser1"])]
+    assert np.all(s_el <= s_ref) and np.all(np.isfinite(nm))

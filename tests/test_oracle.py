@@ -285,3 +285,33 @@ def test_flattened_argmin_closed_form():
                     ecul_literal(z, aps)
             else:
                 assert np.array_equal(ecul_literal(z, aps), aps[f])
+
+
+def test_ser_oracle_matches_reference():
+    """SER/log_max_SER.py em decisions + the script's SER expression (:162)."""
+    from oracle.ser import em_hard_with_decisions, ser_reference, ser_elementwise
+    d = golden("ser_logmax")
+    n_rx = int(d["n_rx"])
+    for k in range(2):
+        th, dec = em_hard_with_decisions(d[f"Y_d{k}"], d[f"Y_p{k}"], u_from_zp(d[f"Z_p{k}"], n_rx),
+                                         d["Ptd"], d["aps"], float(d[f"varn{k}"]), int(d["itera"]),
+                                         d[f"h0{k}"])
+        assert rel(th, d[f"theta{k}"]) < 1e-12
+        assert np.array_equal(dec, d[f"X_dest{k}"])
+        assert ser_reference(d["X_d"], d[f"X_dest{k}"]) == float(d[f"ser{k}"])
+        assert 0.0 <= ser_elementwise(d["X_d"], dec) <= ser_reference(d["X_d"], dec)
+
+
+def test_ser_sweep_replays_reference_data(sbce):
+    """sweeps.gen_ser reproduces log_max_SER.py's draw order (data of the fixture)."""
+    d = golden("ser_logmax")
+    points, varns = sbce.sweeps.gen_ser(tuple(int(x) for x in d["snr"]), int(d["T_d"]),
+                                        int(d["T_p"]), int(d["N"]), int(d["n_rx"]),
+                                        int(d["n_tx"]), 1, int(d["M"]), 10.0, 5)
+    for k in range(2):
+        t = points[k][0]
+        # Y = Z h is a dense matmul in the reference: equal to rounding, not bitwise
+        assert rel(t["Y_d"], d[f"Y_d{k}"]) < 1e-13 and rel(t["Y_p"], d[f"Y_p{k}"]) < 1e-13
+        assert rel(t["h0"], d[f"h0{k}"]) < 1e-12
+        assert np.array_equal(t["X_d"], d["X_d"])
+        assert abs(varns[k] - float(d[f"varn{k}"])) < 1e-15
