@@ -42,6 +42,7 @@
  *   iters_done [B] int32             optional output: iterations performed
  *   status   [B] int32               per-trial flags (SBCE_STATUS_*)
  *   x_dest   [B][T_d][n_tx]          optional output: last-iteration decisions
+ *   x_sup    [B][T_d][n_tx]          optional superimposed pilot symbols
  */
 #ifndef SBCE_H_
 #define SBCE_H_
@@ -120,6 +121,9 @@ typedef struct sbce_ptrs {
     void* x_dest;           /* may be NULL; hard E-step modes only (HARD/ZF/MMSE):
                                [B][T_d][n_tx] decisions of the last E-step
                                (SER/log_max_SER.py:77-78) */
+    const void* x_sup;      /* may be NULL; SOFT/HARD only: [B][T_d][n_tx] pilot
+                               symbols superimposed on the data, hypotheses x_j + x_sup[t]
+                               (Parallel/ParallelProtocol_Tp.py:63-86; t_p is then 0) */
 } sbce_ptrs;
 
 /* ABI version (SBCE_ABI_VERSION). */

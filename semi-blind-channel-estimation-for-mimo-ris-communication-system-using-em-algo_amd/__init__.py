@@ -9,12 +9,12 @@ from . import _lib, qam, signal_model, layout, distributed  # noqa: F401
 from . import sweeps  # noqa: F401
 from ._lib import SbceUnavailable, SbceError  # noqa: F401
 from .em import (  # noqa: F401
-    em, em_ml, em_llf, em_ml_llf, em_ml_ser, em_pm, em_pm_soft, em_zf, em_mmse, em_zero_init,
-    em_batch, ser_batch, estep_batch,
+    em, em_ml, em_llf, em_ml_llf, em_ml_ser, em_pm, em_pm_soft, em_zf, em_mmse, em_superimposed,
+    em_zero_init, em_batch, ser_batch, estep_batch,
     mstep_batch, nmse_batch, EMEngine,
 )
 
 __all__ = ["em", "em_ml", "em_llf", "em_ml_llf", "em_ml_ser", "em_pm", "em_pm_soft", "em_zf",
-           "em_mmse", "ser_batch",
+           "em_mmse", "em_superimposed", "ser_batch",
            "em_zero_init", "em_batch",
            "SbceUnavailable", "SbceError", "qam", "signal_model"]

@@ -47,7 +47,8 @@ class Ptrs(ctypes.Structure):
                 ("x_d_true", ctypes.c_void_p), ("llf", ctypes.c_void_p),
                 ("h_true", ctypes.c_void_p), ("iters_done", ctypes.c_void_p),
                 ("status", ctypes.c_void_p), ("workspace", ctypes.c_void_p),
-                ("workspace_bytes", ctypes.c_size_t), ("x_dest", ctypes.c_void_p)]
+                ("workspace_bytes", ctypes.c_size_t), ("x_dest", ctypes.c_void_p),
+                ("x_sup", ctypes.c_void_p)]
 
 
 _lib = None

@@ -16,7 +16,7 @@ constexpr size_t kAlign = 256;
 size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 struct Carve {
-    size_t mom, R, rhs, done, tol, winv, ppsi, pS, total;
+    size_t mom, R, rhs, done, ysh, tol, winv, ppsi, pS, total;
 };
 
 bool make_problem(const sbce_dims* d, Problem& pb) {
@@ -39,7 +39,8 @@ Carve carve(const Problem& pb) {
     c.R = align_up(c.mom + (size_t)pb.B * pb.Td * MS * sizeof(cd));
     c.rhs = align_up(c.R + (size_t)pb.B * pb.L * pb.L * sizeof(cd));
     c.done = align_up(c.rhs + (size_t)pb.B * pb.L * pb.NR * sizeof(cd));
-    c.tol = align_up(c.done + (size_t)pb.B * sizeof(int32_t));
+    c.ysh = align_up(c.done + (size_t)pb.B * sizeof(int32_t));         // superimposed pilots
+    c.tol = align_up(c.ysh + (size_t)pb.B * pb.Td * pb.NR * sizeof(cd));
     c.winv = c.ppsi = c.pS = c.tol;
     c.total = c.tol;
     if (pb.L > kLargeL) {                    // tiled large-L M-step (mstep_large.hip)
@@ -111,6 +112,9 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     const bool hard = estep_mode == SBCE_ESTEP_HARD || estep_mode == SBCE_ESTEP_ZF ||
                       estep_mode == SBCE_ESTEP_MMSE;
     if (p->x_dest && (!hard || !aligned16(p->x_dest))) return SBCE_EINVAL;
+    if (p->x_sup && ((estep_mode != SBCE_ESTEP_SOFT && estep_mode != SBCE_ESTEP_HARD) ||
+                     !aligned16(p->x_sup)))
+        return SBCE_EINVAL;
     if (pb.B == 0 || iters == 0) return SBCE_OK;
     hipStream_t s = (hipStream_t)hip_stream;
     const Carve c = carve(pb);
@@ -131,8 +135,19 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     ma.status = p->status; ma.done = ea.done; ma.solve_mode = solve_mode;
     set_large(ma, ws, c);
 
+    EstepArgs eas = ea;                      // superimposed pilots: E-step on y - H x_p
+    if (p->x_sup) eas.yd = (const cd*)(ws + c.ysh);
     for (int it = 0; it < iters; ++it) {
-        if ((rc = hip_rc(launch_estep(pb, ea, estep_mode, s)))) return rc;
+        if (p->x_sup) {
+            if ((rc = hip_rc(launch_sup_shift_y(pb, ea.yd, ea.psid, ea.theta, (const cd*)p->x_sup,
+                                                (cd*)(ws + c.ysh), ea.done, s))))
+                return rc;
+            if ((rc = hip_rc(launch_estep(pb, eas, estep_mode, s)))) return rc;
+            if ((rc = hip_rc(launch_sup_shift_mom(pb, ea.mom, (const cd*)p->x_sup, ea.done, s))))
+                return rc;
+        } else if ((rc = hip_rc(launch_estep(pb, ea, estep_mode, s)))) {
+            return rc;
+        }
         if ((rc = hip_rc(launch_mstep_build(pb, ma, s)))) return rc;
         if ((rc = hip_rc(launch_chol_solve(pb, ma, s)))) return rc;
         if (p->llf &&

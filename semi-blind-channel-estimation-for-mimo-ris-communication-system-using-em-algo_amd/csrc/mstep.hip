@@ -171,6 +171,51 @@ __global__ __launch_bounds__(256) void nmse_kernel(const cd* theta, const cd* h,
     if (threadIdx.x == 0) out[b] = num / den;
 }
 
+// Superimposed pilots ("Parallel/ParallelProtocol_Tp.py":63-86): hypotheses x_j + x_p,t.
+// The E-step runs on y'_t = y_t - H_t x_p,t (thread per (symbol, receive antenna)) and
+// the moments of x_j + x_p,t follow by the shift m' = m + x_p,
+// S' = S + m x_p^H + x_p m^H + x_p x_p^H (thread per symbol).
+__global__ __launch_bounds__(256) void sup_shift_y_kernel(const cd* yd, const cd* psid,
+                                                          const cd* theta, const cd* xsup,
+                                                          cd* yout, const int32_t* done, long n,
+                                                          int Td, int P, int NT, int NR) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const long sym = e / NR;
+    const int r = (int)(e - sym * NR);
+    const int b = (int)(sym / Td);
+    if (done && done[b]) return;
+    const cd* th = theta + (size_t)b * P * NT * NR;
+    const cd* ps = psid + (size_t)sym * P;
+    const cd* xp = xsup + (size_t)sym * NT;
+    cd acc = yd[e];
+    for (int p = 0; p < P; ++p) {
+        cd hx = czero();
+        for (int a = 0; a < NT; ++a) hx = cfma(hx, th[(p * NT + a) * NR + r], xp[a]);
+        acc = csub(acc, cmul(ps[p], hx));
+    }
+    yout[e] = acc;
+}
+
+__global__ __launch_bounds__(256) void sup_shift_mom_kernel(cd* mom, const cd* xsup,
+                                                            const int32_t* done, long nsym,
+                                                            int Td, int NT) {
+    const long sym = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (sym >= nsym) return;
+    if (done && done[sym / Td]) return;
+    cd* mo = mom + (size_t)sym * (NT + NT * NT);
+    const cd* xp = xsup + (size_t)sym * NT;
+    for (int i = 0; i < NT; ++i)
+        for (int j = 0; j < NT; ++j) {
+            cd v = mo[NT + i * NT + j];
+            v = cadd(v, cmulc(mo[i], xp[j]));
+            v = cadd(v, cmulc(xp[i], mo[j]));
+            v = cadd(v, cmulc(xp[i], xp[j]));
+            mo[NT + i * NT + j] = v;
+        }
+    for (int i = 0; i < NT; ++i) mo[i] = cadd(mo[i], xp[i]);
+}
+
 // Last-iteration hard decisions (PMd/SER/log_max_SER.py:77-78): for the hard E-step modes
 // m_t IS the decided hypothesis (weight 1), so x_dest[b][t] = m_t of the final E-step.
 __global__ __launch_bounds__(256) void decisions_kernel(const cd* mom, cd* xdest, long n, int NT) {
@@ -306,6 +351,24 @@ hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t
 
 hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* out, hipStream_t s) {
     hipLaunchKernelGGL(nmse_kernel, dim3(pb.B), dim3(256), 0, s, theta, h, out, pb.K);
+    return hipGetLastError();
+}
+
+hipError_t launch_sup_shift_y(const Problem& pb, const cd* yd, const cd* psid, const cd* theta,
+                              const cd* xsup, cd* yout, const int32_t* done, hipStream_t s) {
+    const long n = (long)pb.B * pb.Td * pb.NR;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(sup_shift_y_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, yd,
+                       psid, theta, xsup, yout, done, n, pb.Td, pb.P, pb.NT, pb.NR);
+    return hipGetLastError();
+}
+
+hipError_t launch_sup_shift_mom(const Problem& pb, cd* mom, const cd* xsup, const int32_t* done,
+                                hipStream_t s) {
+    const long n = (long)pb.B * pb.Td;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(sup_shift_mom_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       mom, xsup, done, n, pb.Td, pb.NT);
     return hipGetLastError();
 }
 

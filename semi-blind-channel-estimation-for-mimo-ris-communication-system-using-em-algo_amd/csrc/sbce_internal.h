@@ -132,6 +132,10 @@ hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w
 hipError_t chol_debug_clock(unsigned long long* out);   // diagnostic (SBCE_CHOL_SKIP & 64)
 hipError_t chol_debug_clock_reset();
 hipError_t launch_decisions(const Problem& pb, const cd* mom, cd* xdest, hipStream_t s);
+hipError_t launch_sup_shift_y(const Problem& pb, const cd* yd, const cd* psid, const cd* theta,
+                              const cd* xsup, cd* yout, const int32_t* done, hipStream_t s);
+hipError_t launch_sup_shift_mom(const Problem& pb, cd* mom, const cd* xsup, const int32_t* done,
+                                hipStream_t s);
 hipError_t launch_ser(const Problem& pb, const cd* xdest, const cd* xtrue, double* out,
                       hipStream_t s);
 hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* out,

@@ -58,7 +58,7 @@ _SOLVES = {"chol": _lib.SBCE_SOLVE_CHOL, "drop": _lib.SBCE_SOLVE_CHOL_DROP}
 
 def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_true=None,
              h_true=None, solve="chol", return_device=False, partition_r=0,
-             return_decisions=False):
+             return_decisions=False, x_sup=None):
     """Run ``itera`` EM iterations on a batch of independent trials.
 
     Array layouts (complex128, batch-major, include/sbce.h):
@@ -69,7 +69,8 @@ def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_t
     h_true (B,K) -> the reference's oracle early stop (PM.py:110-112).
     mode: "soft" | "hard" | "pm" | "pm_soft" | "zf" | "mmse"; partition_r selects the PM
     list size.  return_decisions (hard modes): x_dest (B,T_d,n_tx), the last E-step's
-    decisions (SER/log_max_SER.py:77-78).
+    decisions (SER/log_max_SER.py:77-78).  x_sup (B,T_d,n_tx): pilot symbols superimposed
+    on the data (Parallel/ParallelProtocol_Tp.py:63-86), soft/hard modes.
     Inputs may be numpy arrays or CUDA complex128 tensors (used in place).
     Returns dict(theta (B,K), llf (B,itera) or None, status (B,), iters_done (B,)).
     """
@@ -106,13 +107,15 @@ def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_t
     llf = torch.zeros((B, max(itera, 1)), dtype=torch.float64, device="cuda") if Xd is not None else None
     xdest = (torch.zeros((B, T_d, n_tx), dtype=torch.complex128, device="cuda")
              if return_decisions else None)
+    Xs = dev(x_sup)
     ptrs = _lib.Ptrs(Yd.data_ptr(), Yp.data_ptr() if T_p else Yd.data_ptr(), Ps.data_ptr(),
                      Up.data_ptr() if T_p else Yd.data_ptr(), Cs.data_ptr(), th.data_ptr(),
                      Xd.data_ptr() if Xd is not None else None,
                      llf.data_ptr() if llf is not None else None,
                      Ht.data_ptr() if Ht is not None else None, iters_done.data_ptr(),
                      status.data_ptr(), ws.data_ptr(), ws.numel(),
-                     xdest.data_ptr() if xdest is not None else None)
+                     xdest.data_ptr() if xdest is not None else None,
+                     Xs.data_ptr() if Xs is not None else None)
     stream = torch.cuda.current_stream().cuda_stream
     _lib.check(lib.sbce_em(dims, ptrs, int(itera), _MODES[mode], _SOLVES[solve], stream), "sbce_em")
     out = dict(theta=th, llf=llf, status=status, iters_done=iters_done)
@@ -298,6 +301,28 @@ def em_ml_ser(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn
                    mode="hard", solve=solve, return_decisions=True)
     th = _finish(res, verbose, itera)
     return th, [x[None, :] for x in res["x_dest"][0]]
+
+
+def em_superimposed(Y, T, Z, X_d, X_p, T_p, T_d, n_tx, PsiTilde_t, all_possibleSymbols, M, varn,
+                    itera, N, verbose=False, solve="chol"):
+    """Superimposed-pilot EM (Parallel/ParallelProtocol_Tp.py:63-86, same signature):
+    T = max(T_d, T_p) symbols y_t carrying x_d,t + x_p,t (both zero-padded), soft
+    posterior over x_j + x_p,t, no separate pilot block, theta_0 = 0.  Z is accepted for
+    signature parity (the reference only passes it through)."""
+    aps = np.asarray(all_possibleSymbols)
+    n_tx = aps.shape[1]
+    Psi = np.asarray(PsiTilde_t)[:, :T]
+    n_rx = np.asarray(Y[0]).shape[0]
+    Xp = np.zeros((T, n_tx), dtype=complex)
+    xp = np.stack([np.asarray(x).reshape(-1) for x in X_p]) if len(X_p) else Xp[:0]
+    Xp[:min(T, xp.shape[0])] = xp[:T]
+    L = Psi.shape[0] * n_tx
+    y = np.stack([np.asarray(v).reshape(-1) for v in Y[:T]])[None]
+    res = em_batch(y, np.zeros((1, 0, n_rx), dtype=complex), Psi.T[None],
+                   np.zeros((1, 0, L), dtype=complex), cons_from_aps(aps, int(M)), varn, itera,
+                   np.zeros((1, L * n_rx), dtype=complex), mode="soft", solve=solve,
+                   x_sup=Xp[None])
+    return _finish(res, verbose, itera)
 
 
 def ser_batch(x_dest, x_d_true):

@@ -91,6 +91,16 @@ def irs_matrix(T_p, T_d, N, beta_min=0.0, beta_max=2 * np.pi, amp=1.0, pilot="df
     return Ptp, Ptd
 
 
+def dft_phases(rows, T, den):
+    """rows x T matrix exp(-2j pi t n / den), element-wise as the reference loops
+    (Parallel/ParallelProtocol_Tp.py:89-94 uses rows = N+1, den = T)."""
+    Psi = np.zeros((rows, T), dtype=complex)
+    for n in range(rows):
+        for t in range(T):
+            Psi[n, t] = np.exp((-1j * 2 * np.pi * (t) * (n)) / (den))
+    return Psi
+
+
 def insert_direct(Psi):
     """Prepend the direct-path ones row (PMd/Proposed_method_NMSEvsTp.py:161)."""
     return np.insert(Psi, 0, np.ones((1, Psi.shape[1]), dtype="complex128"), axis=0)
@@ -98,7 +108,12 @@ def insert_direct(Psi):
 
 def pilot_regressors(Psi_p, X_p):
     """u_p = psi_p (x) x_p (T_p x L); Z_p[t] = u_p^T (x) I_{n_rx}."""
-    X = np.stack([np.asarray(x).reshape(-1) for x in X_p]) if isinstance(X_p, list) else X_p
+    if isinstance(X_p, list):
+        if not X_p:
+            return np.zeros((0, 0), dtype=complex)
+        X = np.stack([np.asarray(x).reshape(-1) for x in X_p])
+    else:
+        X = X_p
     return np.einsum("pt,ta->tpa", Psi_p, X).reshape(Psi_p.shape[1], -1)
 
 
@@ -123,7 +138,8 @@ def received_signals(T_p, T_d, Psi_tp, Psi_td, n_rx, n_tx, X_d, X_p, h, varn, rs
     symbol (same order as the reference).  U_d uses the TRUE data symbols
     (the reference's Z_d, genie regressors for the LLF)."""
     rs = _rs(rs)
-    U_p = pilot_regressors(Psi_tp[:, :T_p], X_p[:T_p])
+    U_p = (pilot_regressors(Psi_tp[:, :T_p], X_p[:T_p]) if T_p
+           else np.zeros((0, Psi_td.shape[0] * n_tx), dtype=complex))
     U_d = pilot_regressors(Psi_td, X_d)
     n_p = np.stack([rs.normal(loc=0, scale=np.sqrt(varn / 2), size=(n_rx, 2)).view(np.complex128)[:, 0]
                     for _ in range(T_p)]) if T_p else np.zeros((0, n_rx), dtype=complex)

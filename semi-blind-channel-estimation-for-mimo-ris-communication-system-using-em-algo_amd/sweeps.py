@@ -5,6 +5,7 @@ estimator with every trial of a sweep point batched into ONE sbce_em call.
   nmse_vs_td   "Proposed method/Proposed_method_NMSEvsTd.py":121-157
   nmse_vs_snr  "Proposed method/SNR/all_Detectors.py":331-395 (exact and log-max EMs)
   ser_vs_snr   "Proposed method/SER/log_max_SER.py":124-167 (log-max EM decisions)
+  nmse_vs_tp_superimposed  "Parallel/ParallelProtocol_Tp.py":106-136 (superimposed pilots)
 
 Data generation (host, NumPy):
   replay=True   the reference's exact legacy-RandomState call order after
@@ -229,3 +230,60 @@ def ser_vs_snr(SNR=(-5, 0, 5, 10, 15, 20), T_d=50, T_p=20, N=30, n_rx=2, n_tx=2,
     acc.allreduce(dist)
     ser = acc.mean_extra()
     return np.asarray(SNR), ser[:, 0], ser[:, 1], acc.mean_nmse()
+
+
+def gen_superimposed(T_p=(4, 8, 12, 16, 20, 24, 28, 32, 36, 40), T_d=50, N=32, n_rx=8, n_tx=1,
+                     monte_iter=50, M=16, varn=0.1, seed=0, replay=True, varh=1.0, keep=None):
+    """Data of Parallel/ParallelProtocol_Tp.py:114-122 in the reference draw order: per
+    trial channelMatrix (C-order h, :10-16), symbols(T_d); per T_p irsMatrix(T, N)
+    ((N+1) x T DFT, deterministic), pilotSymbols, dataPilotSymbols (zero-padded sum),
+    receivedSignals (one noise draw per symbol)."""
+    keep = set(range(monte_iter)) if keep is None else set(keep)
+    points = [[] for _ in T_p]
+    if replay:
+        np.random.seed(seed)
+    for i in range(monte_iter):
+        rs = None if replay else _trial_rng(seed, i)
+        if not replay and i not in keep:
+            continue
+        h = sm.channel_matrix(n_tx, n_rx, N, varh, order="C", rs=rs)
+        X_d, _ = sm.symbols(n_tx, M, T_d, rs=rs)
+        for k, tp in enumerate(T_p):
+            T = max(T_d, tp)
+            Psi = sm.dft_phases(N + 1, T, T)
+            X_p = sm.pilot_symbols(n_tx, M, tp, rs=rs)
+            xd = np.zeros((T, n_tx), dtype=complex)
+            xp = np.zeros((T, n_tx), dtype=complex)
+            xd[:T_d] = np.stack([x.reshape(-1) for x in X_d])
+            xp[:tp] = np.stack([x.reshape(-1) for x in X_p])
+            X = xd + xp
+            _, Y, _, _, _ = sm.received_signals(0, T, Psi[:, :0], Psi, n_rx, n_tx, list(X), [], h,
+                                                varn, rs=rs, with_initial=False)
+            if i in keep:
+                points[k].append(dict(Y=Y, Psi=Psi, X_sup=xp, h=h))
+    return points
+
+
+def nmse_vs_tp_superimposed(T_p=(4, 8, 12, 16, 20, 24, 28, 32, 36, 40), T_d=50, N=32, n_rx=8,
+                            n_tx=1, itera=20, monte_iter=50, M=16, varn=0.1, seed=0, replay=True,
+                            varh=1.0):
+    """Mean NMSE per pilot length of the superimposed-pilot protocol
+    (Parallel/ParallelProtocol_Tp.py:106-136; NMSE :129)."""
+    dist, world, rank = _dist()
+    mine = shard(monte_iter, world, rank).tolist()
+    points = gen_superimposed(T_p, T_d, N, n_rx, n_tx, monte_iter, M, varn, seed, replay, varh,
+                              keep=mine)
+    acc = Accumulators(len(T_p))
+    cons = qam_constellation(M)
+    for k, trials in enumerate(points):
+        if not trials:
+            continue
+        L = (N + 1) * n_tx
+        B = len(trials)
+        r = em_batch(np.stack([t["Y"] for t in trials]), np.zeros((B, 0, n_rx), dtype=complex),
+                     np.stack([t["Psi"].T for t in trials]), np.zeros((B, 0, L), dtype=complex),
+                     cons, varn, itera, np.zeros((B, L * n_rx), dtype=complex), mode="soft",
+                     x_sup=np.stack([t["X_sup"] for t in trials]))
+        acc.add(k, _nmse(r["theta"], np.stack([t["h"] for t in trials])))
+    acc.allreduce(dist)
+    return np.asarray(T_p), acc.mean_nmse()

@@ -303,6 +303,30 @@ def case_ser():
     return "ser_logmax", out
 
 
+def case_superimposed():
+    """Parallel/ParallelProtocol_Tp.py: superimposed data + pilot (dataPilotSymbols :41-53),
+    soft EM with hypotheses x_j + x_p,t and no separate pilot block (em :63-86), zero
+    initialisation, driver draw order :114-122; T_p shorter and longer than T_d."""
+    N, n_tx, n_rx, T_d, M, varn, itera, T_ps = 4, 1, 4, 20, 16, 0.1, 3, (8, 30)
+    ns = load_defs(os.path.join(REF, "Parallel", "ParallelProtocol_Tp.py"))
+    np.random.seed(17)
+    h = quiet(ns["channelMatrix"], n_tx, n_rx, N, 1.0)
+    X_d, aps = ns["symbols"](n_tx, M, T_d)
+    out = dict(N=N, n_tx=n_tx, n_rx=n_rx, T_d=T_d, M=M, varn=varn, itera=itera,
+               T_ps=np.asarray(T_ps), h=np.asarray(h).reshape(-1), aps=aps,
+               X_d=np.stack(X_d)[..., 0])
+    for k, T_p in enumerate(T_ps):
+        T = max(T_d, T_p)
+        Psi = ns["irsMatrix"](T, N)
+        X_p = ns["pilotSymbols"](n_tx, M, T_p)
+        X = ns["dataPilotSymbols"](n_tx, X_p, X_d)
+        Y, Z = ns["receivedSignals"](T, Psi, n_rx, n_tx, X, h, varn)
+        th = quiet(ns["em"], Y, T, Z, X_d, X_p, T_p, T_d, n_tx, Psi, aps, M, varn, itera, N)
+        out.update({f"Psi{k}": Psi, f"X_p{k}": np.stack(X_p)[..., 0], f"X{k}": X,
+                    f"Y{k}": np.stack(Y)[..., 0], f"theta{k}": np.asarray(th).reshape(-1)})
+    return "superimposed", out
+
+
 def case_qam():
     """Constellation tables of the vendored komm QAM (PMd/QAM.py:320-322)."""
     return "qam", {f"cons{M}": _cons(M) for M in (4, 16, 64, 256)}
@@ -313,6 +337,7 @@ CASES = {
     "pm_nt4": (case_pm, ("pm_nt4", 3, 4, 4, 24, 8, 4, 0.1, 3, 12, 0, 2)),
     "pm_nt3_m16": (case_pm, ("pm_nt3_m16", 4, 3, 3, 24, 10, 16, 0.3, 3, 13, 1, 1)),
     "ser_logmax": (case_ser, ()),
+    "superimposed": (case_superimposed, ()),
     "det_nt3": (case_det, ("det_nt3", 4, 3, 4, 30, 10, 4, 0.2, 3, 21)),
     "det_nt2_m16": (case_det, ("det_nt2_m16", 5, 2, 3, 30, 12, 16, 0.3, 3, 22)),
     "kat1_s7": (case_kat1, (7,)),

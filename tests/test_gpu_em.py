@@ -236,6 +236,9 @@ def test_snr_sweep_entry_point_reproduces_reference_curve(sbce):
     ("Proposed_method_NMSEvsTp.py", ["--monte-iter", "2", "--T-p", "8", "40", "--N", "8"], 2),
     ("Proposed_method_NMSEvsTd.py", ["--monte-iter", "2", "--T-d", "20", "40", "--N", "8"], 2),
     ("nmse_vs_snr.py", ["--monte-iter", "2", "--SNR", "0", "20"], 2),
+    ("log_max_SER.py", ["--monte-iter", "2", "--SNR", "0", "20", "--N", "8"], 2),
+    ("ParallelProtocol_Tp.py", ["--monte-iter", "2", "--T-p", "8", "60", "--N", "8",
+                                "--itera", "3"], 2),
 ])
 def test_sweep_scripts_run(sbce, script, args, rows, tmp_path):
     import os
@@ -471,3 +474,28 @@ def test_ser_sweep_entry_point(sbce):
                                                   10.0, 5)
     assert list(s_ref) == [float(d["ser0"]), float(d["ser1"])]
     assert np.all(s_el <= s_ref) and np.all(np.isfinite(nm))
+
+
+# ---------------------------------------------------------------- superimposed pilots
+def test_em_superimposed_matches_reference(sbce):
+    d = golden("superimposed")
+    for k in range(2):
+        T = d[f"Y{k}"].shape[0]
+        Y = [y[:, None] for y in d[f"Y{k}"]]
+        X_d = [x[:, None] for x in d["X_d"]]
+        X_p = [x[:, None] for x in d[f"X_p{k}"]]
+        th = sbce.em_superimposed(Y, T, None, X_d, X_p, len(X_p), int(d["T_d"]), int(d["n_tx"]),
+                                  d[f"Psi{k}"], d["aps"], int(d["M"]), float(d["varn"]),
+                                  int(d["itera"]), int(d["N"]))
+        assert rel(th, d[f"theta{k}"]) < THETA_TOL
+
+
+def test_superimposed_sweep_entry_point(sbce):
+    d = golden("superimposed")
+    tps, nm = sbce.sweeps.nmse_vs_tp_superimposed(tuple(int(x) for x in d["T_ps"]), int(d["T_d"]),
+                                                  int(d["N"]), int(d["n_rx"]), int(d["n_tx"]),
+                                                  int(d["itera"]), 1, int(d["M"]),
+                                                  float(d["varn"]), 17)
+    h = d["h"]
+    ref = [np.sum(np.abs(d[f"theta{k}"] - h) ** 2) / np.sum(np.abs(h) ** 2) for k in range(2)]
+    assert np.allclose(nm, ref, rtol=1e-9, atol=0)

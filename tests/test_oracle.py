@@ -315,3 +315,33 @@ def test_ser_sweep_replays_reference_data(sbce):
         assert rel(t["h0"], d[f"h0{k}"]) < 1e-12
         assert np.array_equal(t["X_d"], d["X_d"])
         assert abs(varns[k] - float(d[f"varn{k}"])) < 1e-15
+
+
+def _sup_padded(d, k):
+    T = d[f"Y{k}"].shape[0]
+    Xs = np.zeros((T, int(d["n_tx"])), dtype=complex)
+    Xp = d[f"X_p{k}"][:T]
+    Xs[:Xp.shape[0]] = Xp
+    return Xs
+
+
+def test_superimposed_oracle_matches_reference():
+    """Parallel/ParallelProtocol_Tp.py em: hypotheses x_j + x_p,t, T_p < T_d and T_p > T_d."""
+    from oracle.superimposed import em_superimposed
+    d = golden("superimposed")
+    for k in range(2):
+        th = em_superimposed(d[f"Y{k}"], d[f"Psi{k}"], d["aps"], float(d["varn"]),
+                             int(d["itera"]), _sup_padded(d, k))
+        assert rel(th, d[f"theta{k}"]) < 1e-12
+
+
+def test_superimposed_sweep_replays_reference_data(sbce):
+    d = golden("superimposed")
+    pts = sbce.sweeps.gen_superimposed(tuple(int(x) for x in d["T_ps"]), int(d["T_d"]), int(d["N"]),
+                                       int(d["n_rx"]), int(d["n_tx"]), 1, int(d["M"]),
+                                       float(d["varn"]), 17)
+    for k in range(2):
+        t = pts[k][0]
+        assert np.array_equal(t["h"], d["h"]) and np.array_equal(t["Psi"], d[f"Psi{k}"])
+        assert np.array_equal(t["X_sup"], _sup_padded(d, k))
+        assert rel(t["Y"], d[f"Y{k}"]) < 1e-13
