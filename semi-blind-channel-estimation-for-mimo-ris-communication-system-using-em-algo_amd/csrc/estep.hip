@@ -412,7 +412,13 @@ struct MfmaConst {
     double inv_s2, thr_d;
 };
 
-template <int NT, int NR, int MODE, int TU>
+// V16 (M == 16, NA == 2): the A operand's V term, V[kk][i & 15] = V[kk][lane & 15], is the
+// same for every tile, so it is hoisted into registers (one LDS read + add per MFMA
+// instead of two reads + add).  gamma_k is not added to the 16 accumulators: the skip
+// tests use min(acc) + gamma and the rare exp path adds it back.  (PMC at cfg1 showed
+// the f64 VALU work between the MFMAs, which does not co-execute with them, as the
+// limiter: 40 % MFMA busy.)
+template <int NT, int NR, int MODE, int TU, bool V16 = false>
 __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst c) {
     constexpr int NA = NT / 2;
     constexpr int NB = NT - NA;
@@ -514,6 +520,9 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
     }
     const int col = lane & 15;
     const int rq = lane >> 4;
+    double vreg[STEPS];
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) vreg[s] = V16 ? s_V[(4 * s + rq) * 16 + col] : 0.0;
     const int nktile = c.JB >> 4;
     const int ntile_chunk = c.chunk >> 4;
     bool table_ready = false;
@@ -572,29 +581,40 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
             }
             for (int tg = 0; tg < ntile_chunk; tg += TU) {
                 // TU independent 16x16 tiles in flight: STEPS*TU MFMAs per group
+                // accumulators start at alpha_i; gamma_k (lane constant) is added to the
+                // tile minima only
                 d4v acc[TU];
 #pragma unroll
                 for (int u = 0; u < TU; ++u)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[u][j] = s_al[(tg + u) * 16 + rq + 4 * j] + gam;
+                    for (int j = 0; j < 4; ++j) acc[u][j] = s_al[(tg + u) * 16 + rq + 4 * j];
 #pragma unroll
                 for (int s = 0; s < STEPS; ++s)
 #pragma unroll
                     for (int u = 0; u < TU; ++u) {
-                        const int ia = i0 + (tg + u) * 16 + col;          // A-operand row
                         const int kk = 4 * s + rq;
-                        double av = s_U[kk * c.M + ((NA == 2) ? (ia >> c.lm) : ia)];
-                        if (NA == 2) av += s_V[kk * c.M + (ia & mask)];
+                        double av;
+                        if (V16) {
+                            av = s_U[kk * 16 + (i0 >> 4) + tg + u] + vreg[s];
+                        } else {
+                            const int ia = i0 + (tg + u) * 16 + col;      // A-operand row
+                            av = s_U[kk * c.M + ((NA == 2) ? (ia >> c.lm) : ia)];
+                            if (NA == 2) av += s_V[kk * c.M + (ia & mask)];
+                        }
                         acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bop[s], acc[u], 0, 0, 0);
                     }
                 if (MODE == SBCE_ESTEP_HARD) {
+                    const double lim = best_d - gam;       // acc + gam < best_d  <=>  acc < lim
 #pragma unroll
                     for (int u = 0; u < TU; ++u)
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
-                            const int jj = (i0 + (tg + u) * 16 + rq + 4 * j) * c.JB + k;
                             const double dv = acc[u][j];
-                            if (dv < best_d || (dv == best_d && jj < best_j)) { best_d = dv; best_j = jj; }
+                            if (dv <= lim) {
+                                const int jj = (i0 + (tg + u) * 16 + rq + 4 * j) * c.JB + k;
+                                const double dd = dv + gam;
+                                if (dd < best_d || (dd == best_d && jj < best_j)) { best_d = dd; best_j = jj; }
+                            }
                         }
                     continue;
                 }
@@ -602,6 +622,7 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
 #pragma unroll
                 for (int u = 1; u < TU; ++u)
                     cm = fmin(cm, fmin(fmin(acc[u][0], acc[u][1]), fmin(acc[u][2], acc[u][3])));
+                cm += gam;
                 if (__any(cm < mshift)) {
                     double mn = fmin(cm, mshift);
                     for (int off = 32; off >= 1; off >>= 1) mn = fmin(mn, shfl_xor_d(mn, off));
@@ -620,12 +641,13 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
                 if (!__any(cm <= mshift + c.thr_d)) continue;
 #pragma unroll
                 for (int u = 0; u < TU; ++u) {
-                    const double cmu = fmin(fmin(acc[u][0], acc[u][1]), fmin(acc[u][2], acc[u][3]));
+                    const double cmu =
+                        fmin(fmin(acc[u][0], acc[u][1]), fmin(acc[u][2], acc[u][3])) + gam;
                     if (!__any(cmu <= mshift + c.thr_d)) continue;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int i = i0 + (tg + u) * 16 + rq + 4 * j;
-                        const double w = fexp_neg((mshift - acc[u][j]) * inv_s2);
+                        const double w = fexp_neg((mshift - (acc[u][j] + gam)) * inv_s2);
                         cd xa[NA];
 #pragma unroll
                         for (int q = 0; q < NA; ++q) xa[q] = s_cons[(i >> (c.lm * (NA - 1 - q))) & mask];
@@ -748,6 +770,15 @@ template <int NT, int NR>
 hipError_t dispatch_mfma_mode(const MfmaConst& c, size_t lds, long blocks, const EstepArgs& a,
                               int mode, hipStream_t s) {
     const bool tu4 = (c.chunk / 16) % 4 == 0;
+    if (NT == 4 && c.M == 16 && tu4) {            // cfg1 geometry: hoisted V operand
+        if (mode == SBCE_ESTEP_HARD)
+            hipLaunchKernelGGL((estep_mfma_kernel<NT, NR, SBCE_ESTEP_HARD, 4, true>),
+                               dim3((unsigned)blocks), dim3(64 * kMfmaWaves), lds, s, a, c);
+        else
+            hipLaunchKernelGGL((estep_mfma_kernel<NT, NR, SBCE_ESTEP_SOFT, 4, true>),
+                               dim3((unsigned)blocks), dim3(64 * kMfmaWaves), lds, s, a, c);
+        return hipGetLastError();
+    }
     if (mode == SBCE_ESTEP_HARD) {
         if (tu4)
             hipLaunchKernelGGL((estep_mfma_kernel<NT, NR, SBCE_ESTEP_HARD, 4>), dim3((unsigned)blocks),
