@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define SBCE_ABI_VERSION 2
+#define SBCE_ABI_VERSION 3
 
 /* return codes */
 #define SBCE_OK 0
@@ -75,6 +75,13 @@ extern "C" {
 #define SBCE_ESTEP_ZF 4         /* zero-forcing hard decision (n_rx >= n_tx):
                                    all_detectorsvsTd.py:98-133 */
 #define SBCE_ESTEP_MMSE 5       /* MMSE hard decision: all_detectorsvsTd.py:54-96 */
+#define SBCE_ESTEP_GAUSS 6      /* Gaussian-prior EM (x ~ CN(0, varx^2 I), no constellation):
+                                   MIMO_Gaussian_proposed.py:56-89.  m_t = LMMSE mean, S_t = the
+                                   posterior covariance WITHOUT m m^H (the reference adds the
+                                   scalar ||mu_t||^2 to every entry instead, :73-75; for n_rx = 1
+                                   that term is kept as R += c 1 1^T, for n_rx >= 2 it cancels
+                                   in the pseudo-inverse, see sbce_gauss_expand).  P = N rows of
+                                   psi (no direct path); dims.varx used; cons ignored */
 
 /* M-step solve modes (SURVEY.md §7 hard part 3) */
 #define SBCE_SOLVE_CHOL 0       /* Hermitian Cholesky of the reduced L x L system
@@ -102,6 +109,8 @@ typedef struct sbce_dims {
     int32_t partition_r;/* PM modes: list = M^(p+1) with p = int(partition_r /
                            log2 M) (PM.py:74), at most 64 members; else 0 */
     double varn;        /* noise variance parameter; posterior uses varn^2 */
+    double varx;        /* SBCE_ESTEP_GAUSS only: symbol variance parameter, the prior
+                           covariance uses varx^2 (MIMO_Gaussian_proposed.py:44); else ignored */
 } sbce_dims;
 
 typedef struct sbce_ptrs {
@@ -161,6 +170,16 @@ int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments,
  * (T_d,n_tx,1) - (T_d,1,n_tx) broadcast, / (T_d n_tx)); ser_out[2b+1] = element-wise SER. */
 int sbce_ser(const sbce_dims* d, const void* x_dest, const void* x_d_true, double* ser_out,
              void* hip_stream);
+
+/* Gaussian-prior EM output in the reference's format: the n_rx x (N n_tx n_rx^2) matrix
+ * H_l = B pinv(A) of MIMO_Gaussian_proposed.py:77-85, from the reduced estimate theta
+ * ([B][K], K = N n_tx n_rx, the M-step of sbce_em with SBCE_ESTEP_GAUSS).  With
+ * e = vec(I_{n_rx}), f = 1 - e, Lr = N n_tx and theta_r = row r of the reduced channel,
+ *   n_rx >= 2:  H_l[r] = kron(theta_r, e^T) / n_rx - (theta_r . 1) / (Lr (n_rx^2 - n_rx)) kron(1, f^T)
+ *   n_rx == 1:  H_l = theta^T
+ * (the all-ones term c J the reference adds to A has range outside span kron(., e) for
+ * n_rx >= 2, where c drops out of pinv(A)).  h_out: [B][n_rx][N n_tx n_rx^2] complex. */
+int sbce_gauss_expand(const sbce_dims* d, const void* theta, void* h_out, void* hip_stream);
 
 /* Per-trial NMSE ||theta - h||^2 / ||h||^2 (Proposed_method_NMSEvsTp.py:172). */
 int sbce_nmse(const sbce_dims* d, const void* theta, const void* h_true,

@@ -11,10 +11,11 @@ from ._lib import SbceUnavailable, SbceError  # noqa: F401
 from .em import (  # noqa: F401
     em, em_ml, em_llf, em_ml_llf, em_ml_ser, em_pm, em_pm_soft, em_zf, em_mmse, em_superimposed,
     em_zero_init, em_batch, ser_batch, estep_batch,
-    mstep_batch, nmse_batch, EMEngine,
+    mstep_batch, nmse_batch, EMEngine, EM_Gaussian_proposed, gauss_expand_batch,
+    gaussian_regressors, reduce_gaussian_channel,
 )
 
 __all__ = ["em", "em_ml", "em_llf", "em_ml_llf", "em_ml_ser", "em_pm", "em_pm_soft", "em_zf",
-           "em_mmse", "em_superimposed", "ser_batch",
+           "em_mmse", "em_superimposed", "ser_batch", "EM_Gaussian_proposed", "gauss_expand_batch",
            "em_zero_init", "em_batch",
            "SbceUnavailable", "SbceError", "qam", "signal_model"]

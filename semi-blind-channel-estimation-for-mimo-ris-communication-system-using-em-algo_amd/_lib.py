@@ -10,13 +10,14 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsbce.so")
 
-SBCE_ABI_VERSION = 2
+SBCE_ABI_VERSION = 3
 SBCE_ESTEP_SOFT = 0
 SBCE_ESTEP_HARD = 1
 SBCE_ESTEP_PM = 2
 SBCE_ESTEP_PM_SOFT = 3
 SBCE_ESTEP_ZF = 4
 SBCE_ESTEP_MMSE = 5
+SBCE_ESTEP_GAUSS = 6
 SBCE_SOLVE_CHOL = 0
 SBCE_SOLVE_CHOL_DROP = 1
 SBCE_STATUS_NONHPD = 1
@@ -24,7 +25,7 @@ SBCE_STATUS_PILOT = 2
 SBCE_STATUS_DETECTOR = 4
 
 EXPORTED = ("sbce_abi_version", "sbce_strerror", "sbce_workspace_bytes", "sbce_em",
-            "sbce_estep", "sbce_mstep", "sbce_ser", "sbce_nmse")
+            "sbce_estep", "sbce_mstep", "sbce_ser", "sbce_gauss_expand", "sbce_nmse")
 
 
 class SbceUnavailable(RuntimeError):
@@ -38,7 +39,8 @@ class SbceError(RuntimeError):
 class Dims(ctypes.Structure):
     _fields_ = [("batch", ctypes.c_int32), ("n_tx", ctypes.c_int32), ("n_rx", ctypes.c_int32),
                 ("n_psi", ctypes.c_int32), ("t_p", ctypes.c_int32), ("t_d", ctypes.c_int32),
-                ("m", ctypes.c_int32), ("partition_r", ctypes.c_int32), ("varn", ctypes.c_double)]
+                ("m", ctypes.c_int32), ("partition_r", ctypes.c_int32), ("varn", ctypes.c_double),
+                ("varx", ctypes.c_double)]
 
 
 class Ptrs(ctypes.Structure):
@@ -81,6 +83,9 @@ def load(path=None):
     lib.sbce_ser.restype = ctypes.c_int
     lib.sbce_ser.argtypes = [ctypes.POINTER(Dims), ctypes.c_void_p, ctypes.c_void_p,
                              ctypes.c_void_p, ctypes.c_void_p]
+    lib.sbce_gauss_expand.restype = ctypes.c_int
+    lib.sbce_gauss_expand.argtypes = [ctypes.POINTER(Dims), ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p]
     lib.sbce_nmse.restype = ctypes.c_int
     lib.sbce_nmse.argtypes = [ctypes.POINTER(Dims), ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.c_void_p, ctypes.c_void_p]

@@ -27,6 +27,7 @@ bool make_problem(const sbce_dims* d, Problem& pb) {
     if (d->n_tx > 8 || d->n_rx > 8) return false;
     pb.B = d->batch; pb.NT = d->n_tx; pb.NR = d->n_rx; pb.P = d->n_psi;
     pb.Tp = d->t_p; pb.Td = d->t_d; pb.M = d->m; pb.varn = d->varn; pb.pr = d->partition_r;
+    pb.varx = d->varx;
     pb.L = pb.P * pb.NT;
     pb.K = pb.L * pb.NR;
     return true;
@@ -109,6 +110,8 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     if (!estep_supported(pb, estep_mode) || !chol_supported(pb)) return SBCE_EUNSUPPORTED;
     if (solve_mode != SBCE_SOLVE_CHOL && solve_mode != SBCE_SOLVE_CHOL_DROP) return SBCE_EINVAL;
     if (p->llf && !p->x_d_true) return SBCE_EINVAL;
+    const bool gauss = estep_mode == SBCE_ESTEP_GAUSS;
+    if (gauss && !(pb.varx > 0.0)) return SBCE_EINVAL;
     const bool hard = estep_mode == SBCE_ESTEP_HARD || estep_mode == SBCE_ESTEP_ZF ||
                       estep_mode == SBCE_ESTEP_MMSE;
     if (p->x_dest && (!hard || !aligned16(p->x_dest))) return SBCE_EINVAL;
@@ -149,6 +152,9 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
             return rc;
         }
         if ((rc = hip_rc(launch_mstep_build(pb, ma, s)))) return rc;
+        // Gaussian prior, n_rx = 1: the reference's all-ones covariance term stays in A
+        // (MIMO_Gaussian_proposed.py:73-76): R += c 1 1^T
+        if (gauss && pb.NR == 1 && (rc = hip_rc(launch_gauss_rank1(pb, ma, s)))) return rc;
         if ((rc = hip_rc(launch_chol_solve(pb, ma, s)))) return rc;
         if (p->llf &&
             (rc = hip_rc(launch_llf(pb, ma.theta, ma.yp, ma.up, ma.yd, ma.psid,
@@ -176,6 +182,7 @@ int sbce_estep(const sbce_dims* d, const sbce_ptrs* p, int estep_mode, void* mom
     int rc = check_ptrs(p, pb, false);
     if (rc) return rc;
     if (!moments || !aligned16(moments)) return SBCE_EINVAL;
+    if (estep_mode == SBCE_ESTEP_GAUSS && !(pb.varx > 0.0)) return SBCE_EINVAL;
     if (!estep_supported(pb, estep_mode)) return SBCE_EUNSUPPORTED;
     if (pb.B == 0) return SBCE_OK;
     EstepArgs ea;
@@ -231,6 +238,14 @@ int sbce_ser(const sbce_dims* d, const void* x_dest, const void* x_d_true, doubl
     if (pb.B == 0) return SBCE_OK;
     return hip_rc(launch_ser(pb, (const cd*)x_dest, (const cd*)x_d_true, ser_out,
                              (hipStream_t)hip_stream));
+}
+
+int sbce_gauss_expand(const sbce_dims* d, const void* theta, void* h_out, void* hip_stream) {
+    Problem pb;
+    if (!make_problem(d, pb) || !theta || !h_out || !aligned16(theta) || !aligned16(h_out))
+        return SBCE_EINVAL;
+    if (pb.B == 0) return SBCE_OK;
+    return hip_rc(launch_gauss_expand(pb, (const cd*)theta, (cd*)h_out, (hipStream_t)hip_stream));
 }
 
 int sbce_nmse(const sbce_dims* d, const void* theta, const void* h_true, double* nmse_out,

@@ -889,13 +889,13 @@ hipError_t dispatch_nr(int NR, const Geometry& g, const EstepArgs& a, int mode, 
 }  // namespace
 
 bool estep_supported(const Problem& pb, int mode) {
-    if (mode >= SBCE_ESTEP_PM && mode <= SBCE_ESTEP_MMSE) return estep_pm_supported(pb, pb.pr, mode);
+    if (mode >= SBCE_ESTEP_PM && mode <= SBCE_ESTEP_GAUSS) return estep_pm_supported(pb, pb.pr, mode);
     Geometry g;
     return (mode == SBCE_ESTEP_SOFT || mode == SBCE_ESTEP_HARD) && make_geometry(pb, g);
 }
 
 hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStream_t s) {
-    if (mode >= SBCE_ESTEP_PM && mode <= SBCE_ESTEP_MMSE) return launch_estep_pm(pb, a, mode, pb.pr, s);
+    if (mode >= SBCE_ESTEP_PM && mode <= SBCE_ESTEP_GAUSS) return launch_estep_pm(pb, a, mode, pb.pr, s);
     const char* impl = getenv("SBCE_ESTEP_IMPL");   // "valu" forces the VALU kernel (A/B runs)
     const bool force_valu = impl && impl[0] == 'v';
     MfmaConst mc;

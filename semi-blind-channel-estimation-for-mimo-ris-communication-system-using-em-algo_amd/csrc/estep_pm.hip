@@ -1,4 +1,6 @@
-// List / linear-detector E-steps.  MODE 4/5: ZF / MMSE hard decisions of
+// List / linear-detector / Gaussian-prior E-steps.  MODE 6: the Gaussian-prior E-step of
+// "Proposed method/MIMO_Gaussian_proposed.py":69-76 in reduced form (see the MODE == 6
+// branch).  MODE 4/5: ZF / MMSE hard decisions of
 // "Proposed method/all_detectorsvsTd.py":98-133 / :54-96 (see the MODE >= 4 branch).
 // PM (partitioned-detector) E-step: "Proposed method/PM.py":57-104 (uniform list
 // weights) and "Proposed method/PM_beta.py":55-95 (posterior list weights), the
@@ -31,6 +33,7 @@ constexpr int kAugW = 16;          // augmented-matrix row stride ([G | I], G in
 struct PmConst {
     int B, Td, P, M, lm, NT, NR, NA, JA;
     double inv_s2, s2;
+    double vx;                     // Gaussian prior: varx^2 (MIMO_Gaussian_proposed.py:44)
 };
 
 struct PmLds {                      // per-wave LDS carve (complex doubles unless noted)
@@ -123,6 +126,52 @@ __global__ __launch_bounds__(64 * kPmWaves) void estep_pm_kernel(EstepArgs a, Pm
     if (lane < NR) yv[lane] = a.yd[(size_t)gsym * NR + lane];
     if (lane < NT) cols[lane] = lane;
     wave_sync();
+
+    if (MODE == 6) {
+        // ---- Gaussian prior x ~ CN(0, vx I), vx = varx^2 (MIMO_Gaussian_proposed.py:69-76) ----
+        // With z_t = (psi_t (x) x_t) (x) vec(I) the posterior of z_t reduces to that of x_t on
+        // H_eff = H_true (all P = N rows of psi, no off-by-one):
+        //   M = varn^2 I + vx H H^H (n_rx x n_rx, :71),  W = H^H M^-1,
+        //   m = vx W y (:72),  C = vx I - vx^2 W H (:74-75, without the m m^H part: the
+        //   reference's mean_prod is the SCALAR ||mu||^2, handled in the M-step).
+        {
+            const int u = lane >> 3, v = lane & 7;
+            if (u < NR && v < NR) {
+                cd acc = czero();
+                for (int q = 0; q < NT; ++q) acc = cfmac(acc, Ht[q * NR + u], Ht[q * NR + v]);
+                acc = cscale(acc, c.vx);
+                if (u == v) acc.x += c.s2;
+                aug[u * kAugW + v] = acc;
+                aug[u * kAugW + 8 + v] = (u == v) ? cmk(1.0, 0.0) : czero();
+            }
+        }
+        wave_sync();
+        gj_inverse(aug, NR, lane);
+        {
+            const int aa = lane / NR, r = lane - aa * NR;    // W[aa][r], lanes < NT*NR <= 64
+            if (aa < NT) {
+                cd acc = czero();
+                for (int u = 0; u < NR; ++u) acc = cfma(acc, cconj(Ht[aa * NR + u]), aug[u * kAugW + 8 + r]);
+                GB[aa * NR + r] = acc;
+            }
+        }
+        wave_sync();
+        cd* out = a.mom + (size_t)gsym * (NT + NT * NT);
+        const int ai = lane >> 3, bi = lane & 7;
+        if (ai < NT && bi < NT) {
+            cd acc = czero();
+            for (int r = 0; r < NR; ++r) acc = cfma(acc, GB[ai * NR + r], Ht[bi * NR + r]);
+            acc = cscale(acc, -c.vx * c.vx);
+            if (ai == bi) acc.x += c.vx;
+            out[NT + ai * NT + bi] = acc;
+        }
+        if (lane < NT) {
+            cd acc = czero();
+            for (int r = 0; r < NR; ++r) acc = cfma(acc, GB[lane * NR + r], yv[r]);
+            out[lane] = cscale(acc, c.vx);
+        }
+        return;
+    }
 
     if (MODE >= 4) {
         // ---- ZF / MMSE hard decision (all_detectorsvsTd.py:70-72, :111-113) ----
@@ -295,7 +344,7 @@ bool estep_pm_supported(const Problem& pb, int partition_r, int mode) {
     if (pb.NT < 1 || pb.NT > 8 || pb.NR < 1 || pb.NR > 8) return false;
     if (pb.M < 2 || pb.M > 64 || (pb.M & (pb.M - 1))) return false;
     if (mode == SBCE_ESTEP_ZF) return pb.NR >= pb.NT;     // pinv = (H^H H)^{-1} H^H
-    if (mode == SBCE_ESTEP_MMSE) return true;
+    if (mode == SBCE_ESTEP_MMSE || mode == SBCE_ESTEP_GAUSS) return true;
     if (partition_r < 0) return false;
     const int p = (int)((double)partition_r / log2((double)pb.M));
     const int NA = p + 1;
@@ -313,11 +362,12 @@ hipError_t launch_estep_pm(const Problem& pb, const EstepArgs& a, int mode, int 
     int lm = 0;
     while ((1 << lm) < pb.M) ++lm;
     c.lm = lm;
-    const bool det = mode == SBCE_ESTEP_ZF || mode == SBCE_ESTEP_MMSE;
+    const bool det = mode == SBCE_ESTEP_ZF || mode == SBCE_ESTEP_MMSE || mode == SBCE_ESTEP_GAUSS;
     c.NA = det ? 1 : (int)((double)partition_r / log2((double)pb.M)) + 1;
     c.JA = 1 << (lm * c.NA);
     c.inv_s2 = 1.0 / (pb.varn * pb.varn);
     c.s2 = pb.varn * pb.varn;
+    c.vx = pb.varx * pb.varx;
     const size_t lds = (64 + (size_t)kPmWaves * PmLds::TOTAL) * sizeof(cd);
     const long nsym = (long)pb.B * pb.Td;
     const long blocks = (nsym + kPmWaves - 1) / kPmWaves;
@@ -328,6 +378,7 @@ hipError_t launch_estep_pm(const Problem& pb, const EstepArgs& a, int mode, int 
         case SBCE_ESTEP_PM_SOFT: hipLaunchKernelGGL(estep_pm_kernel<3>, g, blk, lds, s, a, c); break;
         case SBCE_ESTEP_ZF: hipLaunchKernelGGL(estep_pm_kernel<4>, g, blk, lds, s, a, c); break;
         case SBCE_ESTEP_MMSE: hipLaunchKernelGGL(estep_pm_kernel<5>, g, blk, lds, s, a, c); break;
+        case SBCE_ESTEP_GAUSS: hipLaunchKernelGGL(estep_pm_kernel<6>, g, blk, lds, s, a, c); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -171,6 +171,56 @@ __global__ __launch_bounds__(256) void nmse_kernel(const cd* theta, const cd* h,
     if (threadIdx.x == 0) out[b] = num / den;
 }
 
+// Gaussian prior, n_rx = 1 ("Proposed method/MIMO_Gaussian_proposed.py":73-76): the
+// reference's covar adds the scalar ||mu_t||^2 = ||psi_t||^2 ||m_t||^2 to every entry of A,
+// i.e. R += c 1 1^T with c = sum_t ||psi_t||^2 ||m_t||^2 (one block per trial).
+__global__ __launch_bounds__(256) void gauss_rank1_kernel(MstepArgs a, int Td, int P, int NT,
+                                                          int L) {
+    __shared__ double sh[4];
+    const int b = blockIdx.x;
+    if (a.done && a.done[b]) return;
+    const int MS = NT + NT * NT;
+    double c = 0.0;
+    for (int t = threadIdx.x; t < Td; t += blockDim.x) {
+        const cd* ps = a.psid + ((size_t)b * Td + t) * P;
+        const cd* m = a.mom + ((size_t)b * Td + t) * MS;
+        double np2 = 0.0, nm2 = 0.0;
+        for (int p = 0; p < P; ++p) np2 += cabs2(ps[p]);
+        for (int q = 0; q < NT; ++q) nm2 += cabs2(m[q]);
+        c = fma(np2, nm2, c);
+    }
+    c = block_sum(c, sh);
+    cd* R = a.R + (size_t)b * L * L;
+    for (int e = threadIdx.x; e < L * L; e += blockDim.x) R[e].x += c;
+}
+
+// H_l of "Proposed method/MIMO_Gaussian_proposed.py":77-85 from the reduced estimate
+// (include/sbce.h, sbce_gauss_expand): block (r, b) writes row r of trial b.
+__global__ __launch_bounds__(256) void gauss_expand_kernel(const cd* theta, cd* out, int Lr,
+                                                           int NR) {
+    __shared__ double sh[4];
+    const int r = blockIdx.x, b = blockIdx.y;
+    const cd* th = theta + (size_t)b * Lr * NR;
+    const long Q = (long)Lr * NR * NR;
+    cd* o = out + ((size_t)b * NR + r) * Q;
+    if (NR == 1) {
+        for (int c = threadIdx.x; c < Lr; c += blockDim.x) o[c] = th[c];
+        return;
+    }
+    double sx = 0.0, sy = 0.0;
+    for (int c = threadIdx.x; c < Lr; c += blockDim.x) { sx += th[c * NR + r].x; sy += th[c * NR + r].y; }
+    sx = block_sum(sx, sh);
+    sy = block_sum(sy, sh);
+    const double inv_n = 1.0 / NR;
+    const double g = -1.0 / ((double)Lr * (double)(NR * NR - NR));
+    const cd off = cmk(sx * g, sy * g);
+    for (long e = threadIdx.x; e < Q; e += blockDim.x) {
+        const int c = (int)(e / (NR * NR)), i = (int)(e - (long)c * NR * NR);
+        const bool diag = (i / NR) == (i % NR);
+        o[e] = diag ? cscale(th[c * NR + r], inv_n) : off;
+    }
+}
+
 // Superimposed pilots ("Parallel/ParallelProtocol_Tp.py":63-86): hypotheses x_j + x_p,t.
 // The E-step runs on y'_t = y_t - H_t x_p,t (thread per (symbol, receive antenna)) and
 // the moments of x_j + x_p,t follow by the shift m' = m + x_p,
@@ -346,6 +396,17 @@ hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t
 #undef SBCE_RHS
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_gauss_rank1(const Problem& pb, const MstepArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(gauss_rank1_kernel, dim3(pb.B), dim3(256), 0, s, a, pb.Td, pb.P, pb.NT, pb.L);
+    return hipGetLastError();
+}
+
+hipError_t launch_gauss_expand(const Problem& pb, const cd* theta, cd* out, hipStream_t s) {
+    hipLaunchKernelGGL(gauss_expand_kernel, dim3(pb.NR, pb.B), dim3(256), 0, s, theta, out, pb.L,
+                       pb.NR);
     return hipGetLastError();
 }
 

@@ -84,6 +84,7 @@ struct Problem {
     int B, NT, NR, P, Tp, Td, M, L, K;
     int pr;            // partition_r (PM E-step modes)
     double varn;
+    double varx;       // Gaussian-prior E-step (SBCE_ESTEP_GAUSS)
 };
 
 struct EstepArgs {
@@ -138,6 +139,8 @@ hipError_t launch_sup_shift_mom(const Problem& pb, cd* mom, const cd* xsup, cons
                                 hipStream_t s);
 hipError_t launch_ser(const Problem& pb, const cd* xdest, const cd* xtrue, double* out,
                       hipStream_t s);
+hipError_t launch_gauss_rank1(const Problem& pb, const MstepArgs& a, hipStream_t s);
+hipError_t launch_gauss_expand(const Problem& pb, const cd* theta, cd* out, hipStream_t s);
 hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* out,
                        hipStream_t s);
 hipError_t launch_llf(const Problem& pb, const cd* theta, const cd* yp, const cd* up,

@@ -20,6 +20,9 @@ Reference operator -> entry point here:
                                PM_beta.py:42-112 (posterior list weights) -> em_pm_soft()
   em_zf / em_mmse(..., h_initial, h)
                                all_detectorsvsTd.py:98-133 / :54-96      -> em_zf(), em_mmse()
+  EM_Gaussian_proposed(y_d, y_p, T_d, T_p, z_p, PsiTilde_td, varn, itera, H_initial, varx, n_tx)
+                               MIMO_Gaussian_proposed.py:56-89 (Gaussian prior)
+                                                                        -> EM_Gaussian_proposed()
 Batched form for sweeps / benchmark: ``em_batch`` (one sbce_em call for all trials).
 
 Semantics kept from the reference: inputs are not mutated, theta is returned
@@ -52,13 +55,13 @@ def _dev(torch, arr, dtype=None):
 
 _MODES = {"soft": _lib.SBCE_ESTEP_SOFT, "hard": _lib.SBCE_ESTEP_HARD, "pm": _lib.SBCE_ESTEP_PM,
           "pm_soft": _lib.SBCE_ESTEP_PM_SOFT, "zf": _lib.SBCE_ESTEP_ZF,
-          "mmse": _lib.SBCE_ESTEP_MMSE}
+          "mmse": _lib.SBCE_ESTEP_MMSE, "gauss": _lib.SBCE_ESTEP_GAUSS}
 _SOLVES = {"chol": _lib.SBCE_SOLVE_CHOL, "drop": _lib.SBCE_SOLVE_CHOL_DROP}
 
 
 def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_true=None,
              h_true=None, solve="chol", return_device=False, partition_r=0,
-             return_decisions=False, x_sup=None):
+             return_decisions=False, x_sup=None, varx=1.0):
     """Run ``itera`` EM iterations on a batch of independent trials.
 
     Array layouts (complex128, batch-major, include/sbce.h):
@@ -70,7 +73,10 @@ def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_t
     mode: "soft" | "hard" | "pm" | "pm_soft" | "zf" | "mmse"; partition_r selects the PM
     list size.  return_decisions (hard modes): x_dest (B,T_d,n_tx), the last E-step's
     decisions (SER/log_max_SER.py:77-78).  x_sup (B,T_d,n_tx): pilot symbols superimposed
-    on the data (Parallel/ParallelProtocol_Tp.py:63-86), soft/hard modes.
+    on the data (Parallel/ParallelProtocol_Tp.py:63-86), soft/hard modes.  mode "gauss":
+    Gaussian-prior EM (MIMO_Gaussian_proposed.py:56-89) with prior variance parameter varx;
+    psi_d then has P = N rows (no direct path), cons is ignored, theta is the reduced
+    channel (gauss_expand_batch gives the reference's n_rx x Q matrix).
     Inputs may be numpy arrays or CUDA complex128 tensors (used in place).
     Returns dict(theta (B,K), llf (B,itera) or None, status (B,), iters_done (B,)).
     """
@@ -97,7 +103,7 @@ def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_t
     M = Cs.shape[0]
     if th.shape != (B, L * n_rx):
         raise ValueError(f"theta0 shape {tuple(th.shape)} != {(B, L * n_rx)}")
-    dims = _lib.Dims(B, n_tx, n_rx, P, T_p, T_d, M, int(partition_r), float(varn))
+    dims = _lib.Dims(B, n_tx, n_rx, P, T_p, T_d, M, int(partition_r), float(varn), float(varx))
     ws_bytes = _lib.workspace_bytes(dims)
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device="cuda")
     status = torch.zeros(B, dtype=torch.int32, device="cuda")
@@ -325,6 +331,87 @@ def em_superimposed(Y, T, Z, X_d, X_p, T_p, T_d, n_tx, PsiTilde_t, all_possibleS
     return _finish(res, verbose, itera)
 
 
+_GAUSS_CONS = np.array([1.0 + 0j, -1.0 + 0j])      # placeholder table: the Gaussian E-step has none
+
+
+def gauss_expand_batch(theta, n_tx, n_rx, return_device=False):
+    """The reference's n_rx x (N n_tx n_rx^2) channel matrix H_l (MIMO_Gaussian_proposed.py:
+    77-85) from reduced Gaussian-EM estimates theta (B, N n_tx n_rx), on the device
+    (sbce_gauss_expand)."""
+    torch = _torch()
+    lib = _lib.load()
+    th = theta if isinstance(theta, torch.Tensor) else _dev(torch, theta, np.complex128)
+    th = th.contiguous()
+    B, K = th.shape
+    P = K // (n_tx * n_rx)
+    Q = P * n_tx * n_rx * n_rx
+    dims = _lib.Dims(B, n_tx, n_rx, P, 0, 1, 2, 0, 1.0, 1.0)
+    out = torch.empty((B, n_rx, Q), dtype=torch.complex128, device="cuda")
+    _lib.check(lib.sbce_gauss_expand(dims, th.data_ptr(), out.data_ptr(),
+                                     torch.cuda.current_stream().cuda_stream), "sbce_gauss_expand")
+    if return_device:
+        return out
+    return out.cpu().numpy()
+
+
+def gaussian_regressors(z_p, N, n_tx, n_rx):
+    """u_p = psi_p (x) x_p from the reference's z_p = vec(kron(u_p^T, I_{n_rx})) =
+    u_p (x) vec(I_{n_rx}) (received_proposed :126); raises if z_p has another structure."""
+    L = N * n_tx
+    e = np.eye(n_rx).flatten(order="F")
+    if not len(z_p):
+        return np.zeros((0, L), dtype=complex)
+    Z = np.stack([np.asarray(z).reshape(-1) for z in z_p])
+    if Z.shape[1] != L * n_rx * n_rx:
+        raise ValueError(f"z_p has {Z.shape[1]} rows, expected N n_tx n_rx^2 = {L * n_rx * n_rx}")
+    U = Z[:, ::n_rx * n_rx]                           # first vec(I) entry of each block (= 1)
+    if not np.allclose(Z, np.einsum("tl,i->tli", U, e).reshape(Z.shape), rtol=1e-12, atol=0):
+        raise ValueError("z_p is not kron(psi_p (x) x_p, vec(I_n_rx)) (received_proposed :126)")
+    return U
+
+
+def reduce_gaussian_channel(H, n_tx, n_rx):
+    """Reduced channel theta[c n_rx + r] = H[r, c n_rx^2 : (c+1) n_rx^2] . vec(I): the only
+    part of H the Gaussian E-step sees (H Sigma_t, Sigma_t = kron(., e e^H))."""
+    H = np.asarray(H, dtype=complex)
+    Lr = H.shape[1] // (n_rx * n_rx)
+    Hr = np.einsum("rcjj->rc", H.reshape(n_rx, Lr, n_rx, n_rx))
+    return Hr.T.reshape(-1)
+
+
+last_gaussian_reduced = None
+
+
+def EM_Gaussian_proposed(y_d, y_p, T_d, T_p, z_p, PsiTilde_td, varn, itera, H_initial, varx,
+                         n_tx, verbose=False, solve="chol"):
+    """Gaussian-prior EM (Proposed method/MIMO_Gaussian_proposed.py:56-89, same signature):
+    x ~ CN(0, varx I) with the reference's prior covariance varx^2 kron(kron(psi psi^H, I),
+    vec(I) vec(I)^H) (:33-45), itera + 1 iterations (``while j <= itera``), returns the
+    n_rx x (N n_tx n_rx^2) matrix H_l.  The device runs the reduced form (include/sbce.h,
+    SBCE_ESTEP_GAUSS / sbce_gauss_expand); the reference's inv = lstsq pseudo-inverse equals
+    the reduced inverse whenever the reduced G is nonsingular (status flags a non-HPD G)."""
+    global last_gaussian_reduced
+    Psi = np.asarray(PsiTilde_td)[:, :T_d]
+    N = Psi.shape[0]
+    n_rx = np.asarray(y_d[0]).shape[0]
+    U_p = gaussian_regressors(z_p[:T_p], N, n_tx, n_rx)
+    yd = np.stack([np.asarray(v).reshape(-1) for v in y_d[:T_d]])[None]
+    yp = (np.stack([np.asarray(v).reshape(-1) for v in y_p[:T_p]])[None] if T_p
+          else np.zeros((1, 0, n_rx), dtype=complex))
+    th0 = reduce_gaussian_channel(H_initial, n_tx, n_rx)[None]
+    res = em_batch(yd, yp, Psi.T[None], U_p[None], _GAUSS_CONS, varn, int(itera) + 1, th0,
+                   mode="gauss", solve=solve, varx=varx, return_device=True)
+    torch = _torch()
+    global last_status
+    last_status = int(res["status"][0].item())
+    last_gaussian_reduced = res["theta"][0].cpu().numpy()
+    H = gauss_expand_batch(res["theta"], n_tx, n_rx)[0]
+    if verbose:
+        print(np.linalg.norm(H))
+    torch.cuda.current_stream().synchronize()
+    return H
+
+
 def ser_batch(x_dest, x_d_true):
     """Per-trial SER on the device (sbce_ser): (ser_reference, ser_elementwise), the first
     being the expression of PMd/SER/log_max_SER.py:162."""
@@ -347,14 +434,15 @@ def em_zero_init(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, v
 
 
 # ------------------------------------------------------------------ diagnostic stages
-def _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn, partition_r=0):
+def _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn, partition_r=0, varx=1.0):
     def dev(x):
         return _dev(torch, x, np.complex128)
     Yd, Yp, Ps, Up, Cs, Th = (dev(y_d), dev(y_p), dev(psi_d), dev(u_p), dev(cons), dev(theta))
     B, T_d, n_rx = Yd.shape
     T_p, P, L = Yp.shape[1], Ps.shape[2], Up.shape[2]
     n_tx = L // P
-    dims = _lib.Dims(B, n_tx, n_rx, P, T_p, T_d, Cs.shape[0], int(partition_r), float(varn))
+    dims = _lib.Dims(B, n_tx, n_rx, P, T_p, T_d, Cs.shape[0], int(partition_r), float(varn),
+                     float(varx))
     ws = torch.empty(max(_lib.workspace_bytes(dims), 16), dtype=torch.uint8, device="cuda")
     status = torch.zeros(B, dtype=torch.int32, device="cuda")
     ptrs = _lib.Ptrs(Yd.data_ptr(), Yp.data_ptr() if T_p else Yd.data_ptr(), Ps.data_ptr(),
@@ -364,7 +452,7 @@ def _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn, partition_r=0):
     return dims, ptrs, keep
 
 
-def estep_batch(y_d, psi_d, cons, theta, varn, n_tx, mode="soft", partition_r=0):
+def estep_batch(y_d, psi_d, cons, theta, varn, n_tx, mode="soft", partition_r=0, varx=1.0):
     """One device E-step (sbce_estep): returns m (B,T_d,n_tx), S (B,T_d,n_tx,n_tx)."""
     torch = _torch()
     lib = _lib.load()
@@ -372,7 +460,8 @@ def estep_batch(y_d, psi_d, cons, theta, varn, n_tx, mode="soft", partition_r=0)
     P = np.shape(psi_d)[2]
     y_p = np.zeros((B, 0, n_rx), dtype=complex)
     u_p = np.zeros((B, 0, P * n_tx), dtype=complex)
-    dims, ptrs, keep = _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn, partition_r)
+    dims, ptrs, keep = _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn, partition_r,
+                                    varx)
     mom = torch.zeros((B, T_d, n_tx + n_tx * n_tx), dtype=torch.complex128, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
     _lib.check(lib.sbce_estep(dims, ptrs, _MODES[mode], mom.data_ptr(), stream), "sbce_estep")

@@ -151,6 +151,26 @@ def received_signals(T_p, T_d, Psi_tp, Psi_td, n_rx, n_tx, X_d, X_p, h, varn, rs
     return Y_p, Y_d, U_p, U_d, h0
 
 
+def gaussian_channel(varh, N, n_rx, n_tx, rs=None):
+    """channelMatrix1 of MIMO_Gaussian_proposed.py:9-14 in reduced form: h =
+    vec(khatri_rao(H_BS^T, H_SU)) (column-major, no direct path); the reference's full
+    matrix is H = kron(h^T, I_{n_rx}) (full_gaussian_channel)."""
+    rs = _rs(rs)
+    H_BS = rs.normal(loc=0, scale=np.sqrt(varh / 2), size=(N, n_tx * 2)).view(np.complex128)
+    H_SU = rs.normal(loc=0, scale=np.sqrt(varh / 2), size=(n_rx, N * 2)).view(np.complex128)
+    return sla.khatri_rao(H_BS.T, H_SU).flatten(order="F")
+
+
+def full_gaussian_channel(h, n_rx):
+    return np.kron(np.asarray(h)[None, :], np.eye(n_rx, dtype=complex))
+
+
+def gaussian_symbols(n_tx, T, varx, rs=None):
+    """symbols / pilotSymbols of MIMO_Gaussian_proposed.py:17-22: (n_tx, T) CN(0, varx)."""
+    rs = _rs(rs)
+    return rs.normal(loc=0, scale=np.sqrt(varx / 2), size=(n_tx, T * 2)).view(np.complex128)
+
+
 def snr_to_varn(snr_db, power=10.0):
     """varn = power / 10^(SNR/10) (PMd/SNR/all_Detectors.py:351-354; power = 16-QAM E_s)."""
     return power / np.power(10.0, np.asarray(snr_db, dtype=float) / 10.0)

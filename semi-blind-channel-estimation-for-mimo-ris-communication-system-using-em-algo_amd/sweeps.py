@@ -6,6 +6,7 @@ estimator with every trial of a sweep point batched into ONE sbce_em call.
   nmse_vs_snr  "Proposed method/SNR/all_Detectors.py":331-395 (exact and log-max EMs)
   ser_vs_snr   "Proposed method/SER/log_max_SER.py":124-167 (log-max EM decisions)
   nmse_vs_tp_superimposed  "Parallel/ParallelProtocol_Tp.py":106-136 (superimposed pilots)
+  nmse_vs_tp_gaussian      "Proposed method/MIMO_Gaussian_proposed.py":158-177 (Gaussian prior)
 
 Data generation (host, NumPy):
   replay=True   the reference's exact legacy-RandomState call order after
@@ -20,7 +21,7 @@ import numpy as np
 
 from . import signal_model as sm
 from .distributed import Accumulators, shard
-from .em import em_batch, ser_batch
+from .em import em_batch, ser_batch, gauss_expand_batch, nmse_batch, _GAUSS_CONS
 from .qam import qam_constellation
 
 
@@ -285,5 +286,56 @@ def nmse_vs_tp_superimposed(T_p=(4, 8, 12, 16, 20, 24, 28, 32, 36, 40), T_d=50, 
                      cons, varn, itera, np.zeros((B, L * n_rx), dtype=complex), mode="soft",
                      x_sup=np.stack([t["X_sup"] for t in trials]))
         acc.add(k, _nmse(r["theta"], np.stack([t["h"] for t in trials])))
+    acc.allreduce(dist)
+    return np.asarray(T_p), acc.mean_nmse()
+
+
+def gen_gaussian(T_p=(8, 12, 16, 20, 24, 28, 32, 36, 40), T_d=50, N=32, n_rx=2, n_tx=2,
+                 monte_iter=1, varn=0.1, varx=1.0, seed=0, replay=True, varh=1.0, keep=None):
+    """Data of MIMO_Gaussian_proposed.py:160-169 in the reference draw order: per trial
+    channelMatrix1 and symbols(n_tx, T_d, varx); per T_p irsMatrix (N x T_p DFT + T_d
+    uniform phase draws), pilotSymbols, received_proposed (one noise draw per symbol).
+    Reduced form: u_p = psi_p (x) x_p, y = H z = H_r u, h_initial = Y_p pinv(Z_p) reduced."""
+    keep = set(range(monte_iter)) if keep is None else set(keep)
+    points = [[] for _ in T_p]
+    if replay:
+        np.random.seed(seed)
+    for i in range(monte_iter):
+        rs = None if replay else _trial_rng(seed, i)
+        if not replay and i not in keep:
+            continue
+        h = sm.gaussian_channel(varh, N, n_rx, n_tx, rs=rs)
+        X_d = sm.gaussian_symbols(n_tx, T_d, varx, rs=rs)
+        for k, tp in enumerate(T_p):
+            Ptp, Ptd = sm.irs_matrix(tp, T_d, N, pilot="dft_n", rs=rs)
+            Ptp = Ptp[:N]
+            X_p = sm.gaussian_symbols(n_tx, tp, varx, rs=rs)
+            Y_p, Y_d, U_p, _, h0 = sm.received_signals(tp, T_d, Ptp, Ptd, n_rx, n_tx, X_d.T,
+                                                       X_p.T, h, varn, rs=rs)
+            if i in keep:
+                points[k].append(dict(Y_d=Y_d, Y_p=Y_p, U_p=U_p, Psi_d=Ptd, h0=h0, h=h))
+    return points
+
+
+def nmse_vs_tp_gaussian(T_p=(8, 12, 16, 20, 24, 28, 32, 36, 40), T_d=50, N=32, n_rx=2, n_tx=2,
+                        itera=3, monte_iter=1, varn=0.1, varx=1.0, seed=0, replay=True,
+                        varh=1.0):
+    """Mean NMSE per pilot length of the Gaussian-prior EM (MIMO_Gaussian_proposed.py:
+    158-177): trace(|(H_hat - H)^H (H_hat - H)|) / ||H||^2 (:173) on the full n_rx x Q
+    matrices, H_hat = the reference-format expansion of the device estimate."""
+    dist, world, rank = _dist()
+    mine = shard(monte_iter, world, rank).tolist()
+    points = gen_gaussian(T_p, T_d, N, n_rx, n_tx, monte_iter, varn, varx, seed, replay, varh,
+                          keep=mine)
+    acc = Accumulators(len(T_p))
+    for k, trials in enumerate(points):
+        if not trials:
+            continue
+        d = _pack(trials, N)
+        r = em_batch(d["y_d"], d["y_p"], d["psi_d"], d["u_p"], _GAUSS_CONS, varn, itera + 1,
+                     d["theta0"], mode="gauss", varx=varx, return_device=True)
+        Hh = gauss_expand_batch(r["theta"], n_tx, n_rx, return_device=True)
+        Hf = np.stack([sm.full_gaussian_channel(h, n_rx).reshape(-1) for h in d["h"]])
+        acc.add(k, nmse_batch(Hh.reshape(len(trials), -1), Hf).cpu().numpy())
     acc.allreduce(dist)
     return np.asarray(T_p), acc.mean_nmse()

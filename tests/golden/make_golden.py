@@ -327,6 +327,33 @@ def case_superimposed():
     return "superimposed", out
 
 
+def case_gaussian():
+    """Proposed method/MIMO_Gaussian_proposed.py: Gaussian-prior EM (EM_Gaussian_proposed
+    :56-89, run itera + 1 times) on the script's own generators (channelMatrix1, symbols,
+    pilotSymbols, irsMatrix, received_proposed; driver order :160-170), n_rx = 1, 2, 3."""
+    out = {}
+    for k, (N, n_tx, n_rx, T_d, T_p, varn, varx, itera, seed) in enumerate(
+            [(4, 2, 2, 12, 8, 0.1, 1.0, 3, 31), (4, 2, 1, 12, 8, 0.1, 1.0, 3, 32),
+             (3, 1, 3, 10, 6, 0.2, 1.0, 2, 33), (4, 2, 2, 12, 8, 0.1, 0.7, 2, 34)]):
+        ns = load_defs(os.path.join(PMD, "MIMO_Gaussian_proposed.py"),
+                       beta_max=2 * np.pi)
+        np.random.seed(seed)
+        H = ns["channelMatrix1"](1.0, N, n_rx, n_tx)
+        X_d = ns["symbols"](n_tx, T_d, varx)
+        Ptp, Ptd = ns["irsMatrix"](T_p, T_d, N, 0.0, 1.0)
+        X_p = ns["pilotSymbols"](n_tx, T_p, varx)
+        y_p, y_d, z_p, z_d, H0 = ns["received_proposed"](T_p, T_d, Ptp, Ptd, n_rx, n_tx, X_d,
+                                                         X_p, H, varn)
+        Hh = quiet(ns["EM_Gaussian_proposed"], y_d, y_p, T_d, T_p, z_p, Ptd, varn, itera, H0,
+                   varx, n_tx)
+        out.update({f"dims{k}": np.array([N, n_tx, n_rx, T_d, T_p, itera]),
+                    f"varn{k}": varn, f"varx{k}": varx, f"H{k}": H, f"X_d{k}": X_d,
+                    f"X_p{k}": X_p, f"Ptp{k}": Ptp, f"Ptd{k}": Ptd,
+                    f"Y_p{k}": np.stack(y_p)[..., 0], f"Y_d{k}": np.stack(y_d)[..., 0],
+                    f"Z_p{k}": np.stack(z_p)[..., 0], f"H0{k}": H0, f"H_hat{k}": Hh})
+    return "gaussian", out
+
+
 def case_qam():
     """Constellation tables of the vendored komm QAM (PMd/QAM.py:320-322)."""
     return "qam", {f"cons{M}": _cons(M) for M in (4, 16, 64, 256)}
@@ -338,6 +365,7 @@ CASES = {
     "pm_nt3_m16": (case_pm, ("pm_nt3_m16", 4, 3, 3, 24, 10, 16, 0.3, 3, 13, 1, 1)),
     "ser_logmax": (case_ser, ()),
     "superimposed": (case_superimposed, ()),
+    "gaussian": (case_gaussian, ()),
     "det_nt3": (case_det, ("det_nt3", 4, 3, 4, 30, 10, 4, 0.2, 3, 21)),
     "det_nt2_m16": (case_det, ("det_nt2_m16", 5, 2, 3, 30, 12, 16, 0.3, 3, 22)),
     "kat1_s7": (case_kat1, (7,)),

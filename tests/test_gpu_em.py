@@ -239,6 +239,7 @@ def test_snr_sweep_entry_point_reproduces_reference_curve(sbce):
     ("log_max_SER.py", ["--monte-iter", "2", "--SNR", "0", "20", "--N", "8"], 2),
     ("ParallelProtocol_Tp.py", ["--monte-iter", "2", "--T-p", "8", "60", "--N", "8",
                                 "--itera", "3"], 2),
+    ("MIMO_Gaussian_proposed.py", ["--monte-iter", "2", "--T-p", "8", "40"], 2),
 ])
 def test_sweep_scripts_run(sbce, script, args, rows, tmp_path):
     import os
@@ -499,3 +500,54 @@ def test_superimposed_sweep_entry_point(sbce):
     h = d["h"]
     ref = [np.sum(np.abs(d[f"theta{k}"] - h) ** 2) / np.sum(np.abs(h) ** 2) for k in range(2)]
     assert np.allclose(nm, ref, rtol=1e-9, atol=0)
+
+
+# ---------------------------------------------------------------- Gaussian-prior EM
+def _gauss_case(d, k):
+    N, n_tx, n_rx, T_d, T_p, itera = (int(v) for v in d[f"dims{k}"])
+    return N, n_tx, n_rx, T_d, T_p, itera, float(d[f"varn{k}"]), float(d[f"varx{k}"])
+
+
+@pytest.mark.parametrize("k", range(4))
+def test_em_gaussian_matches_reference(sbce, k):
+    """Drop-in EM_Gaussian_proposed (MIMO_Gaussian_proposed.py:56-89, reference signature and
+    output format) vs the reference's own H_l: n_rx = 2, 1 (rank-one all-ones term kept),
+    3, and varx != 1."""
+    d = golden("gaussian")
+    N, n_tx, n_rx, T_d, T_p, itera, varn, varx = _gauss_case(d, k)
+    y_d = [y[:, None] for y in d[f"Y_d{k}"]]
+    y_p = [y[:, None] for y in d[f"Y_p{k}"]]
+    z_p = [z[:, None] for z in d[f"Z_p{k}"]]
+    H = sbce.EM_Gaussian_proposed(y_d, y_p, T_d, T_p, z_p, d[f"Ptd{k}"], varn, itera, d[f"H0{k}"],
+                                  varx, n_tx)
+    ref = d[f"H_hat{k}"]
+    assert H.shape == ref.shape and H.dtype == np.complex128
+    assert rel(H, ref) < 1e-9
+
+
+@pytest.mark.parametrize("n_tx,n_rx", [(2, 2), (5, 3), (3, 8), (8, 1), (1, 4)])
+def test_gaussian_estep_matches_oracle(sbce, n_tx, n_rx):
+    """Device Gaussian E-step (LMMSE mean + posterior covariance) vs oracle, batch of 3."""
+    from oracle.gaussian import gaussian_moments
+    rng = np.random.default_rng(n_tx * 10 + n_rx)
+    B, N, T_d, varn, varx = 3, 5, 7, 0.3, 0.8
+    cn = lambda *s: (rng.standard_normal(s) + 1j * rng.standard_normal(s)) / np.sqrt(2)
+    th = cn(B, N * n_tx * n_rx)
+    y = cn(B, T_d, n_rx) * 3
+    psi = np.exp(1j * rng.uniform(0, 2 * np.pi, (B, T_d, N)))
+    m, S = sbce.estep_batch(y, psi, np.array([1 + 0j, -1 + 0j]), th, varn, n_tx, mode="gauss",
+                            varx=varx)
+    for b in range(B):
+        Hr = th[b].reshape(N * n_tx, n_rx).T
+        mo, Co = gaussian_moments(Hr, y[b], psi[b].T, varn, varx, n_tx)
+        assert rel(m[b], mo) < 1e-12 and rel(S[b], Co) < 1e-12
+
+
+def test_gaussian_sweep_entry_point(sbce):
+    """sweeps.nmse_vs_tp_gaussian (the script's driver, NMSE :173) on the fixture's data."""
+    d = golden("gaussian")
+    N, n_tx, n_rx, T_d, T_p, itera, varn, varx = _gauss_case(d, 0)
+    tps, nm = sbce.sweeps.nmse_vs_tp_gaussian((T_p,), T_d, N, n_rx, n_tx, itera, 1, varn, varx, 31)
+    H = d["H0"]
+    ref = np.sum(np.abs(d["H_hat0"] - H) ** 2) / np.sum(np.abs(H) ** 2)
+    assert np.allclose(nm, [ref], rtol=1e-9, atol=0)

@@ -345,3 +345,57 @@ def test_superimposed_sweep_replays_reference_data(sbce):
         assert np.array_equal(t["h"], d["h"]) and np.array_equal(t["Psi"], d[f"Psi{k}"])
         assert np.array_equal(t["X_sup"], _sup_padded(d, k))
         assert rel(t["Y"], d[f"Y{k}"]) < 1e-13
+
+
+# ---------------------------------------------------------------- Gaussian-prior EM
+def _gauss_case(d, k):
+    N, n_tx, n_rx, T_d, T_p, itera = (int(v) for v in d[f"dims{k}"])
+    return N, n_tx, n_rx, T_d, T_p, itera, float(d[f"varn{k}"]), float(d[f"varx{k}"])
+
+
+@pytest.mark.parametrize("k", range(4))
+def test_gaussian_oracle_matches_reference(k):
+    """MIMO_Gaussian_proposed.py EM_Gaussian_proposed: the literal Q x Q restatement and the
+    reduced form (+ expansion) against the reference's own output (n_rx = 2, 1, 3; varx != 1)."""
+    from oracle import gaussian as g
+    d = golden("gaussian")
+    N, n_tx, n_rx, T_d, T_p, itera, varn, varx = _gauss_case(d, k)
+    ref = d[f"H_hat{k}"]
+    lit = g.em_gaussian_literal(d[f"Y_d{k}"], d[f"Y_p{k}"], d[f"Z_p{k}"], d[f"Ptd{k}"], varn,
+                                itera, d[f"H0{k}"], varx, n_tx)
+    assert rel(lit, ref) < 1e-10
+    U = np.stack([np.kron(d[f"Ptp{k}"][:, t], d[f"X_p{k}"][:, t]) for t in range(T_p)])
+    Hr = g.em_gaussian_reduced(d[f"Y_d{k}"], d[f"Y_p{k}"], U, d[f"Ptd{k}"], varn, itera,
+                               g.reduce_channel(d[f"H0{k}"], n_tx, n_rx), varx, n_tx)
+    assert rel(g.expand(Hr, n_rx), ref) < 1e-10
+
+
+def test_gaussian_host_layout(sbce):
+    """Host-side reduction of the reference's z_p / H_initial (em.gaussian_regressors,
+    em.reduce_gaussian_channel) against the oracle."""
+    from oracle import gaussian as g
+    d = golden("gaussian")
+    for k in range(4):
+        N, n_tx, n_rx, T_d, T_p, itera, varn, varx = _gauss_case(d, k)
+        U = sbce.gaussian_regressors(list(d[f"Z_p{k}"]), N, n_tx, n_rx)
+        Uo = np.stack([np.kron(d[f"Ptp{k}"][:, t], d[f"X_p{k}"][:, t]) for t in range(T_p)])
+        assert rel(U, Uo) < 1e-15
+        th = sbce.reduce_gaussian_channel(d[f"H0{k}"], n_tx, n_rx)
+        assert rel(th, g.reduce_channel(d[f"H0{k}"], n_tx, n_rx).T.reshape(-1)) < 1e-15
+    bad = np.array(d["Z_p0"])
+    bad[0, 1] = 1.0
+    with pytest.raises(ValueError):
+        sbce.gaussian_regressors(list(bad), 4, 2, 2)
+
+
+def test_gaussian_sweep_replays_reference_data(sbce):
+    """sweeps.gen_gaussian reproduces the reference script's draw order (fixture case 0/1)."""
+    d = golden("gaussian")
+    for k, seed in ((0, 31), (1, 32)):
+        N, n_tx, n_rx, T_d, T_p, itera, varn, varx = _gauss_case(d, k)
+        t = sbce.sweeps.gen_gaussian((T_p,), T_d, N, n_rx, n_tx, 1, varn, varx, seed)[0][0]
+        H = sbce.signal_model.full_gaussian_channel(t["h"], n_rx)
+        assert np.array_equal(H, d[f"H{k}"])
+        assert np.array_equal(t["Psi_d"], d[f"Ptd{k}"])
+        assert rel(t["Y_d"], d[f"Y_d{k}"]) < 1e-13 and rel(t["Y_p"], d[f"Y_p{k}"]) < 1e-13
+        assert rel(t["h0"], sbce.reduce_gaussian_channel(d[f"H0{k}"], n_tx, n_rx)) < 1e-12
