@@ -20,8 +20,9 @@ Two faces:
   * ``em_gaussian_literal`` — the Q x Q computation as written (small sizes only);
   * ``em_gaussian_reduced`` — what the GPU computes: with H_eff(t) = sum_n psi_n Hr_n
     (Hr = the reduced n_rx x (N n_tx) channel, Hr[:, c] = H[:, block c] e), per symbol
-        M_t = varn^2 I + varx^2 H_eff H_eff^H,  m_t = varx^2 H_eff^H M_t^-1 y_t,
-        C_t = varx^2 I - varx^4 H_eff^H M_t^-1 H_eff,
+        m_t = varx^2 H_eff^H M_t^-1 y_t,  C_t = varx^2 I - varx^4 H_eff^H M_t^-1 H_eff
+    (M_t = varn^2 I + varx^2 H_eff H_eff^H), evaluated in the equivalent push-through form
+        A_t = H_eff^H H_eff + (varn^2 / varx^2) I,  m_t = A_t^-1 H_eff^H y_t,  C_t = varn^2 A_t^-1,
     G = sum_p u_p u_p^H + sum_t (psi_t psi_t^H) (x) C_t (the reduced M-step with S_t = C_t),
     Hr = B G^-1 (B = sum_p y_p u_p^H + sum_t y_t (psi_t (x) m_t)^H); for n_rx = 1 the
     all-ones term stays: G + c 1 1^T, c = sum_t ||psi_t||^2 ||m_t||^2.  ``expand`` maps Hr
@@ -100,10 +101,10 @@ def gaussian_moments(Hr, Y_d, Psi_td, varn, varx, n_tx):
     C = np.zeros((T_d, n_tx, n_tx), dtype=complex)
     for t in range(T_d):
         He = np.einsum("rna,n->ra", Hc, Psi_td[:, t])
-        Mt = varn ** 2 * np.eye(n_rx) + vx * He @ np.conj(He).T
-        W = np.conj(He).T @ np.linalg.inv(Mt)
-        m[t] = vx * W @ Y_d[t]
-        C[t] = vx * np.eye(n_tx) - vx * vx * W @ He
+        # push-through form of vx H^H (varn^2 I + vx H H^H)^-1 (.) (positive definite C)
+        Ainv = np.linalg.inv(np.conj(He).T @ He + (varn ** 2 / vx) * np.eye(n_tx))
+        m[t] = Ainv @ (np.conj(He).T @ Y_d[t])
+        C[t] = varn ** 2 * Ainv
     return m, C
 
 

@@ -284,21 +284,6 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
 // C/D value q at row (l>>4) + 4q, column l&15.
 constexpr int KCM = 16;                // k-chunk of the A-operand register pipeline
 
-// 1/sqrt(x) for x > 0 in ~10 dependent VALU ops instead of the ~25 of the IEEE sqrt +
-// division sequences (whose latency sets the pace of the column chain): exponent split,
-// v_rsq_f32 seed on the mantissa, two f64 Newton steps (2^-24 -> 2^-48 -> ~1 ulp).
-__device__ __forceinline__ double fast_rsqrt(double x) {
-    const int e = __builtin_amdgcn_frexp_exp(x);          // x = m 2^e, m in [0.5, 1)
-    const int h = e >> 1;
-    const double xs = __builtin_amdgcn_ldexp(x, -2 * h);  // in [0.5, 2)
-    double y = (double)__builtin_amdgcn_rsqf((float)xs);
-    double r = fma(-xs * y, y, 1.0);
-    y = fma(0.5 * y, r, y);
-    r = fma(-xs * y, y, 1.0);
-    y = fma(0.5 * y, r, y);
-    return __builtin_amdgcn_ldexp(y, -h);
-}
-
 // One-wave factorisation of the w x w diagonal block held in LDS A[16][16] (lower part
 // valid).  Lane l owns entries (row (l>>4) + 4h, col l&15), h < 4.  Column c costs ONE
 // LDS round trip: every lane reads the pivot and the column entries it needs, then

@@ -402,6 +402,106 @@ __global__ __launch_bounds__(256) void estep_kernel(EstepArgs a, EstepConst c) {
 // ============================================================================
 typedef double d4v __attribute__((ext_vector_type(4)));
 
+// Initial bound for the hypothesis sweep: the distance ||y - H x_c||^2 of x_c = the
+// per-stream nearest constellation points of the regularised LS estimate
+// (H^H H + reg I)^-1 H^H y.  x_c is a real hypothesis, so its weight bounds the posterior
+// maximum from below: as the initial log-sum-exp shift it loses nothing, and as the initial
+// hard-decision bound (plus a rounding margin) it keeps the argmin.  At medium and high SNR
+// x_c is the ML point, the running minimum never moves and nearly every tile group is
+// dismissed by one comparison.  Wave-uniform (every lane computes the same value); `scale`
+// bounds the magnitude of the terms a tile distance is assembled from (rounding margin).
+template <int NT, int NR>
+__device__ double candidate_distance(const cd* H, const cd* yg, const cd* s_cons, int M,
+                                     double reg, cd* scratch, int lane, double& scale) {
+    cd* sG = scratch;            // [NT][NT]
+    cd* sHy = scratch + 16;      // [NT]
+    if (lane < NT * NT) {
+        const int u = lane / NT, v = lane - u * NT;
+        cd acc = czero();
+#pragma unroll
+        for (int r = 0; r < NR; ++r) acc = cfmac(acc, H[v * NR + r], H[u * NR + r]);
+        if (u == v) acc.x += reg;
+        sG[lane] = acc;
+    } else if (lane >= 32 && lane < 32 + NT) {
+        const int u = lane - 32;
+        cd acc = czero();
+#pragma unroll
+        for (int r = 0; r < NR; ++r) acc = cfmac(acc, yg[r], H[u * NR + r]);
+        sHy[u] = acc;
+    }
+    wave_sync();
+    // complex Cholesky G = L L^H and the two triangular solves, in registers
+    cd Lm[NT][NT];
+    double dinv[NT];
+    cd z[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        double d = sG[j * NT + j].x;
+#pragma unroll
+        for (int k = 0; k < j; ++k) d -= cabs2(Lm[j][k]);
+        const double inv = fast_rsqrt(fmax(d, 1e-300));
+        dinv[j] = inv;
+#pragma unroll
+        for (int i = j + 1; i < NT; ++i) {
+            cd s = sG[i * NT + j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) s = csub(s, cmulc(Lm[i][k], Lm[j][k]));
+            Lm[i][j] = cscale(s, inv);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+        cd s = sHy[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) s = csub(s, cmul(Lm[i][k], z[k]));
+        z[i] = cscale(s, dinv[i]);
+    }
+#pragma unroll
+    for (int i = NT - 1; i >= 0; --i) {
+        cd s = z[i];
+#pragma unroll
+        for (int k = i + 1; k < NT; ++k) s = csub(s, cmul(cconj(Lm[k][i]), z[k]));
+        z[i] = cscale(s, dinv[i]);
+    }
+    // nearest constellation point per stream: lanes 16 q .. 16 q + 15 handle stream q
+    const int qa = lane >> 4;
+    cd za = z[0];
+#pragma unroll
+    for (int q = 1; q < NT; ++q) za = csel(qa == q, z[q], za);
+    double bd = INFINITY;
+    int bs = 0;
+    if (qa < NT)
+        for (int s = lane & 15; s < M; s += 16) {
+            const double dd = cabs2(csub(za, s_cons[s]));
+            if (dd < bd) { bd = dd; bs = s; }
+        }
+    for (int off = 8; off >= 1; off >>= 1) {
+        const double od = shfl_xor_d(bd, off);
+        const int os = __shfl_xor(bs, off);
+        if (od < bd || (od == bd && os < bs)) { bd = od; bs = os; }
+    }
+    cd x[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) x[q] = s_cons[__shfl(bs, 16 * q)];
+    double d0 = 0.0, sc = 0.0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        cd res = yg[r];
+        sc += cabs2(res);
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            const cd hx = cmul(H[q * NR + r], x[q]);
+            res = csub(res, hx);
+            sc += NT * cabs2(hx);
+        }
+        d0 += cabs2(res);
+    }
+    wave_sync();                 // scratch is reused by the caller
+    scale = sc;
+    return d0;
+}
+
+
 constexpr int kMfmaWaves = 2;
 constexpr int kChunk = 256;
 
@@ -410,6 +510,9 @@ struct MfmaConst {
     int JA, JB, chunk, nparts;
     int tab_d;                 // per-wave LDS doubles
     double inv_s2, thr_d;
+    double reg;                // ridge of the candidate's LS estimate (0.1 varn^2)
+    int nkt_pad;               // column tiles JB / 16, rounded up to even (LDS carve)
+    int prune;                 // column-tile bounds on (SBCE_ESTEP_PRUNE=0 disables: A/B runs)
 };
 
 // V16 (M == 16, NA == 2): the A operand's V term, V[kk][i & 15] = V[kk][lane & 15], is the
@@ -418,8 +521,98 @@ struct MfmaConst {
 // tests use min(acc) + gamma and the rare exp path adds it back.  (PMC at cfg1 showed
 // the f64 VALU work between the MFMAs, which does not co-execute with them, as the
 // limiter: 40 % MFMA busy.)
-template <int NT, int NR, int MODE, int TU, bool V16 = false>
-__global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst c) {
+// Exact lower bounds per column tile (16 consecutive k): every hypothesis (i, k) has
+//   d_ik = ||y - H_A x_A(i) - H_B x_B(k)||^2 >= min_x ||(y - H_B x_B(k)) - H_A x||^2
+//        = ||P (y - H_B x_B(k))||^2,      P = projector onto span(H_A)^perp
+// (the best continuous x_A can do no better: the partial distance of a sphere decoder).
+// A tile whose bound exceeds the skip bound holds only hypotheses whose weights are below
+// e^-50 of the posterior maximum (soft) or that cannot be the argmin (hard), exactly the
+// hypotheses the per-group test already discards, so the sweep skips their MFMAs.  P comes
+// from a twice-orthogonalised Gram-Schmidt basis of H_A, lane r of each 8-lane group owning
+// component r; a near-dependent H_A (or n_rx <= |A|, where P = 0) leaves the bounds at 0.
+// Returns the magnitude scale of the bound terms (rounding margin).
+template <int NT, int NR>
+__device__ double column_tile_bounds(const cd* H, const cd* yg, const cd* s_cons, int M, int lm,
+                                     int nkt, double* s_lb, cd* scratch, int lane) {
+    constexpr int NA = NT / 2, NB = NT - NA;
+    const int mask = M - 1;
+    const int r = lane & 7;
+    const bool own = r < NR;
+    int xa[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) xa[i] = (lane ^ (32 >> i)) << 2;     // xor 32 .. 1
+    auto rsum = [&](double v) {                                      // sum over the 8-lane group
+#pragma unroll
+        for (int i = 3; i < 6; ++i) v += bperm_d(v, xa[i]);
+        return v;
+    };
+    auto rdot = [&](cd u, cd v) { return cmk(rsum(fma(v.x, u.x, v.y * u.y)),    // u^H v
+                                             rsum(fma(v.y, u.x, -v.x * u.y))); };
+    cd u[NA];
+    bool ok = true;
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+        cd v = own ? H[q * NR + r] : czero();
+        const double h2 = rsum(cabs2(v));
+#pragma unroll
+        for (int rep = 0; rep < 2; ++rep)
+#pragma unroll
+            for (int j = 0; j < q; ++j) v = csub(v, cmul(u[j], rdot(u[j], v)));
+        const double n2 = rsum(cabs2(v));
+        ok = ok && h2 > 0.0 && n2 > 1e-6 * h2;
+        u[q] = cscale(v, ok ? fast_rsqrt(n2) : 0.0);
+    }
+    cd w = own ? yg[r] : czero();
+    double sc = rsum(cabs2(w));
+    cd g[NB];
+    double g2 = 0.0;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        g[b] = own ? H[(NA + b) * NR + r] : czero();
+        g2 += cabs2(g[b]);
+    }
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+        w = csub(w, cmul(u[j], rdot(u[j], w)));
+#pragma unroll
+        for (int b = 0; b < NB; ++b) g[b] = csub(g[b], cmul(u[j], rdot(u[j], g[b])));
+    }
+    if (lane < NR) {
+        scratch[r] = w;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) scratch[8 * (b + 1) + r] = g[b];
+    }
+    // scale: ||y||^2 + NB sum_b ||h_b||^2 max|c|^2 bounds every term of a bound
+    double cmax2 = lane < M ? cabs2(s_cons[lane]) : 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) cmax2 = fmax(cmax2, bperm_d(cmax2, xa[i]));
+    sc += NB * cmax2 * rsum(g2);
+    wave_sync();
+    for (int kt0 = 0; kt0 < nkt; kt0 += 4) {
+        const int kt = kt0 + (lane >> 4);
+        const int k = kt * 16 + (lane & 15);
+        cd xb[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) xb[b] = s_cons[(k >> (lm * (NB - 1 - b))) & mask];
+        double lb = 0.0;
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) {
+            cd res = scratch[rr];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) res = csub(res, cmul(scratch[8 * (b + 1) + rr], xb[b]));
+            lb += cabs2(res);
+        }
+        if (!ok) lb = 0.0;
+#pragma unroll
+        for (int i = 2; i < 6; ++i) lb = fmin(lb, bperm_d(lb, xa[i]));   // 16-lane minimum
+        if ((lane & 15) == 0 && kt < nkt) s_lb[kt] = lb;
+    }
+    wave_sync();
+    return sc;
+}
+
+template <int NT, int NR, int MODE, int TU, bool V16>
+__device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaConst& c) {
     constexpr int NA = NT / 2;
     constexpr int NB = NT - NA;
     constexpr int NO = NT * NR;
@@ -438,7 +631,9 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
     double* s_al = wbase + 2 * NO;                             // chunk
     double* s_U = s_al + c.chunk;                              // [KPAD][M]
     double* s_V = s_U + 4 * STEPS * c.M;                       // [KPAD][M]   (NA == 2)
-    double* s_tab = s_V + 4 * STEPS * c.M;                     // scratch: 64 cd
+    double* s_Q2 = s_V + 4 * STEPS * c.M;                      // [KPAD][M]   (V16)
+    double* s_lb = s_Q2 + 4 * STEPS * c.M;                     // [nkt] column-tile bounds
+    double* s_tab = s_lb + c.nkt_pad;                          // scratch: 64 cd
 
     for (int i = threadIdx.x; i < c.M; i += blockDim.x) s_cons[i] = a.cons[i];
     __syncthreads();
@@ -473,9 +668,16 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
     }
     const cd* H = s_heff;
     const double inv_s2 = c.inv_s2;
+    double cscale_d;
+    const double d0 = candidate_distance<NT, NR>(H, a.yd + (size_t)gsym * NR, s_cons, c.M, c.reg,
+                                                 reinterpret_cast<cd*>(s_tab), lane, cscale_d);
+    const double lb_scale = column_tile_bounds<NT, NR>(H, a.yd + (size_t)gsym * NR, s_cons, c.M,
+                                                       c.lm, c.JB >> 4, s_lb,
+                                                       reinterpret_cast<cd*>(s_tab), lane);
+    const double lb_margin = c.prune ? 1e-9 * lb_scale : INFINITY;
 
     // lane-level accumulators (see VALU kernel)
-    double mshift = INFINITY;
+    double mshift = d0;              // a real hypothesis' distance (candidate_distance)
     double tot_c = 0.0;
     cd tot_muA[NA];
     double nu[NA];
@@ -492,7 +694,8 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
     }
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) { tot_mB[bb] = czero(); tot_nB[bb] = 0.0; }
-    double best_d = INFINITY;
+    double best_d = d0 + 1e-10 * cscale_d + 1e-300;   // admits the argmin (rounding margin)
+                                                       // (== hard_bound below)
     int best_j = 0x7fffffff;
 
     // U_s = -2 (y - h_0 x_s),  V_s = 2 h_1 x_s  so that  -2 p_i = U_{s0(i)} + V_{s1(i)}
@@ -501,7 +704,7 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
         wave_sync();
         for (int e = lane; e < c.M * 4 * STEPS; e += 64) {
             const int kk = e / c.M, sx = e - kk * c.M;
-            double u = 0.0, v = 0.0;
+            double u = 0.0, v = 0.0, q2 = 0.0;
             if (kk < K2) {
                 const int r = kk >> 1;
                 const cd x = s_cons[sx];
@@ -512,52 +715,85 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
                     const cd hv = cmul(H[1 * NR + r], x);
                     v = 2.0 * ((kk & 1) ? hv.y : hv.x);
                 }
+                if (V16) {
+                    const cd hq = cmul(H[NA * NR + r], x);
+                    q2 = (kk & 1) ? hq.y : hq.x;
+                }
             }
             s_U[e] = u;
             if (NA == 2) s_V[e] = v;
+            if (V16) s_Q2[e] = q2;
         }
         wave_sync();
     }
     const int col = lane & 15;
     const int rq = lane >> 4;
-    double vreg[STEPS];
+    // V16: hoisted A-operand V term, and the B operand q_k = h_NA x_kt + h_NA+1 x_col split
+    // into a per-kt LDS row (s_Q2) plus a lane constant (q3reg)
+    double vreg[STEPS], q3reg[STEPS];
 #pragma unroll
-    for (int s = 0; s < STEPS; ++s) vreg[s] = V16 ? s_V[(4 * s + rq) * 16 + col] : 0.0;
+    for (int s = 0; s < STEPS; ++s) {
+        const int kk = 4 * s + rq;
+        vreg[s] = V16 ? s_V[kk * 16 + col] : 0.0;
+        double q3 = 0.0;
+        if (V16 && kk < K2) {
+            const cd hx = cmul(H[(NA + 1) * NR + (kk >> 1)], s_cons[col]);
+            q3 = (kk & 1) ? hx.y : hx.x;
+        }
+        q3reg[s] = q3;
+    }
+    const int xaddr16 = (lane ^ 16) << 2, xaddr32 = (lane ^ 32) << 2;
     const int nktile = c.JB >> 4;
     const int ntile_chunk = c.chunk >> 4;
     bool table_ready = false;
 
+    const double hard_bound = d0 + 1e-10 * cscale_d + 1e-300;
     for (int kt = 0; kt < nktile; ++kt) {
+        // exact column-tile bound (column_tile_bounds): wave-uniform skip of the whole tile
+        if (s_lb[kt] > ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin)
+            continue;
         const int k = kt * 16 + col;
         cd xb[NB];
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb) xb[bb] = s_cons[(k >> (c.lm * (NB - 1 - bb))) & mask];
-        cd qv[NR];
-        double gam = 0.0;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            cd acc = czero();
-#pragma unroll
-            for (int bb = 0; bb < NB; ++bb) acc = cfma(acc, H[(NA + bb) * NR + r], xb[bb]);
-            qv[r] = acc;
-            gam += cabs2(acc);
-        }
         double bop[STEPS];
+        double gam = 0.0;
+        if constexpr (V16) {
+            // gamma_k = ||q_k||^2 = sum over the 4 lanes of column k of their bop^2
 #pragma unroll
-        for (int s = 0; s < STEPS; ++s) {
-            const int kk = 4 * s + rq;
-            double v = 0.0;
+            for (int s = 0; s < STEPS; ++s) {
+                bop[s] = s_Q2[(4 * s + rq) * 16 + kt] + q3reg[s];
+                gam = fma(bop[s], bop[s], gam);
+            }
+            gam += bperm_d(gam, xaddr16);
+            gam += bperm_d(gam, xaddr32);
+        } else {
+            cd qv[NR];
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-                if (kk == 2 * r) v = qv[r].x;
-                if (kk == 2 * r + 1) v = qv[r].y;
+                cd acc = czero();
+#pragma unroll
+                for (int bb = 0; bb < NB; ++bb) acc = cfma(acc, H[(NA + bb) * NR + r], xb[bb]);
+                qv[r] = acc;
+                gam += cabs2(acc);
             }
-            bop[s] = v;
+#pragma unroll
+            for (int s = 0; s < STEPS; ++s) {
+                const int kk = 4 * s + rq;
+                double v = 0.0;
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    if (kk == 2 * r) v = qv[r].x;
+                    if (kk == 2 * r + 1) v = qv[r].y;
+                }
+                bop[s] = v;
+            }
         }
         double ck = 0.0;
         cd mu[NA];
 #pragma unroll
         for (int q = 0; q < NA; ++q) mu[q] = czero();
+        bool touched = false;       // wave-uniform: an exp was taken in this column tile
 
         for (int i0 = 0; i0 < c.JA; i0 += c.chunk) {
             if (!table_ready) {
@@ -580,9 +816,8 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
                 table_ready = (c.JA == c.chunk);
             }
             for (int tg = 0; tg < ntile_chunk; tg += TU) {
-                // TU independent 16x16 tiles in flight: STEPS*TU MFMAs per group
-                // accumulators start at alpha_i; gamma_k (lane constant) is added to the
-                // tile minima only
+                // TU independent 16x16 tiles in flight: STEPS*TU MFMAs per group;
+                // accumulators start at alpha_i, gamma_k (lane constant) stays outside
                 d4v acc[TU];
 #pragma unroll
                 for (int u = 0; u < TU; ++u)
@@ -603,8 +838,19 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
                         }
                         acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bop[s], acc[u], 0, 0, 0);
                     }
+                double cm = fmin(fmin(acc[0][0], acc[0][1]), fmin(acc[0][2], acc[0][3]));
+#pragma unroll
+                for (int u = 1; u < TU; ++u)
+                    cm = fmin(cm, fmin(fmin(acc[u][0], acc[u][1]), fmin(acc[u][2], acc[u][3])));
+                // one comparison per tile group (soft: within thr of the shift, hard: not
+                // worse than this lane's best); the common case skips everything below
                 if (MODE == SBCE_ESTEP_HARD) {
-                    const double lim = best_d - gam;       // acc + gam < best_d  <=>  acc < lim
+                    if (!__any(cm + gam <= best_d)) continue;
+                } else if (!__any(cm + gam <= mshift + c.thr_d)) {
+                    continue;
+                }
+                if (MODE == SBCE_ESTEP_HARD) {
+                    const double lim = best_d - gam;
 #pragma unroll
                     for (int u = 0; u < TU; ++u)
 #pragma unroll
@@ -618,15 +864,11 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
                         }
                     continue;
                 }
-                double cm = fmin(fmin(acc[0][0], acc[0][1]), fmin(acc[0][2], acc[0][3]));
-#pragma unroll
-                for (int u = 1; u < TU; ++u)
-                    cm = fmin(cm, fmin(fmin(acc[u][0], acc[u][1]), fmin(acc[u][2], acc[u][3])));
                 cm += gam;
                 if (__any(cm < mshift)) {
                     double mn = fmin(cm, mshift);
                     for (int off = 32; off >= 1; off >>= 1) mn = fmin(mn, shfl_xor_d(mn, off));
-                    const double f = (mshift == INFINITY) ? 0.0 : fexp_neg((mn - mshift) * inv_s2);
+                    const double f = fexp_neg((mn - mshift) * inv_s2);
                     mshift = mn;
                     tot_c *= f; ck *= f; kap = cscale(kap, f); tot_kB = cscale(tot_kB, f);
 #pragma unroll
@@ -639,6 +881,7 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
                     for (int bb = 0; bb < NB; ++bb) { tot_mB[bb] = cscale(tot_mB[bb], f); tot_nB[bb] *= f; }
                 }
                 if (!__any(cm <= mshift + c.thr_d)) continue;
+                touched = true;
 #pragma unroll
                 for (int u = 0; u < TU; ++u) {
                     const double cmu =
@@ -662,7 +905,7 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
                 }
             }
         }
-        if (MODE == SBCE_ESTEP_SOFT) {
+        if (MODE == SBCE_ESTEP_SOFT && touched) {
             tot_c += ck;
 #pragma unroll
             for (int bb = 0; bb < NB; ++bb) {
@@ -700,18 +943,27 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
         }
         return;
     }
-    tot_c = seg_sum(tot_c, 64);
-    kap = seg_sum(kap, 64);
-    tot_kB = seg_sum(tot_kB, 64);
+    int xa[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) xa[i] = (lane ^ (32 >> i)) << 2;
+    auto wsum = [&](double v) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) v += bperm_d(v, xa[i]);
+        return v;
+    };
+    auto wsumc = [&](cd v) { return cmk(wsum(v.x), wsum(v.y)); };
+    tot_c = wsum(tot_c);
+    kap = wsumc(kap);
+    tot_kB = wsumc(tot_kB);
 #pragma unroll
     for (int q = 0; q < NA; ++q) {
-        tot_muA[q] = seg_sum(tot_muA[q], 64);
-        nu[q] = seg_sum(nu[q], 64);
+        tot_muA[q] = wsumc(tot_muA[q]);
+        nu[q] = wsum(nu[q]);
 #pragma unroll
-        for (int bb = 0; bb < NB; ++bb) tot_X[q][bb] = seg_sum(tot_X[q][bb], 64);
+        for (int bb = 0; bb < NB; ++bb) tot_X[q][bb] = wsumc(tot_X[q][bb]);
     }
 #pragma unroll
-    for (int bb = 0; bb < NB; ++bb) { tot_mB[bb] = seg_sum(tot_mB[bb], 64); tot_nB[bb] = seg_sum(tot_nB[bb], 64); }
+    for (int bb = 0; bb < NB; ++bb) { tot_mB[bb] = wsumc(tot_mB[bb]); tot_nB[bb] = wsum(tot_nB[bb]); }
     if (lane == 0) {
         const double iz = 1.0 / tot_c;
         cd m[NT];
@@ -742,6 +994,18 @@ __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst 
     }
 }
 
+template <int NT, int NR, int MODE, int TU, bool V16 = false>
+__global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst c) {
+    estep_mfma_body<NT, NR, MODE, TU, V16>(a, c);
+}
+// Same kernel held to 168 VGPRs (3 waves per SIMD); the few spills this costs at
+// n_rx <= 4 sit in the per-column-tile code, outside the MFMA group loop.
+template <int NT, int NR, int MODE, int TU, bool V16 = false>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) void
+estep_mfma_kernel_occ3(EstepArgs a, MfmaConst c) {
+    estep_mfma_body<NT, NR, MODE, TU, V16>(a, c);
+}
+
 bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     if (pb.NT < 2 || pb.NT > 4 || pb.NR < 1 || pb.NR > 8) return false;
     if (pb.M < 2 || pb.M > 64 || (pb.M & (pb.M - 1))) return false;
@@ -756,10 +1020,14 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     const int NO = pb.NT * pb.NR;
     c.nparts = NO <= 64 ? 64 / NO : 1;
     const int steps = (2 * pb.NR + 3) / 4;
-    c.tab_d = 2 * NO + c.chunk + 2 * (4 * steps) * pb.M + 128;   // heff|alpha|U|V|64-cd scratch
+    c.nkt_pad = (int)((JB / 16 + 1) / 2 * 2);
+    c.tab_d = 2 * NO + c.chunk + 3 * (4 * steps) * pb.M + c.nkt_pad + 128;   // heff|alpha|U|V|Q2|lb|scratch
+    const char* pr = getenv("SBCE_ESTEP_PRUNE");
+    c.prune = !(pr && pr[0] == '0');
     c.tab_d = (c.tab_d + 1) / 2 * 2;          // keep 16-B alignment per wave
     c.inv_s2 = 1.0 / (pb.varn * pb.varn);
     c.thr_d = kSkipThr * pb.varn * pb.varn;
+    c.reg = 0.1 * pb.varn * pb.varn;
     lds = 64 * sizeof(cd) + (size_t)kMfmaWaves * c.tab_d * sizeof(double);
     const long nsym = (long)pb.B * pb.Td;
     blocks = (nsym + kMfmaWaves - 1) / kMfmaWaves;
@@ -771,6 +1039,18 @@ hipError_t dispatch_mfma_mode(const MfmaConst& c, size_t lds, long blocks, const
                               int mode, hipStream_t s) {
     const bool tu4 = (c.chunk / 16) % 4 == 0;
     if (NT == 4 && c.M == 16 && tu4) {            // cfg1 geometry: hoisted V operand
+        const char* occ = getenv("SBCE_ESTEP_OCC");   // "2": no VGPR cap (A/B runs)
+        if constexpr (NR <= 4) {
+            if (!(occ && occ[0] == '2')) {
+                if (mode == SBCE_ESTEP_HARD)
+                    hipLaunchKernelGGL((estep_mfma_kernel_occ3<NT, NR, SBCE_ESTEP_HARD, 4, true>),
+                                       dim3((unsigned)blocks), dim3(64 * kMfmaWaves), lds, s, a, c);
+                else
+                    hipLaunchKernelGGL((estep_mfma_kernel_occ3<NT, NR, SBCE_ESTEP_SOFT, 4, true>),
+                                       dim3((unsigned)blocks), dim3(64 * kMfmaWaves), lds, s, a, c);
+                return hipGetLastError();
+            }
+        }
         if (mode == SBCE_ESTEP_HARD)
             hipLaunchKernelGGL((estep_mfma_kernel<NT, NR, SBCE_ESTEP_HARD, 4, true>),
                                dim3((unsigned)blocks), dim3(64 * kMfmaWaves), lds, s, a, c);

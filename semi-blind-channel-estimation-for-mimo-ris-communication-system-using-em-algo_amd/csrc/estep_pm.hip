@@ -130,45 +130,29 @@ __global__ __launch_bounds__(64 * kPmWaves) void estep_pm_kernel(EstepArgs a, Pm
     if (MODE == 6) {
         // ---- Gaussian prior x ~ CN(0, vx I), vx = varx^2 (MIMO_Gaussian_proposed.py:69-76) ----
         // With z_t = (psi_t (x) x_t) (x) vec(I) the posterior of z_t reduces to that of x_t on
-        // H_eff = H_true (all P = N rows of psi, no off-by-one):
-        //   M = varn^2 I + vx H H^H (n_rx x n_rx, :71),  W = H^H M^-1,
-        //   m = vx W y (:72),  C = vx I - vx^2 W H (:74-75, without the m m^H part: the
-        //   reference's mean_prod is the SCALAR ||mu||^2, handled in the M-step).
-        {
-            const int u = lane >> 3, v = lane & 7;
-            if (u < NR && v < NR) {
-                cd acc = czero();
-                for (int q = 0; q < NT; ++q) acc = cfmac(acc, Ht[q * NR + u], Ht[q * NR + v]);
-                acc = cscale(acc, c.vx);
-                if (u == v) acc.x += c.s2;
-                aug[u * kAugW + v] = acc;
-                aug[u * kAugW + 8 + v] = (u == v) ? cmk(1.0, 0.0) : czero();
-            }
-        }
-        wave_sync();
-        gj_inverse(aug, NR, lane);
-        {
-            const int aa = lane / NR, r = lane - aa * NR;    // W[aa][r], lanes < NT*NR <= 64
-            if (aa < NT) {
-                cd acc = czero();
-                for (int u = 0; u < NR; ++u) acc = cfma(acc, cconj(Ht[aa * NR + u]), aug[u * kAugW + 8 + r]);
-                GB[aa * NR + r] = acc;
-            }
-        }
-        wave_sync();
-        cd* out = a.mom + (size_t)gsym * (NT + NT * NT);
-        const int ai = lane >> 3, bi = lane & 7;
-        if (ai < NT && bi < NT) {
-            cd acc = czero();
-            for (int r = 0; r < NR; ++r) acc = cfma(acc, GB[ai * NR + r], Ht[bi * NR + r]);
-            acc = cscale(acc, -c.vx * c.vx);
-            if (ai == bi) acc.x += c.vx;
-            out[NT + ai * NT + bi] = acc;
-        }
+        // H_eff = H_true (all P = N rows of psi, no off-by-one).  The reference's form
+        //   m = vx H^H (varn^2 I + vx H H^H)^-1 y,  C = vx I - vx^2 H^H (...)^-1 H   (:71-75)
+        // is evaluated through the push-through identity as
+        //   A = H^H H + (varn^2 / vx) I,  m = A^-1 H^H y,  C = varn^2 A^-1,
+        // equal in exact arithmetic and positive definite by construction (the difference
+        // form loses definiteness once the reference's iteration diverges).  C excludes
+        // m m^H: the reference's mean_prod is the SCALAR ||mu||^2 (M-step, n_rx = 1).
+        gram(aug, Ht, cols, NT, NR, lane);
+        if (lane < NT) aug[lane * kAugW + lane].x += c.s2 / c.vx;
         if (lane < NT) {
             cd acc = czero();
-            for (int r = 0; r < NR; ++r) acc = cfma(acc, GB[lane * NR + r], yv[r]);
-            out[lane] = cscale(acc, c.vx);
+            for (int r = 0; r < NR; ++r) acc = cfmac(acc, yv[r], Ht[lane * NR + r]);   // H^H y
+            Gy[lane] = acc;
+        }
+        wave_sync();
+        gj_inverse(aug, NT, lane);
+        cd* out = a.mom + (size_t)gsym * (NT + NT * NT);
+        const int ai = lane >> 3, bi = lane & 7;
+        if (ai < NT && bi < NT) out[NT + ai * NT + bi] = cscale(aug[ai * kAugW + 8 + bi], c.s2);
+        if (lane < NT) {
+            cd acc = czero();
+            for (int q = 0; q < NT; ++q) acc = cfma(acc, aug[lane * kAugW + 8 + q], Gy[q]);
+            out[lane] = acc;
         }
         return;
     }

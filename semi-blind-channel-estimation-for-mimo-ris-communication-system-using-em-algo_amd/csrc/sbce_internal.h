@@ -78,6 +78,29 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 __device__ __forceinline__ double shfl_xor_d(double v, int m) { return __shfl_xor(v, m); }
+// ds_bpermute of a double from the lane whose byte address (4 * lane) is `addr`; with the
+// address computed once, a butterfly step costs no VALU beyond the combine
+__device__ __forceinline__ double bperm_d(double v, int addr) {
+    const int lo = __builtin_amdgcn_ds_bpermute(addr, __double2loint(v));
+    const int hi = __builtin_amdgcn_ds_bpermute(addr, __double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+
+// 1/sqrt(x) for x > 0 in ~10 dependent VALU ops instead of the ~25 of the IEEE sqrt +
+// division sequences (whose latency sets the pace of the column chain): exponent split,
+// v_rsq_f32 seed on the mantissa, two f64 Newton steps (2^-24 -> 2^-48 -> ~1 ulp).
+__device__ __forceinline__ double fast_rsqrt(double x) {
+    const int e = __builtin_amdgcn_frexp_exp(x);          // x = m 2^e, m in [0.5, 1)
+    const int h = e >> 1;
+    const double xs = __builtin_amdgcn_ldexp(x, -2 * h);  // in [0.5, 2)
+    double y = (double)__builtin_amdgcn_rsqf((float)xs);
+    double r = fma(-xs * y, y, 1.0);
+    y = fma(0.5 * y, r, y);
+    r = fma(-xs * y, y, 1.0);
+    y = fma(0.5 * y, r, y);
+    return __builtin_amdgcn_ldexp(y, -h);
+}
+
 
 // ------------------------------------------------------------------ launch API
 struct Problem {

@@ -383,13 +383,16 @@ last_gaussian_reduced = None
 
 
 def EM_Gaussian_proposed(y_d, y_p, T_d, T_p, z_p, PsiTilde_td, varn, itera, H_initial, varx,
-                         n_tx, verbose=False, solve="chol"):
+                         n_tx, verbose=False, solve="drop"):
     """Gaussian-prior EM (Proposed method/MIMO_Gaussian_proposed.py:56-89, same signature):
     x ~ CN(0, varx I) with the reference's prior covariance varx^2 kron(kron(psi psi^H, I),
     vec(I) vec(I)^H) (:33-45), itera + 1 iterations (``while j <= itera``), returns the
     n_rx x (N n_tx n_rx^2) matrix H_l.  The device runs the reduced form (include/sbce.h,
-    SBCE_ESTEP_GAUSS / sbce_gauss_expand); the reference's inv = lstsq pseudo-inverse equals
-    the reduced inverse whenever the reduced G is nonsingular (status flags a non-HPD G)."""
+    SBCE_ESTEP_GAUSS / sbce_gauss_expand).  The reference's M-step inverse is the lstsq
+    pseudo-inverse (:47-53), so the default solve is the pivot-dropping Cholesky ("drop"),
+    identical to the plain inverse whenever the reduced G is well conditioned.  (At the
+    script's own defaults the reference iteration diverges after one step, NMSE ~1e6 and
+    growing; past that point neither its output nor this one is numerically meaningful.)"""
     global last_gaussian_reduced
     Psi = np.asarray(PsiTilde_td)[:, :T_d]
     N = Psi.shape[0]

@@ -333,7 +333,7 @@ def nmse_vs_tp_gaussian(T_p=(8, 12, 16, 20, 24, 28, 32, 36, 40), T_d=50, N=32, n
             continue
         d = _pack(trials, N)
         r = em_batch(d["y_d"], d["y_p"], d["psi_d"], d["u_p"], _GAUSS_CONS, varn, itera + 1,
-                     d["theta0"], mode="gauss", varx=varx, return_device=True)
+                     d["theta0"], mode="gauss", varx=varx, solve="drop", return_device=True)
         Hh = gauss_expand_batch(r["theta"], n_tx, n_rx, return_device=True)
         Hf = np.stack([sm.full_gaussian_channel(h, n_rx).reshape(-1) for h in d["h"]])
         acc.add(k, nmse_batch(Hh.reshape(len(trials), -1), Hf).cpu().numpy())

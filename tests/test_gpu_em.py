@@ -508,7 +508,7 @@ def _gauss_case(d, k):
     return N, n_tx, n_rx, T_d, T_p, itera, float(d[f"varn{k}"]), float(d[f"varx{k}"])
 
 
-@pytest.mark.parametrize("k", range(4))
+@pytest.mark.parametrize("k", range(5))
 def test_em_gaussian_matches_reference(sbce, k):
     """Drop-in EM_Gaussian_proposed (MIMO_Gaussian_proposed.py:56-89, reference signature and
     output format) vs the reference's own H_l: n_rx = 2, 1 (rank-one all-ones term kept),
@@ -522,7 +522,7 @@ def test_em_gaussian_matches_reference(sbce, k):
                                   varx, n_tx)
     ref = d[f"H_hat{k}"]
     assert H.shape == ref.shape and H.dtype == np.complex128
-    assert rel(H, ref) < 1e-9
+    assert rel(H, ref) < (1e-9 if k < 4 else 1e-4)     # case 4: the reference's own lstsq ~1e-5
 
 
 @pytest.mark.parametrize("n_tx,n_rx", [(2, 2), (5, 3), (3, 8), (8, 1), (1, 4)])

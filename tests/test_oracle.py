@@ -353,7 +353,7 @@ def _gauss_case(d, k):
     return N, n_tx, n_rx, T_d, T_p, itera, float(d[f"varn{k}"]), float(d[f"varx{k}"])
 
 
-@pytest.mark.parametrize("k", range(4))
+@pytest.mark.parametrize("k", range(5))
 def test_gaussian_oracle_matches_reference(k):
     """MIMO_Gaussian_proposed.py EM_Gaussian_proposed: the literal Q x Q restatement and the
     reduced form (+ expansion) against the reference's own output (n_rx = 2, 1, 3; varx != 1)."""
@@ -361,13 +361,16 @@ def test_gaussian_oracle_matches_reference(k):
     d = golden("gaussian")
     N, n_tx, n_rx, T_d, T_p, itera, varn, varx = _gauss_case(d, k)
     ref = d[f"H_hat{k}"]
+    # case 4 (N = 32, Q = 256): the reference's lstsq pseudo-inverse of the rank-65 256 x 256
+    # A is itself only good to ~1e-5 (two lstsq orderings differ by 2e-5)
+    tol = 1e-10 if k < 4 else 1e-4
     lit = g.em_gaussian_literal(d[f"Y_d{k}"], d[f"Y_p{k}"], d[f"Z_p{k}"], d[f"Ptd{k}"], varn,
                                 itera, d[f"H0{k}"], varx, n_tx)
-    assert rel(lit, ref) < 1e-10
+    assert rel(lit, ref) < tol
     U = np.stack([np.kron(d[f"Ptp{k}"][:, t], d[f"X_p{k}"][:, t]) for t in range(T_p)])
     Hr = g.em_gaussian_reduced(d[f"Y_d{k}"], d[f"Y_p{k}"], U, d[f"Ptd{k}"], varn, itera,
                                g.reduce_channel(d[f"H0{k}"], n_tx, n_rx), varx, n_tx)
-    assert rel(g.expand(Hr, n_rx), ref) < 1e-10
+    assert rel(g.expand(Hr, n_rx), ref) < tol
 
 
 def test_gaussian_host_layout(sbce):
