@@ -16,10 +16,13 @@ after the timed region, as in the reference's Monte-Carlo average
 (Proposed_method_NMSEvsTp.py:176).
 
 Also reported (one JSON line on rank 0):
-  roofline      E-step kernel (dominant) timed live with HIP events on the
-                launch stream; algorithmic flops per launch (DESIGN.md §4);
-                peak = FP64 rate of MI355X; traffic from the committed
-                rocprofv3 PMC summary when present.
+  roofline      the dominant phase (E-step or M-step, whichever is longer per
+                EM iteration) timed live with HIP events on the launch stream;
+                M-step: algorithmic flops per launch; E-step: the
+                FP64 MFMAs it issued (device counter; its exact bounds skip
+                provably negligible hypothesis tiles), with the full-enumeration
+                flops next to it; peak = FP64 rate of MI355X; traffic from the
+                committed rocprofv3 PMC summary when present.
   cpu_baseline  the build's vectorised float64 NumPy port of the same
                 algorithm (oracle/em_reduced.py) on a bounded sample of the
                 same workload, on this host's cores (rank 0, N=1 only).
@@ -213,6 +216,20 @@ def main():
     e1.record(stream)
     torch.cuda.synchronize()
     estep_ms = e0.elapsed_time(e1) / args.kernel_reps
+    # FP64 MFMAs the exact E-step actually issued at this theta (its exact column-tile
+    # bounds skip provably negligible tiles): one counted launch outside the timed loops
+    mfma_issued = None
+    lib = pkg._lib.load()
+    if mode in ("soft", "hard") and hasattr(lib, "sbce_debug_estep_mfma"):
+        import ctypes
+        cnt = ctypes.c_ulonglong(0)
+        os.environ["SBCE_ESTEP_COUNT"] = "1"
+        lib.sbce_debug_estep_mfma(None, 1)
+        eng.estep()
+        torch.cuda.synchronize()
+        lib.sbce_debug_estep_mfma(ctypes.byref(cnt), 0)
+        del os.environ["SBCE_ESTEP_COUNT"]
+        mfma_issued = int(cnt.value)
     e0.record(stream)
     for _ in range(args.kernel_reps):
         eng.mstep()
@@ -234,18 +251,30 @@ def main():
     if mode in ("soft", "hard"):
         flops = estep_flops_per_trial_iter(n_tx, n_rx, T_d, M) * B
         algo_bytes = estep_bytes_per_trial_iter(n_tx, n_rx, P, T_d) * B
-        achieved_tf = flops / (estep_ms * 1e-3) / 1e12
         if pmc and pmc.get("config") == args.config and pmc.get("trials") == B:
             traffic = pmc.get("hbm_bytes_per_launch")
-        roofline = {"bound": "mfma", "pipe": "FP64 MFMA v_mfma_f64_16x16x4f64 (+ FP64 VALU)",
-                    "kernel": "estep_mfma_kernel",
-                    "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
-                    "algorithmic_bytes": algo_bytes,
-                    "hbm_GBps_algorithmic": algo_bytes / (estep_ms * 1e-3) / 1e9,
-                    "hbm_frac_algorithmic": algo_bytes / (estep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                    "flops_per_launch": flops}
+        # executed work: the MFMAs issued (16x16x4 f64 = 2048 flop each); the full
+        # enumeration's flops are reported next to it ("enumeration_*")
+        executed = mfma_issued * 2048 if mfma_issued is not None else flops
+        achieved_tf = executed / (estep_ms * 1e-3) / 1e12
+        estep_roof = {"bound": "mfma", "pipe": "FP64 MFMA v_mfma_f64_16x16x4f64 (+ FP64 VALU)",
+                      "kernel": "estep_mfma_kernel", "ms": estep_ms,
+                      "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                      "flops_per_launch": executed,
+                      "enumeration_flops_per_launch": flops,
+                      "enumeration_fraction_issued": executed / flops,
+                      "algorithmic_bytes": algo_bytes,
+                      "hbm_GBps_algorithmic": algo_bytes / (estep_ms * 1e-3) / 1e9,
+                      "hbm_frac_algorithmic": algo_bytes / (estep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        # the dominant kernel (longest per EM iteration) carries the roofline object
+        if estep_ms >= mstep_ms:
+            roofline = estep_roof
+        else:
+            roofline = dict(mstep_roof, bound="mfma", traffic=None,
+                            pipe="FP64 MFMA v_mfma_f64_16x16x4f64 (+ FP64 VALU)")
     else:
+        estep_roof = None
         # list-detector workloads: the M-step (MFMA tile build + blocked Cholesky) dominates
         roofline = dict(mstep_roof, bound="mfma", traffic=None,
                         pipe="FP64 MFMA v_mfma_f64_16x16x4f64")
@@ -273,6 +302,7 @@ def main():
         "kernels_ms": {"estep": estep_ms, "mstep_build_plus_solve": mstep_ms},
         "roofline": roofline,
         "mstep_roofline": mstep_roof,
+        "estep_roofline": estep_roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(cfg, varn, args.seed,

@@ -16,7 +16,8 @@ constexpr size_t kAlign = 256;
 size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 struct Carve {
-    size_t mom, R, rhs, done, ysh, tol, winv, ppsi, pS, total;
+    size_t mom, R, rhs, done, ysh, prep, tol, winv, ppsi, pS, total;
+    bool has_prep;
 };
 
 bool make_problem(const sbce_dims* d, Problem& pb) {
@@ -41,7 +42,10 @@ Carve carve(const Problem& pb) {
     c.rhs = align_up(c.R + (size_t)pb.B * pb.L * pb.L * sizeof(cd));
     c.done = align_up(c.rhs + (size_t)pb.B * pb.L * pb.NR * sizeof(cd));
     c.ysh = align_up(c.done + (size_t)pb.B * sizeof(int32_t));         // superimposed pilots
-    c.tol = align_up(c.ysh + (size_t)pb.B * pb.Td * pb.NR * sizeof(cd));
+    c.prep = align_up(c.ysh + (size_t)pb.B * pb.Td * pb.NR * sizeof(cd));   // MFMA sweep prep
+    const int ps = estep_prep_stride(pb);
+    c.has_prep = ps > 0;
+    c.tol = align_up(c.prep + (size_t)pb.B * pb.Td * ps * sizeof(double));
     c.winv = c.ppsi = c.pS = c.tol;
     c.total = c.tol;
     if (pb.L > kLargeL) {                    // tiled large-L M-step (mstep_large.hip)
@@ -132,6 +136,7 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     ea.yd = (const cd*)p->y_d; ea.psid = (const cd*)p->psi_d; ea.theta = (const cd*)p->theta;
     ea.cons = (const cd*)p->cons; ea.mom = (cd*)(ws + c.mom); ea.done = early ? done : nullptr;
     ea.status = p->status;
+    ea.prep = c.has_prep ? (double*)(ws + c.prep) : nullptr;
     MstepArgs ma;
     ma.yd = ea.yd; ma.yp = (const cd*)p->y_p; ma.psid = ea.psid; ma.up = (const cd*)p->u_p;
     ma.mom = ea.mom; ma.R = (cd*)(ws + c.R); ma.rhs = (cd*)(ws + c.rhs); ma.theta = (cd*)p->theta;
@@ -189,6 +194,11 @@ int sbce_estep(const sbce_dims* d, const sbce_ptrs* p, int estep_mode, void* mom
     ea.yd = (const cd*)p->y_d; ea.psid = (const cd*)p->psi_d; ea.theta = (const cd*)p->theta;
     ea.cons = (const cd*)p->cons; ea.mom = (cd*)moments; ea.done = nullptr;
     ea.status = p->status;
+    ea.prep = nullptr;               // workspace optional here: use it when it is large enough
+    if (p->workspace && aligned16(p->workspace)) {
+        const Carve c = carve(pb);
+        if (c.has_prep && p->workspace_bytes >= c.total) ea.prep = (double*)((char*)p->workspace + c.prep);
+    }
     return hip_rc(launch_estep(pb, ea, estep_mode, (hipStream_t)hip_stream));
 }
 
@@ -229,6 +239,13 @@ int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int 
 int sbce_debug_chol_clock(unsigned long long* out32, int reset) {
     if (reset) return hip_rc(chol_debug_clock_reset());
     return out32 ? hip_rc(chol_debug_clock(out32)) : SBCE_EINVAL;
+}
+
+// Diagnostic, not part of include/sbce.h: FP64 MFMAs issued by the exact E-step sweep since
+// the last reset (counted only with SBCE_ESTEP_COUNT=1); reset != 0 clears the counter.
+int sbce_debug_estep_mfma(unsigned long long* out, int reset) {
+    if (!reset && !out) return SBCE_EINVAL;
+    return hip_rc(estep_debug_mfma(out, reset));
 }
 
 int sbce_ser(const sbce_dims* d, const void* x_dest, const void* x_d_true, double* ser_out,

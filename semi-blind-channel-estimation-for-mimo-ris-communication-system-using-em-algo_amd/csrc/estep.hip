@@ -513,6 +513,8 @@ struct MfmaConst {
     double reg;                // ridge of the candidate's LS estimate (0.1 varn^2)
     int nkt_pad;               // column tiles JB / 16, rounded up to even (LDS carve)
     int prune;                 // column-tile bounds on (SBCE_ESTEP_PRUNE=0 disables: A/B runs)
+    int count;                 // diagnostic MFMA count (SBCE_ESTEP_COUNT=1)
+    int prep_stride;           // doubles per symbol of EstepArgs::prep
 };
 
 // V16 (M == 16, NA == 2): the A operand's V term, V[kk][i & 15] = V[kk][lane & 15], is the
@@ -611,6 +613,10 @@ __device__ double column_tile_bounds(const cd* H, const cd* yg, const cd* s_cons
     return sc;
 }
 
+// Diagnostic (MfmaConst::count, SBCE_ESTEP_COUNT=1): FP64 MFMAs the sweep issued, for the
+// executed-work roofline next to the bounds' pruning.
+__device__ unsigned long long g_estep_mfma;
+
 template <int NT, int NR, int MODE, int TU, bool V16>
 __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaConst& c) {
     constexpr int NA = NT / 2;
@@ -646,8 +652,12 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     if (a.done && a.done[b]) return;
     const int mask = c.M - 1;
 
+    const double* prep = a.prep ? a.prep + (size_t)gsym * c.prep_stride : nullptr;
     // ---------------- H_eff(t) ----------------
-    {
+    if (prep) {
+        if (lane < NO) s_heff[lane] = cmk(prep[4 + 2 * lane], prep[5 + 2 * lane]);
+        wave_sync();
+    } else {
         const cd* th = a.theta + (size_t)b * c.P * NO;
         const cd* ps = a.psid + (size_t)gsym * c.P;
         const int ntask = NO * c.nparts;
@@ -668,12 +678,19 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     }
     const cd* H = s_heff;
     const double inv_s2 = c.inv_s2;
-    double cscale_d;
-    const double d0 = candidate_distance<NT, NR>(H, a.yd + (size_t)gsym * NR, s_cons, c.M, c.reg,
-                                                 reinterpret_cast<cd*>(s_tab), lane, cscale_d);
-    const double lb_scale = column_tile_bounds<NT, NR>(H, a.yd + (size_t)gsym * NR, s_cons, c.M,
-                                                       c.lm, c.JB >> 4, s_lb,
-                                                       reinterpret_cast<cd*>(s_tab), lane);
+    double cscale_d, d0, lb_scale;
+    if (prep) {                      // estep_prep_kernel did these per symbol
+        d0 = prep[0];
+        cscale_d = prep[1];
+        lb_scale = prep[2];
+        for (int e = lane; e < (c.JB >> 4); e += 64) s_lb[e] = prep[4 + 2 * NO + e];
+        wave_sync();
+    } else {
+        d0 = candidate_distance<NT, NR>(H, a.yd + (size_t)gsym * NR, s_cons, c.M, c.reg,
+                                        reinterpret_cast<cd*>(s_tab), lane, cscale_d);
+        lb_scale = column_tile_bounds<NT, NR>(H, a.yd + (size_t)gsym * NR, s_cons, c.M, c.lm,
+                                              c.JB >> 4, s_lb, reinterpret_cast<cd*>(s_tab), lane);
+    }
     const double lb_margin = c.prune ? 1e-9 * lb_scale : INFINITY;
 
     // lane-level accumulators (see VALU kernel)
@@ -748,6 +765,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     bool table_ready = false;
 
     const double hard_bound = d0 + 1e-10 * cscale_d + 1e-300;
+    unsigned groups = 0;             // wave-uniform count of issued tile groups
     for (int kt = 0; kt < nktile; ++kt) {
         // exact column-tile bound (column_tile_bounds): wave-uniform skip of the whole tile
         if (s_lb[kt] > ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin)
@@ -818,6 +836,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
             for (int tg = 0; tg < ntile_chunk; tg += TU) {
                 // TU independent 16x16 tiles in flight: STEPS*TU MFMAs per group;
                 // accumulators start at alpha_i, gamma_k (lane constant) stays outside
+                ++groups;
                 d4v acc[TU];
 #pragma unroll
                 for (int u = 0; u < TU; ++u)
@@ -922,6 +941,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
         }
     }
 
+    if (c.count && lane == 0) atomicAdd(&g_estep_mfma, (unsigned long long)groups * STEPS * TU);
     constexpr int MS = NT + NT * NT;
     cd* out = a.mom + (size_t)gsym * MS;
     if (MODE == SBCE_ESTEP_HARD) {
@@ -994,6 +1014,199 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     }
 }
 
+// ============================================================================
+// Per-symbol preparation pass (one THREAD per symbol) for the MFMA sweep: H_eff(t), the
+// candidate bound of candidate_distance and the column-tile bounds of column_tile_bounds,
+// written to the workspace (PrepLayout).  These are short dependent chains (a 4 x 4
+// Cholesky, a Gram-Schmidt, M-way minima): inside the sweep kernel one wave would run
+// them serially per symbol; here 64 symbols run them side by side per wave.
+// ============================================================================
+struct PrepConst {
+    int B, Td, P, M, lm, nkt, stride;
+    double reg;
+};
+
+template <int NT, int NR>
+__global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst c) {
+    constexpr int NA = NT / 2, NB = NT - NA, NO = NT * NR;
+    const long nsym = (long)c.B * c.Td;
+    const long gsym = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gsym >= nsym) return;
+    const int b = (int)(gsym / c.Td);
+    if (a.done && a.done[b]) return;
+    const int mask = c.M - 1;
+    // ---- H_eff(t) = sum_p psi_p H_p ----
+    cd H[NT][NR];
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) H[q][r] = czero();
+    const cd* th = a.theta + (size_t)b * c.P * NO;
+    const cd* ps = a.psid + (size_t)gsym * c.P;
+    for (int p = 0; p < c.P; ++p) {
+        const cd psi = ps[p];
+#pragma unroll
+        for (int q = 0; q < NT; ++q)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) H[q][r] = cfma(H[q][r], psi, th[p * NO + q * NR + r]);
+    }
+    cd y[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) y[r] = a.yd[(size_t)gsym * NR + r];
+    double* out = a.prep + (size_t)gsym * c.stride;
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            out[4 + 2 * (q * NR + r)] = H[q][r].x;
+            out[5 + 2 * (q * NR + r)] = H[q][r].y;
+        }
+    // ---- candidate: quantised ridge LS (candidate_distance, same arithmetic order) ----
+    {
+        cd Lm[NT][NT];
+        double dinv[NT];
+        cd z[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            cd gjj = czero();
+#pragma unroll
+            for (int r = 0; r < NR; ++r) gjj = cfmac(gjj, H[j][r], H[j][r]);
+            double d = gjj.x + c.reg;
+#pragma unroll
+            for (int k = 0; k < j; ++k) d -= cabs2(Lm[j][k]);
+            const double inv = fast_rsqrt(fmax(d, 1e-300));
+            dinv[j] = inv;
+#pragma unroll
+            for (int i = j + 1; i < NT; ++i) {
+                cd s = czero();
+#pragma unroll
+                for (int r = 0; r < NR; ++r) s = cfmac(s, H[j][r], H[i][r]);   // G[i][j]
+#pragma unroll
+                for (int k = 0; k < j; ++k) s = csub(s, cmulc(Lm[i][k], Lm[j][k]));
+                Lm[i][j] = cscale(s, inv);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            cd s = czero();
+#pragma unroll
+            for (int r = 0; r < NR; ++r) s = cfmac(s, y[r], H[i][r]);          // (H^H y)_i
+#pragma unroll
+            for (int k = 0; k < i; ++k) s = csub(s, cmul(Lm[i][k], z[k]));
+            z[i] = cscale(s, dinv[i]);
+        }
+#pragma unroll
+        for (int i = NT - 1; i >= 0; --i) {
+            cd s = z[i];
+#pragma unroll
+            for (int k = i + 1; k < NT; ++k) s = csub(s, cmul(cconj(Lm[k][i]), z[k]));
+            z[i] = cscale(s, dinv[i]);
+        }
+        cd x[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            double bd = INFINITY;
+            int bs = 0;
+            for (int s = 0; s < c.M; ++s) {
+                const double dd = cabs2(csub(z[q], a.cons[s]));
+                if (dd < bd) { bd = dd; bs = s; }
+            }
+            x[q] = a.cons[bs];
+        }
+        double d0 = 0.0, sc = 0.0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            cd res = y[r];
+            sc += cabs2(res);
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
+                const cd hx = cmul(H[q][r], x[q]);
+                res = csub(res, hx);
+                sc += NT * cabs2(hx);
+            }
+            d0 += cabs2(res);
+        }
+        out[0] = d0;
+        out[1] = sc;
+    }
+    // ---- column-tile bounds (column_tile_bounds) ----
+    {
+        cd u[NA][NR];
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < NA; ++q) {
+            cd v[NR];
+            double h2 = 0.0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) { v[r] = H[q][r]; h2 += cabs2(v[r]); }
+#pragma unroll
+            for (int rep = 0; rep < 2; ++rep)
+#pragma unroll
+                for (int j = 0; j < q; ++j) {
+                    cd pj = czero();
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) pj = cfmac(pj, v[r], u[j][r]);   // u_j^H v
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) v[r] = csub(v[r], cmul(u[j][r], pj));
+                }
+            double n2 = 0.0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) n2 += cabs2(v[r]);
+            ok = ok && h2 > 0.0 && n2 > 1e-6 * h2;
+            const double inv = ok ? fast_rsqrt(n2) : 0.0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) u[q][r] = cscale(v[r], inv);
+        }
+        cd w[NR], g[NB][NR];
+        double sc = 0.0, g2 = 0.0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) { w[r] = y[r]; sc += cabs2(y[r]); }
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) { g[bb][r] = H[NA + bb][r]; g2 += cabs2(g[bb][r]); }
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {
+            cd pw = czero(), pg[NB];
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb) pg[bb] = czero();
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                pw = cfmac(pw, w[r], u[j][r]);
+#pragma unroll
+                for (int bb = 0; bb < NB; ++bb) pg[bb] = cfmac(pg[bb], g[bb][r], u[j][r]);
+            }
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                w[r] = csub(w[r], cmul(u[j][r], pw));
+#pragma unroll
+                for (int bb = 0; bb < NB; ++bb) g[bb][r] = csub(g[bb][r], cmul(u[j][r], pg[bb]));
+            }
+        }
+        double cmax2 = 0.0;
+        for (int s = 0; s < c.M; ++s) cmax2 = fmax(cmax2, cabs2(a.cons[s]));
+        out[2] = sc + NB * cmax2 * g2;
+        double* lbo = out + 4 + 2 * NO;
+        for (int kt = 0; kt < c.nkt; ++kt) {
+            double lbm = INFINITY;
+            for (int s = 0; s < 16; ++s) {
+                const int k = kt * 16 + s;
+                double lb = 0.0;
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    cd res = w[r];
+#pragma unroll
+                    for (int bb = 0; bb < NB; ++bb)
+                        res = csub(res, cmul(g[bb][r], a.cons[(k >> (c.lm * (NB - 1 - bb))) & mask]));
+                    lb += cabs2(res);
+                }
+                lbm = fmin(lbm, lb);
+            }
+            lbo[kt] = ok ? lbm : 0.0;
+        }
+    }
+}
+
 template <int NT, int NR, int MODE, int TU, bool V16 = false>
 __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst c) {
     estep_mfma_body<NT, NR, MODE, TU, V16>(a, c);
@@ -1024,10 +1237,13 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     c.tab_d = 2 * NO + c.chunk + 3 * (4 * steps) * pb.M + c.nkt_pad + 128;   // heff|alpha|U|V|Q2|lb|scratch
     const char* pr = getenv("SBCE_ESTEP_PRUNE");
     c.prune = !(pr && pr[0] == '0');
+    const char* cnt = getenv("SBCE_ESTEP_COUNT");
+    c.count = cnt && cnt[0] == '1';
     c.tab_d = (c.tab_d + 1) / 2 * 2;          // keep 16-B alignment per wave
     c.inv_s2 = 1.0 / (pb.varn * pb.varn);
     c.thr_d = kSkipThr * pb.varn * pb.varn;
     c.reg = 0.1 * pb.varn * pb.varn;
+    c.prep_stride = 4 + 2 * NO + c.nkt_pad;
     lds = 64 * sizeof(cd) + (size_t)kMfmaWaves * c.tab_d * sizeof(double);
     const long nsym = (long)pb.B * pb.Td;
     blocks = (nsym + kMfmaWaves - 1) / kMfmaWaves;
@@ -1168,6 +1384,22 @@ hipError_t dispatch_nr(int NR, const Geometry& g, const EstepArgs& a, int mode, 
 
 }  // namespace
 
+hipError_t estep_debug_mfma(unsigned long long* out, int reset) {
+    if (reset) {
+        const unsigned long long z = 0;
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_estep_mfma), &z, sizeof(z), 0, hipMemcpyHostToDevice);
+    }
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_estep_mfma), sizeof(*out), 0,
+                               hipMemcpyDeviceToHost);
+}
+
+int estep_prep_stride(const Problem& pb) {
+    MfmaConst mc;
+    size_t lds;
+    long blocks;
+    return make_mfma(pb, mc, lds, blocks) ? mc.prep_stride : 0;
+}
+
 bool estep_supported(const Problem& pb, int mode) {
     if (mode >= SBCE_ESTEP_PM && mode <= SBCE_ESTEP_GAUSS) return estep_pm_supported(pb, pb.pr, mode);
     Geometry g;
@@ -1183,6 +1415,25 @@ hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStre
     long mblocks;
     if (!force_valu && make_mfma(pb, mc, mlds, mblocks)) {
         if (mblocks == 0) return hipSuccess;
+        if (a.prep) {
+            PrepConst pc;
+            pc.B = pb.B; pc.Td = pb.Td; pc.P = pb.P; pc.M = pb.M; pc.lm = mc.lm;
+            pc.nkt = mc.JB >> 4; pc.stride = mc.prep_stride; pc.reg = mc.reg;
+            const long nsym = (long)pb.B * pb.Td;
+            const dim3 pg((unsigned)((nsym + 255) / 256)), pblk(256);
+            hipError_t e = hipErrorInvalidValue;
+            switch (pb.NT * 16 + pb.NR) {
+#define SBCE_PREP(nt, nr) case nt * 16 + nr: hipLaunchKernelGGL((estep_prep_kernel<nt, nr>), pg, pblk, 0, s, a, pc); e = hipGetLastError(); break;
+                SBCE_PREP(2, 1) SBCE_PREP(2, 2) SBCE_PREP(2, 3) SBCE_PREP(2, 4)
+                SBCE_PREP(2, 5) SBCE_PREP(2, 6) SBCE_PREP(2, 7) SBCE_PREP(2, 8)
+                SBCE_PREP(3, 1) SBCE_PREP(3, 2) SBCE_PREP(3, 3) SBCE_PREP(3, 4)
+                SBCE_PREP(3, 5) SBCE_PREP(3, 6) SBCE_PREP(3, 7) SBCE_PREP(3, 8)
+                SBCE_PREP(4, 1) SBCE_PREP(4, 2) SBCE_PREP(4, 3) SBCE_PREP(4, 4)
+                SBCE_PREP(4, 5) SBCE_PREP(4, 6) SBCE_PREP(4, 7) SBCE_PREP(4, 8)
+#undef SBCE_PREP
+            }
+            if (e != hipSuccess) return e;
+        }
         switch (pb.NT) {
             case 2: return dispatch_mfma_nr<2>(pb.NR, mc, mlds, mblocks, a, mode, s);
             case 3: return dispatch_mfma_nr<3>(pb.NR, mc, mlds, mblocks, a, mode, s);

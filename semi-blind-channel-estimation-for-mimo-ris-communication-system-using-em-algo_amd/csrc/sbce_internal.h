@@ -118,6 +118,8 @@ struct EstepArgs {
     cd* mom;           // [B][Td][NT + NT*NT]
     const int32_t* done;  // [B] or null
     int32_t* status;   // [B] or null (detector index flag)
+    double* prep;      // [B*Td][estep_prep_stride] workspace of the MFMA sweep, or null
+                       // (then the sweep kernel prepares each symbol itself)
 };
 
 struct MstepArgs {
@@ -144,6 +146,7 @@ hipError_t launch_estep_pm(const Problem& pb, const EstepArgs& a, int mode, int 
                            hipStream_t s);
 bool estep_pm_supported(const Problem& pb, int partition_r, int mode);
 bool estep_supported(const Problem& pb, int mode);
+int estep_prep_stride(const Problem& pb);   // doubles per symbol, 0 if no MFMA sweep
 hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s);
 bool chol_supported(const Problem& pb);
@@ -162,6 +165,7 @@ hipError_t launch_sup_shift_mom(const Problem& pb, cd* mom, const cd* xsup, cons
                                 hipStream_t s);
 hipError_t launch_ser(const Problem& pb, const cd* xdest, const cd* xtrue, double* out,
                       hipStream_t s);
+hipError_t estep_debug_mfma(unsigned long long* out, int reset);   // SBCE_ESTEP_COUNT=1
 hipError_t launch_gauss_rank1(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_gauss_expand(const Problem& pb, const cd* theta, cd* out, hipStream_t s);
 hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* out,

@@ -437,7 +437,8 @@ def em_zero_init(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, v
 
 
 # ------------------------------------------------------------------ diagnostic stages
-def _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn, partition_r=0, varx=1.0):
+def _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn, partition_r=0, varx=1.0,
+                 workspace=True):
     def dev(x):
         return _dev(torch, x, np.complex128)
     Yd, Yp, Ps, Up, Cs, Th = (dev(y_d), dev(y_p), dev(psi_d), dev(u_p), dev(cons), dev(theta))
@@ -450,13 +451,17 @@ def _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn, partition_r=0, 
     status = torch.zeros(B, dtype=torch.int32, device="cuda")
     ptrs = _lib.Ptrs(Yd.data_ptr(), Yp.data_ptr() if T_p else Yd.data_ptr(), Ps.data_ptr(),
                      Up.data_ptr() if T_p else Yd.data_ptr(), Cs.data_ptr(), Th.data_ptr(), None,
-                     None, None, None, status.data_ptr(), ws.data_ptr(), ws.numel())
+                     None, None, None, status.data_ptr(), ws.data_ptr() if workspace else None,
+                     ws.numel() if workspace else 0)
     keep = (Yd, Yp, Ps, Up, Cs, Th, ws, status)
     return dims, ptrs, keep
 
 
-def estep_batch(y_d, psi_d, cons, theta, varn, n_tx, mode="soft", partition_r=0, varx=1.0):
-    """One device E-step (sbce_estep): returns m (B,T_d,n_tx), S (B,T_d,n_tx,n_tx)."""
+def estep_batch(y_d, psi_d, cons, theta, varn, n_tx, mode="soft", partition_r=0, varx=1.0,
+                workspace=True):
+    """One device E-step (sbce_estep): returns m (B,T_d,n_tx), S (B,T_d,n_tx,n_tx).
+    workspace=False passes no workspace (the exact sweep then prepares each symbol in
+    its own kernel instead of the separate preparation pass)."""
     torch = _torch()
     lib = _lib.load()
     B, T_d, n_rx = np.shape(y_d)
@@ -464,7 +469,7 @@ def estep_batch(y_d, psi_d, cons, theta, varn, n_tx, mode="soft", partition_r=0,
     y_p = np.zeros((B, 0, n_rx), dtype=complex)
     u_p = np.zeros((B, 0, P * n_tx), dtype=complex)
     dims, ptrs, keep = _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn, partition_r,
-                                    varx)
+                                    varx, workspace)
     mom = torch.zeros((B, T_d, n_tx + n_tx * n_tx), dtype=torch.complex128, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
     _lib.check(lib.sbce_estep(dims, ptrs, _MODES[mode], mom.data_ptr(), stream), "sbce_estep")

@@ -206,19 +206,28 @@ def test_singular_system_flags_and_drop_mode(sbce):
                                    (2, 4, 6, 8, 24, 16, 15), (3, 2, 3, 8, 20, 16, 20),
                                    (4, 3, 4, 16, 12, 4, 10), (2, 1, 5, 8, 10, 64, 30)])
 def test_mfma_and_valu_estep_agree(sbce, shape, monkeypatch):
-    """The FP64-MFMA E-step and the VALU E-step compute the same posterior moments."""
+    """The FP64-MFMA E-step (with its preparation pass, with in-kernel preparation, and
+    with the exact tile bounds disabled) and the VALU E-step compute the same posterior
+    moments; hard decisions are identical."""
     n_tx, n_rx, N, T_p, T_d, M, snr = shape
     varn = float(sbce.signal_model.snr_to_varn(snr))
     b = sbce.signal_model.synthetic_batch(3, n_tx, n_rx, N, T_p, T_d, M, varn, seed=21)
     out = {}
-    for impl in ("mfma", "valu"):
+    for impl, ws, prune in (("mfma", True, "1"), ("mfma", False, "1"), ("mfma", True, "0"),
+                            ("valu", True, "1")):
         monkeypatch.setenv("SBCE_ESTEP_IMPL", impl)
-        out[impl] = [sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx, m)
-                     for m in ("soft", "hard")]
+        monkeypatch.setenv("SBCE_ESTEP_PRUNE", prune)
+        out[(impl, ws, prune)] = [sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"],
+                                                   varn, n_tx, m, workspace=ws)
+                                  for m in ("soft", "hard")]
     scale = np.abs(b["cons"]).max() ** 2
-    for (m1, S1), (m2, S2) in zip(out["mfma"], out["valu"]):
-        assert np.abs(m1 - m2).max() < 1e-11 * scale
-        assert np.abs(S1 - S2).max() < 1e-11 * scale
+    ref = out[("valu", True, "1")]
+    for key, res in out.items():
+        (m1, S1), (mh1, _) = res
+        (m2, S2), (mh2, _) = ref
+        assert np.abs(m1 - m2).max() < 1e-11 * scale, key
+        assert np.abs(S1 - S2).max() < 1e-11 * scale, key
+        assert np.array_equal(mh1, mh2), key
 
 
 def test_snr_sweep_entry_point_reproduces_reference_curve(sbce):
