@@ -92,8 +92,10 @@ extern "C" {
 
 /* per-trial status bits */
 #define SBCE_STATUS_NONHPD 1
-#define SBCE_STATUS_PILOT 2     /* L > 512 path: u_p is not a Kronecker product
-                                   psi_p (x) x_p (PM.py:119-130); R's pilot term invalid */
+#define SBCE_STATUS_PILOT 2     /* n_tx in {4, 8}: u_p is not a Kronecker product
+                                   psi_p (x) x_p (PM.py:119-130), so the MFMA build's
+                                   factored pilot term does not apply; R of the trial is
+                                   rebuilt by the general (VALU) path (informational) */
 #define SBCE_STATUS_DETECTOR 4  /* ZF/MMSE: the reference's flattened argmin indexed past
                                    all_possibleSymbols (IndexError at
                                    all_detectorsvsTd.py:52); row flat mod M^n_tx used */

@@ -16,7 +16,7 @@ constexpr size_t kAlign = 256;
 size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 struct Carve {
-    size_t mom, R, rhs, done, ysh, prep, tol, winv, ppsi, pS, total;
+    size_t mom, R, rhs, done, ysh, prep, tol, winv, ppsi, pS, pflag, total;
     bool has_prep;
 };
 
@@ -46,13 +46,18 @@ Carve carve(const Problem& pb) {
     const int ps = estep_prep_stride(pb);
     c.has_prep = ps > 0;
     c.tol = align_up(c.prep + (size_t)pb.B * pb.Td * ps * sizeof(double));
-    c.winv = c.ppsi = c.pS = c.tol;
+    c.ppsi = c.pS = c.pflag = c.winv = c.tol;
     c.total = c.tol;
-    if (pb.L > kLargeL) {                    // tiled large-L M-step (mstep_large.hip)
-        c.winv = align_up(c.tol + (size_t)pb.B * sizeof(double));
-        c.ppsi = align_up(c.winv + (size_t)pb.B * 64 * 64 * sizeof(cd));
+    if (rbuild_herm_supported(pb)) {         // MFMA R build: Kronecker-factored pilots
+        c.ppsi = c.total;
         c.pS = align_up(c.ppsi + (size_t)pb.B * pb.Tp * pb.P * sizeof(cd));
-        c.total = align_up(c.pS + (size_t)pb.B * pb.Tp * pb.NT * pb.NT * sizeof(cd));
+        c.pflag = align_up(c.pS + (size_t)pb.B * pb.Tp * pb.NT * pb.NT * sizeof(cd));
+        c.total = align_up(c.pflag + (size_t)pb.B * sizeof(int32_t));
+    }
+    if (pb.L > kLargeL) {                    // tiled large-L M-step (mstep_large.hip)
+        c.tol = c.total;
+        c.winv = align_up(c.tol + (size_t)pb.B * sizeof(double));
+        c.total = align_up(c.winv + (size_t)pb.B * 64 * 64 * sizeof(cd));
     }
     return c;
 }
@@ -64,6 +69,8 @@ void set_large(MstepArgs& ma, char* ws, const Carve& c) {
     ma.winv = (cd*)(ws + c.winv);
     ma.ppsi = (cd*)(ws + c.ppsi);
     ma.pS = (cd*)(ws + c.pS);
+    ma.pflag = (int32_t*)(ws + c.pflag);
+    ma.gate = nullptr;
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }

@@ -23,7 +23,7 @@ template <int NT>
 __global__ __launch_bounds__(256) void rbuild_kernel(MstepArgs a, int B, int P, int Tp, int Td,
                                                      int L) {
     const int b = blockIdx.y;
-    if (a.done && a.done[b]) return;
+    if ((a.done && a.done[b]) || (a.gate && !a.gate[b])) return;
     const int npairs = P * (P + 1) / 2;
     const int pi = blockIdx.x * blockDim.x + threadIdx.x;
     if (pi >= npairs) return;
@@ -75,7 +75,7 @@ template <int NT>
 __global__ __launch_bounds__(256) void rbuild_wide_kernel(MstepArgs a, int B, int P, int Tp,
                                                           int Td, int L) {
     const int b = blockIdx.y;
-    if (a.done && a.done[b]) return;
+    if ((a.done && a.done[b]) || (a.gate && !a.gate[b])) return;
     const int npairs = P * (P + 1) / 2;
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     const int pi = gid / NT, i = gid - pi * NT;
@@ -367,17 +367,20 @@ __global__ __launch_bounds__(256) void early_stop_kernel(const cd* theta, const 
 
 }  // namespace
 
-hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t s) {
+hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a0, hipStream_t s) {
     const int npairs = pb.P * (pb.P + 1) / 2;
-    const bool tiles = pb.L > kLargeL && rbuild_tile_supported(pb);
-    if (tiles) {
+    MstepArgs a = a0;
+    // NT in {4, 8}: MFMA build from Kronecker-factored pilots (mstep_large.hip), then the
+    // VALU build below re-runs only the trials whose u_p is not a Kronecker product
+    const bool herm = rbuild_herm_supported(pb);
+    if (herm) {
         hipError_t e0 = launch_pilot_factor(pb, a, s);
-        if (e0 == hipSuccess) e0 = launch_rbuild_tiles(pb, a, s);
+        if (e0 == hipSuccess) e0 = launch_rbuild_herm(pb, a, s);
         if (e0 != hipSuccess) return e0;
+        a.gate = a.pflag;
     }
     dim3 g1((npairs + 255) / 256, pb.B);
-    switch (tiles ? 0 : pb.NT) {
-        case 0: break;
+    switch (pb.NT) {
         case 1: hipLaunchKernelGGL(rbuild_kernel<1>, g1, dim3(256), 0, s, a, pb.B, pb.P, pb.Tp, pb.Td, pb.L); break;
         case 2: hipLaunchKernelGGL(rbuild_kernel<2>, g1, dim3(256), 0, s, a, pb.B, pb.P, pb.Tp, pb.Td, pb.L); break;
         case 3: hipLaunchKernelGGL(rbuild_kernel<3>, g1, dim3(256), 0, s, a, pb.B, pb.P, pb.Tp, pb.Td, pb.L); break;

@@ -73,118 +73,195 @@ __global__ __launch_bounds__(64) void pilot_factor_kernel(MstepArgs a, int P, in
         res = fmax(res, cabs2(csub(u[l], v)));
     }
     for (int off = 32; off >= 1; off >>= 1) res = fmax(res, __shfl_xor(res, off));
-    if (lane == 0 && a.status && res > 1e-20 * den) atomicOr(&a.status[b], SBCE_STATUS_PILOT);
+    if (lane == 0 && res > 1e-20 * den) {
+        atomicOr(&a.pflag[b], 1);
+        if (a.status) atomicOr(&a.status[b], SBCE_STATUS_PILOT);
+    }
 }
 
 // ---------------------------------------------------------------- R build (MFMA)
-// Block = 64 x 64 tile (ti >= tj) of R for one trial: pairs p in [ti PB, ti PB + PB),
-// q in [tj PB, ..), PB = 64 / NT.  4 waves; wave w owns TP pair tiles x TA ab tiles of the
-// 16 x 16 MFMA grid (NT = 8: 1 x 4, NT = 4: 4 x 1).  Per 4 symbols: TP operands
-// psi_p conj(psi_q) (A), TA operands S_t[ab] (B), 16 chained MFMAs.
+// R[(p,i),(q,j)] = sum_t psi_t[p] conj(psi_t[q]) S_t[i][j] over the pairs p >= q, with
+// S_t Hermitian.  Writing w = psi_p conj(psi_q) = wr + i wi and S_ij = Sr + i Si (i < j):
+//   R[(p,i),(q,j)] = (sum wr Sr - sum wi Si) + i (sum wr Si + sum wi Sr)
+//   R[(p,j),(q,i)] = (sum wr Sr + sum wi Si) + i (sum wi Sr - sum wr Si)
+//   R[(p,i),(q,i)] = sum wr S_ii + i sum wi S_ii
+// so the whole build is two REAL GEMMs over t, [wr | wi] (pairs x T) times the NT^2 real
+// columns of the Hermitian S (NT diagonal + NT(NT-1)/2 real + as many imaginary parts):
+// half the MFMAs of the complex product of the full S.  Column tiles of 16: item c < 8
+// of a tile is an off-diagonal (i,j) (column c = Re S_ij, c + 8 = Im S_ij) or a pair of
+// diagonals (d0, d1) (column c = S_d0d0, c + 8 = S_d1d1); the epilogue combines columns
+// c and c + 8 with one lane exchange.
+//
+// Block = 4 waves x TPW pair tiles of 16 consecutive pairs (p-major order, p >= q); the
+// phases psi_t of the p and q the block needs (at most min(P, pairs + 1) values, in two
+// index segments) and the real S columns are staged per TC-symbol chunk in LDS; per 4
+// symbols a lane forms w for (its pair, its symbol) once and feeds 2 NT^2/16 MFMAs.
+// Blocks of one trial are placed on one XCD (blockIdx % 8) so psi / S are L2 hits.
 template <int NT>
-__global__ __launch_bounds__(256) void rbuild_tile_kernel(MstepArgs a, int P, int Tp, int Td,
-                                                          int L, int ntr) {
-    constexpr int PB = TB / NT;                 // p (and q) values per tile side
-    constexpr int NAB = NT * NT;
-    constexpr int TA = NAB / 16;                // ab tiles per wave
-    constexpr int TP = 4 / TA;                  // pair tiles per wave
-    constexpr int TC = 16;                      // symbols per LDS chunk
+__device__ __forceinline__ void herm_item(int item, int& i, int& j, bool& diag) {
+    constexpr int NOFF = NT * (NT - 1) / 2;
+    if (item >= NOFF) {
+        diag = true;
+        i = 2 * (item - NOFF);
+        j = i + 1;
+        return;
+    }
+    diag = false;
+    int o = item;
+    i = 0;
+#pragma unroll
+    for (int r = 0; r < NT - 1; ++r) {
+        const int cnt = NT - 1 - r;
+        if (o >= cnt && i == r) { o -= cnt; i = r + 1; }
+    }
+    j = i + 1 + o;
+}
+
+__device__ __forceinline__ void pair_of(int pi, int& p, int& q) {
+    int x = (int)((sqrt(8.0 * pi + 1.0) - 1.0) * 0.5);
+    while ((x + 1) * (x + 2) / 2 <= pi) ++x;
+    while (x * (x + 1) / 2 > pi) --x;
+    p = x;
+    q = pi - x * (x + 1) / 2;
+}
+
+template <int NT, int TPW, int TC>
+__global__ __launch_bounds__(256) void rbuild_herm_kernel(MstepArgs a, int B, int P, int Tp,
+                                                          int Td, int L, int G, int smax) {
+    constexpr int NC = NT * NT;                 // real columns of the Hermitian S
+    constexpr int NCT = NC / 16;                // 16-column MFMA tiles
+    constexpr int PPB = 4 * TPW * 16;           // pairs per block
     constexpr int MS = NT + NT * NT;
-    static_assert(NAB % 16 == 0 && TP * TA == 4, "rbuild_tile: NT in {4, 8}");
-    __shared__ cd s_pp[TC][PB], s_pq[TC][PB];
-    __shared__ cd s_S[TC][NAB];
-    const int b = blockIdx.y;
+    static_assert(NC % 16 == 0, "rbuild_herm: NT in {4, 8}");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cd* s_psi = reinterpret_cast<cd*>(smem);                    // [TC][smax]
+    double* s_S = reinterpret_cast<double*>(s_psi + TC * smax); // [TC][NC]
+
+    const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
+    const int b = (slot / G) * 8 + xcd, g = slot - (slot / G) * G;
+    if (b >= B) return;
     if (a.done && a.done[b]) return;
-    // lower-triangular tile index -> (ti, tj)
-    const int tix = blockIdx.x;
-    int ti = (int)((sqrt(8.0 * tix + 1.0) - 1.0) * 0.5);
-    while ((ti + 1) * (ti + 2) / 2 <= tix) ++ti;
-    while (ti * (ti + 1) / 2 > tix) --ti;
-    const int tj = tix - ti * (ti + 1) / 2;
-    const int p0 = ti * PB, q0 = tj * PB;
+    const int npairs = P * (P + 1) / 2;
+    const int pi0 = g * PPB;
+    if (pi0 >= npairs) return;
+    const int pi1 = min(pi0 + PPB, npairs) - 1;
+    int pa, qa, pb, qb;
+    pair_of(pi0, pa, qa);
+    pair_of(pi1, pb, qb);
+    // staged index segments: [lo1, hi1] then [lo2, hi2] (possibly empty)
+    //   one row:   q in [qa, qb], p = pb                      -> [qa, qb] + [pb, pb]
+    //   two rows, disjoint q ranges [qa, pa] and [0, qb]      -> [0, qb] + [qa, pb]
+    //   otherwise (rows in between are shorter than a block)  -> [0, pb]
+    // so at most (pairs of the block) + 1 <= smax values
+    int lo1 = 0, hi1 = pb, lo2 = pb + 1, hi2 = pb;
+    if (pa == pb) {
+        lo1 = qa; hi1 = qb;
+        if (pb > qb) lo2 = pb;
+    } else if (pb == pa + 1 && qa > qb + 1) {
+        hi1 = qb; lo2 = qa;
+    }
+    const int n1 = hi1 - lo1 + 1;
+    const int cnt = n1 + (hi2 - lo2 + 1);
+
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
-
-    d4v cre[TP][TA], cim[TP][TA];
+    int sp[TPW], sq[TPW];
+    bool ok[TPW];
 #pragma unroll
-    for (int u = 0; u < TP; ++u)
-#pragma unroll
-        for (int v = 0; v < TA; ++v) {
-            cre[u][v] = d4v{0.0, 0.0, 0.0, 0.0};
-            cim[u][v] = d4v{0.0, 0.0, 0.0, 0.0};
-        }
-    // pair of A-operand row i in pair tile u of this wave: pair index (wave*TP + u)*16 + i
-    int pp[TP], pq[TP];
-#pragma unroll
-    for (int u = 0; u < TP; ++u) {
-        const int pi = (wave * TP + u) * 16 + li;
-        pp[u] = pi / PB;
-        pq[u] = pi - pp[u] * PB;
+    for (int u = 0; u < TPW; ++u) {
+        const int pi = pi0 + (wave * TPW + u) * 16 + li;
+        ok[u] = pi <= pi1;
+        int p = pa, q = qa;
+        if (ok[u]) pair_of(pi, p, q);
+        sp[u] = p <= hi1 ? p - lo1 : n1 + p - lo2;
+        sq[u] = q <= hi1 ? q - lo1 : n1 + q - lo2;
     }
+    d4v cr[TPW][NCT], ci[TPW][NCT];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u)
+#pragma unroll
+        for (int v = 0; v < NCT; ++v) {
+            cr[u][v] = d4v{0.0, 0.0, 0.0, 0.0};
+            ci[u][v] = d4v{0.0, 0.0, 0.0, 0.0};
+        }
     const cd* psd = a.psid + (size_t)b * Td * P;
     const cd* mom = a.mom + (size_t)b * Td * MS;
     const cd* psp = a.ppsi + (size_t)b * Tp * P;
-    const cd* pS = a.pS + (size_t)b * Tp * NAB;
+    const cd* pS = a.pS + (size_t)b * Tp * NT * NT;
     const int T = Td + Tp;
     for (int t0 = 0; t0 < T; t0 += TC) {
         __syncthreads();
-        for (int e = tid; e < TC * PB; e += 256) {
-            const int tt = e / PB, k = e - tt * PB, t = t0 + tt;
-            cd vp = czero(), vq = czero();
-            if (t < Td) {
-                if (p0 + k < P) vp = psd[(size_t)t * P + p0 + k];
-                if (q0 + k < P) vq = psd[(size_t)t * P + q0 + k];
-            } else if (t < T) {
-                if (p0 + k < P) vp = psp[(size_t)(t - Td) * P + p0 + k];
-                if (q0 + k < P) vq = psp[(size_t)(t - Td) * P + q0 + k];
-            }
-            s_pp[tt][k] = vp;
-            s_pq[tt][k] = vq;
-        }
-        for (int e = tid; e < TC * NAB; e += 256) {
-            const int tt = e / NAB, k = e - tt * NAB, t = t0 + tt;
+        for (int e = tid; e < TC * cnt; e += 256) {
+            const int tt = e / cnt, k = e - tt * cnt, t = t0 + tt;
+            const int x = k < n1 ? lo1 + k : lo2 + (k - n1);
             cd v = czero();
-            if (t < Td) v = mom[(size_t)t * MS + NT + k];
-            else if (t < T) v = pS[(size_t)(t - Td) * NAB + k];
-            s_S[tt][k] = v;
+            if (t < Td) v = psd[(size_t)t * P + x];
+            else if (t < T) v = psp[(size_t)(t - Td) * P + x];
+            s_psi[tt * smax + k] = v;
+        }
+        for (int e = tid; e < TC * NC; e += 256) {
+            const int tt = e / NC, c = e - tt * NC, t = t0 + tt;
+            const int cc = c & 15, item = (c >> 4) * 8 + (cc & 7), comp = cc >> 3;
+            int i, j;
+            bool dg;
+            herm_item<NT>(item, i, j, dg);
+            const cd* St = t < Td ? mom + (size_t)t * MS + NT : pS + (size_t)(t - Td) * NT * NT;
+            double v = 0.0;
+            if (t < T) {
+                if (dg) v = St[(comp ? j : i) * (NT + 1)].x;
+                else v = comp ? St[i * NT + j].y : St[i * NT + j].x;
+            }
+            s_S[tt * NC + c] = v;
         }
         __syncthreads();
 #pragma unroll
-        for (int s = 0; s < TC / 4; ++s) {
-            const int tt = 4 * s + lk;
-            cd av[TP], bv[TA];
+        for (int s4 = 0; s4 < TC / 4; ++s4) {
+            const int tt = 4 * s4 + lk;
+            double bv[NCT];
 #pragma unroll
-            for (int u = 0; u < TP; ++u) av[u] = cmulc(s_pp[tt][pp[u]], s_pq[tt][pq[u]]);
+            for (int v = 0; v < NCT; ++v) bv[v] = s_S[tt * NC + 16 * v + li];
 #pragma unroll
-            for (int v = 0; v < TA; ++v) bv[v] = s_S[tt][16 * v + li];
+            for (int u = 0; u < TPW; ++u) {
+                const cd w = cmulc(s_psi[tt * smax + sp[u]], s_psi[tt * smax + sq[u]]);
+                const double wr = ok[u] ? w.x : 0.0, wi = ok[u] ? w.y : 0.0;
 #pragma unroll
-            for (int u = 0; u < TP; ++u)
-#pragma unroll
-                for (int v = 0; v < TA; ++v) {
-                    // C += A B (complex): re += ar br - ai bi ; im += ar bi + ai br
-                    cre[u][v] = mfma4(av[u].x, bv[v].x, cre[u][v]);
-                    cre[u][v] = mfma4(-av[u].y, bv[v].y, cre[u][v]);
-                    cim[u][v] = mfma4(av[u].x, bv[v].y, cim[u][v]);
-                    cim[u][v] = mfma4(av[u].y, bv[v].x, cim[u][v]);
+                for (int v = 0; v < NCT; ++v) {
+                    cr[u][v] = mfma4(wr, bv[v], cr[u][v]);
+                    ci[u][v] = mfma4(wi, bv[v], ci[u][v]);
                 }
+            }
         }
     }
-    // write: C row = pair (lk + 4q) of the pair tile, column = ab (li) of the ab tile
+    // epilogue: lane holds pairs lk + 4 q4 of each tile, column li
     cd* R = a.R + (size_t)b * L * L;
+    const int comp = li >> 3;
 #pragma unroll
-    for (int u = 0; u < TP; ++u)
+    for (int v = 0; v < NCT; ++v) {
+        int i, j;
+        bool dg;
+        herm_item<NT>(v * 8 + (li & 7), i, j, dg);
+        const int ri = dg ? (comp ? j : i) : (comp ? j : i);
+        const int cj = dg ? (comp ? j : i) : (comp ? i : j);
 #pragma unroll
-        for (int v = 0; v < TA; ++v)
+        for (int u = 0; u < TPW; ++u)
 #pragma unroll
             for (int q4 = 0; q4 < 4; ++q4) {
-                const int pi = (wave * TP + u) * 16 + lk + 4 * q4;
-                const int p = p0 + pi / PB, q = q0 + pi % PB;
-                const int ab = 16 * v + li, ai = ab / NT, bi = ab - ai * NT;
-                if (p < P && q < P)
-                    R[(size_t)(p * NT + ai) * L + q * NT + bi] = cmk(cre[u][v][q4], cim[u][v][q4]);
+                const double orr = cr[u][v][q4], oi = ci[u][v][q4];
+                const double pr = __shfl_xor(orr, 8), pim = __shfl_xor(oi, 8);
+                double re = orr, im = oi;
+                if (!dg) {
+                    re = comp ? pr + oi : orr - pim;
+                    im = comp ? pim - orr : oi + pr;
+                }
+                const int pi = pi0 + (wave * TPW + u) * 16 + lk + 4 * q4;
+                if (pi <= pi1) {
+                    int p, q;
+                    pair_of(pi, p, q);
+                    R[(size_t)(p * NT + ri) * L + q * NT + cj] = cmk(re, im);
+                }
             }
-    (void)ntr;
+    }
 }
 
 // ---------------------------------------------------------------- tolerance
@@ -435,27 +512,41 @@ __global__ __launch_bounds__(256) void trisolve_kernel(MstepArgs a, int L, int N
 
 }  // namespace
 
-bool rbuild_tile_supported(const Problem& pb) { return pb.NT == 4 || pb.NT == 8; }
+bool rbuild_herm_supported(const Problem& pb) { return pb.NT == 4 || pb.NT == 8; }
 
 hipError_t launch_pilot_factor(const Problem& pb, const MstepArgs& a, hipStream_t s) {
+    if (hipMemsetAsync(a.pflag, 0, (size_t)pb.B * sizeof(int32_t), s) != hipSuccess)
+        return hipErrorInvalidValue;
     if (pb.Tp == 0 || pb.B == 0) return hipSuccess;
     hipLaunchKernelGGL(pilot_factor_kernel, dim3(pb.Tp, pb.B), dim3(64), 0, s, a, pb.P, pb.NT,
                        pb.Tp, pb.L);
     return hipGetLastError();
 }
 
-hipError_t launch_rbuild_tiles(const Problem& pb, const MstepArgs& a, hipStream_t s) {
-    const int ntr = (pb.L + TB - 1) / TB;
-    const dim3 g(ntr * (ntr + 1) / 2, pb.B);
-    if (pb.NT == 8)
-        hipLaunchKernelGGL(rbuild_tile_kernel<8>, g, dim3(256), 0, s, a, pb.P, pb.Tp, pb.Td, pb.L,
-                           ntr);
-    else if (pb.NT == 4)
-        hipLaunchKernelGGL(rbuild_tile_kernel<4>, g, dim3(256), 0, s, a, pb.P, pb.Tp, pb.Td, pb.L,
-                           ntr);
-    else
-        return hipErrorInvalidValue;
+template <int NT, int TPW, int TC>
+static hipError_t launch_herm(const Problem& pb, const MstepArgs& a, int smax, hipStream_t s) {
+    constexpr int PPB = 4 * TPW * 16;
+    const int npairs = pb.P * (pb.P + 1) / 2;
+    const int G = (npairs + PPB - 1) / PPB;
+    const long nblk = 8L * ((pb.B + 7) / 8) * G;
+    const size_t lds = (size_t)TC * smax * sizeof(cd) + (size_t)TC * NT * NT * sizeof(double);
+    if (nblk > 0x7fffffffL || lds > 160 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((rbuild_herm_kernel<NT, TPW, TC>), dim3((unsigned)nblk), dim3(256), lds, s, a,
+                       pb.B, pb.P, pb.Tp, pb.Td, pb.L, G, smax);
     return hipGetLastError();
+}
+
+hipError_t launch_rbuild_herm(const Problem& pb, const MstepArgs& a, hipStream_t s) {
+    // staged phases per block <= min(P, pairs per block + 1) (two p-major index segments)
+    if (pb.NT == 4) {
+        const int smax = pb.P < 257 ? pb.P : 257;
+        return smax <= 130 ? launch_herm<4, 4, 16>(pb, a, smax, s) : launch_herm<4, 4, 8>(pb, a, smax, s);
+    }
+    if (pb.NT == 8) {
+        const int smax = pb.P < 65 ? pb.P : 65;
+        return launch_herm<8, 1, 16>(pb, a, smax, s);
+    }
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_chol_large(const Problem& pb, const MstepArgs& a, hipStream_t s) {

@@ -134,11 +134,14 @@ struct MstepArgs {
     int32_t* status;   // [B] or null
     const int32_t* done;
     int solve_mode;
+    // MFMA R build (NT in {4, 8}) workspace
+    cd* ppsi;          // [B][Tp][P]  pilot phases psi' (Kronecker factor of u_p)
+    cd* pS;            // [B][Tp][NT*NT] pilot x' x'^H
+    int32_t* pflag;    // [B] u_p of the trial is not a Kronecker product (set by pilot_factor)
+    const int32_t* gate;  // VALU build: only trials with gate[b] != 0 (null: all trials)
     // large-L path (L > 512) workspace
     double* tol;       // [B]     pivot threshold
     cd* winv;          // [B][64][64] inverse of the current diagonal tile
-    cd* ppsi;          // [B][Tp][P]  pilot phases psi' (Kronecker factor of u_p)
-    cd* pS;            // [B][Tp][NT*NT] pilot x' x'^H
 };
 
 hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStream_t s);
@@ -151,9 +154,9 @@ hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t
 hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s);
 bool chol_supported(const Problem& pb);
 constexpr int kLargeL = 512;   // L above this: tiled build + blocked right-looking Cholesky
-bool rbuild_tile_supported(const Problem& pb);
+bool rbuild_herm_supported(const Problem& pb);   // MFMA build of the Hermitian R: NT in {4, 8}
 hipError_t launch_pilot_factor(const Problem& pb, const MstepArgs& a, hipStream_t s);
-hipError_t launch_rbuild_tiles(const Problem& pb, const MstepArgs& a, hipStream_t s);
+hipError_t launch_rbuild_herm(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_chol_large(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w, hipStream_t s);
 hipError_t chol_debug_clock(unsigned long long* out);   // diagnostic (SBCE_CHOL_SKIP & 64)

@@ -498,7 +498,11 @@ def mstep_batch(y_d, y_p, psi_d, u_p, cons, m, S, varn, solve="chol"):
                               rhs.data_ptr(), stream), "sbce_mstep")
     torch.cuda.current_stream().synchronize()
     th = keep[5].cpu().numpy()
-    return th, R.cpu().numpy(), rhs.cpu().numpy(), keep[7].cpu().numpy()
+    # the device keeps only R's lower triangle (its strict upper part is factorisation
+    # workspace): return the Hermitian completion
+    R = np.tril(R.cpu().numpy())
+    R = R + np.conj(np.swapaxes(np.tril(R, -1), 1, 2))
+    return th, R, rhs.cpu().numpy(), keep[7].cpu().numpy()
 
 
 def nmse_batch(theta, h):

@@ -410,6 +410,25 @@ def test_large_l_pilot_not_kronecker_is_flagged(sbce):
     assert st[0] & sbce._lib.SBCE_STATUS_PILOT
 
 
+@pytest.mark.parametrize("shape", [(4, 2, 20, 8, 60), (8, 3, 9, 6, 40)])
+def test_mstep_pilot_not_kronecker_falls_back_exactly(sbce, shape):
+    """n_tx in {4, 8} builds R by MFMA from Kronecker-factored pilots; a trial whose u_p
+    is not psi (x) x is flagged and rebuilt by the VALU path, so R stays exact."""
+    n_tx, n_rx, N, T_p, T_d = shape
+    b = sbce.signal_model.synthetic_batch(3, n_tx, n_rx, N, T_p, T_d, 4, 0.05, seed=6)
+    rng = np.random.default_rng(1)
+    u_p = b["u_p"].copy()
+    u_p[1] += 0.1 * (rng.standard_normal(u_p[1].shape) + 1j * rng.standard_normal(u_p[1].shape))
+    x = b["x_d"]
+    S = x[..., :, None] * np.conj(x[..., None, :]) + 0.1 * np.eye(n_tx)
+    _, R, rhs, st = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], u_p, b["cons"], x, S, 0.05)
+    assert [bool(v & sbce._lib.SBCE_STATUS_PILOT) for v in st] == [False, True, False]
+    for i in range(3):
+        R0, rhs0 = mstep_build(u_p[i], b["y_p"][i], b["psi_d"][i].T, b["y_d"][i], x[i], S[i])
+        assert rel(R[i], R0) < 1e-13
+        assert rel(rhs[i], rhs0) < 1e-13
+
+
 def test_large_l_full_em_pm_soft_vs_oracle(sbce):
     """BASELINE cfg 2 estimator (n_tx = n_rx = 8, 16-QAM, PM_beta r = 1) at L = 648: the
     whole device EM (PM E-step + tiled M-step) vs the oracle."""
