@@ -134,8 +134,8 @@ __global__ __launch_bounds__(256) void rbuild_herm_kernel(MstepArgs a, int B, in
     constexpr int MS = NT + NT * NT;
     static_assert(NC % 16 == 0, "rbuild_herm: NT in {4, 8}");
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    cd* s_psi = reinterpret_cast<cd*>(smem);                    // [TC][smax]
-    double* s_S = reinterpret_cast<double*>(s_psi + TC * smax); // [TC][NC]
+    cd* s_psi = reinterpret_cast<cd*>(smem);                    // [TC][cnt] + 64 pad
+    double* s_S = reinterpret_cast<double*>(s_psi + TC * smax + 64);   // [TC][NC]
 
     const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
     const int b = (slot / G) * 8 + xcd, g = slot - (slot / G) * G;
@@ -166,16 +166,30 @@ __global__ __launch_bounds__(256) void rbuild_herm_kernel(MstepArgs a, int B, in
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
+    // A-operand rows of pairs past the block's last pair are computed from a valid pair and
+    // never stored (rows of the product are independent)
     int sp[TPW], sq[TPW];
-    bool ok[TPW];
 #pragma unroll
     for (int u = 0; u < TPW; ++u) {
-        const int pi = pi0 + (wave * TPW + u) * 16 + li;
-        ok[u] = pi <= pi1;
-        int p = pa, q = qa;
-        if (ok[u]) pair_of(pi, p, q);
-        sp[u] = p <= hi1 ? p - lo1 : n1 + p - lo2;
-        sq[u] = q <= hi1 ? q - lo1 : n1 + q - lo2;
+        const int pi = min(pi0 + (wave * TPW + u) * 16 + li, pi1);
+        int p, q;
+        pair_of(pi, p, q);
+        sp[u] = (p <= hi1 ? p - lo1 : n1 + p - lo2) * (int)sizeof(cd);
+        sq[u] = (q <= hi1 ? q - lo1 : n1 + q - lo2) * (int)sizeof(cd);
+    }
+    // S staging: thread -> fixed (symbol-in-chunk, column) slots; its source offset in S_t
+    constexpr int SR = (TC * NC + 255) / 256;
+    int soff[SR];
+    bool sdiagim[SR];
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+        const int c = (tid + 256 * r) % NC;
+        const int cc = c & 15, item = (c >> 4) * 8 + (cc & 7), comp = cc >> 3;
+        int i, j;
+        bool dg;
+        herm_item<NT>(item, i, j, dg);
+        soff[r] = dg ? (comp ? j : i) * (NT + 1) : i * NT + j;
+        sdiagim[r] = !dg && comp;                 // imaginary part of an off-diagonal
     }
     d4v cr[TPW][NCT], ci[TPW][NCT];
 #pragma unroll
@@ -190,45 +204,63 @@ __global__ __launch_bounds__(256) void rbuild_herm_kernel(MstepArgs a, int B, in
     const cd* psp = a.ppsi + (size_t)b * Tp * P;
     const cd* pS = a.pS + (size_t)b * Tp * NT * NT;
     const int T = Td + Tp;
+    const char* s_psib = reinterpret_cast<const char*>(s_psi);
+    const float rcnt = 1.0f / (float)cnt;
+    const int ne = TC * cnt;
     for (int t0 = 0; t0 < T; t0 += TC) {
         __syncthreads();
-        for (int e = tid; e < TC * cnt; e += 256) {
-            const int tt = e / cnt, k = e - tt * cnt, t = t0 + tt;
+        // phases: LDS image linear in e = tt cnt + k, filled by LDS-DMA (global_load_lds,
+        // lane-linear destination, per-lane source): every load of the chunk in flight at
+        // once instead of a chain of L2 round trips; lanes past the image end land in the
+        // 64-entry pad, symbols past T read a valid dummy (their S columns are 0)
+        for (int e0 = wave * 64; e0 < ne; e0 += 256) {
+            const int e = e0 + lane;
+            int tt = (int)((float)e * rcnt);
+            int k = e - tt * cnt;
+            if (k < 0) { --tt; k += cnt; }
+            if (k >= cnt) { ++tt; k -= cnt; }
             const int x = k < n1 ? lo1 + k : lo2 + (k - n1);
-            cd v = czero();
-            if (t < Td) v = psd[(size_t)t * P + x];
-            else if (t < T) v = psp[(size_t)(t - Td) * P + x];
-            s_psi[tt * smax + k] = v;
+            const int t = t0 + tt;
+            const cd* src = psd;
+            if (e < ne && t < Td) src = psd + (size_t)t * P + x;
+            else if (e < ne && t < T) src = psp + (size_t)(t - Td) * P + x;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)(s_psi + e0),
+                                             16, 0, 0);
         }
-        for (int e = tid; e < TC * NC; e += 256) {
-            const int tt = e / NC, c = e - tt * NC, t = t0 + tt;
-            const int cc = c & 15, item = (c >> 4) * 8 + (cc & 7), comp = cc >> 3;
-            int i, j;
-            bool dg;
-            herm_item<NT>(item, i, j, dg);
-            const cd* St = t < Td ? mom + (size_t)t * MS + NT : pS + (size_t)(t - Td) * NT * NT;
-            double v = 0.0;
-            if (t < T) {
-                if (dg) v = St[(comp ? j : i) * (NT + 1)].x;
-                else v = comp ? St[i * NT + j].y : St[i * NT + j].x;
+#pragma unroll
+        for (int r = 0; r < SR; ++r) {
+            const int e = tid + 256 * r;
+            if (SR * 256 == TC * NC || e < TC * NC) {
+                const int tt = e / NC, t = t0 + tt;
+                double v = 0.0;
+                if (t < Td) {
+                    const cd z = mom[(size_t)t * MS + NT + soff[r]];
+                    v = sdiagim[r] ? z.y : z.x;
+                } else if (t < T) {
+                    const cd z = pS[(size_t)(t - Td) * NT * NT + soff[r]];
+                    v = sdiagim[r] ? z.y : z.x;
+                }
+                s_S[e] = v;
             }
-            s_S[tt * NC + c] = v;
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
 #pragma unroll
         for (int s4 = 0; s4 < TC / 4; ++s4) {
             const int tt = 4 * s4 + lk;
+            const char* row = s_psib + tt * cnt * (int)sizeof(cd);
             double bv[NCT];
 #pragma unroll
             for (int v = 0; v < NCT; ++v) bv[v] = s_S[tt * NC + 16 * v + li];
 #pragma unroll
             for (int u = 0; u < TPW; ++u) {
-                const cd w = cmulc(s_psi[tt * smax + sp[u]], s_psi[tt * smax + sq[u]]);
-                const double wr = ok[u] ? w.x : 0.0, wi = ok[u] ? w.y : 0.0;
+                const cd w = cmulc(*reinterpret_cast<const cd*>(row + sp[u]),
+                                   *reinterpret_cast<const cd*>(row + sq[u]));
 #pragma unroll
                 for (int v = 0; v < NCT; ++v) {
-                    cr[u][v] = mfma4(wr, bv[v], cr[u][v]);
-                    ci[u][v] = mfma4(wi, bv[v], ci[u][v]);
+                    cr[u][v] = mfma4(w.x, bv[v], cr[u][v]);
+                    ci[u][v] = mfma4(w.y, bv[v], ci[u][v]);
                 }
             }
         }
@@ -529,7 +561,7 @@ static hipError_t launch_herm(const Problem& pb, const MstepArgs& a, int smax, h
     const int npairs = pb.P * (pb.P + 1) / 2;
     const int G = (npairs + PPB - 1) / PPB;
     const long nblk = 8L * ((pb.B + 7) / 8) * G;
-    const size_t lds = (size_t)TC * smax * sizeof(cd) + (size_t)TC * NT * NT * sizeof(double);
+    const size_t lds = (size_t)(TC * smax + 64) * sizeof(cd) + (size_t)TC * NT * NT * sizeof(double);
     if (nblk > 0x7fffffffL || lds > 160 * 1024) return hipErrorInvalidValue;
     hipLaunchKernelGGL((rbuild_herm_kernel<NT, TPW, TC>), dim3((unsigned)nblk), dim3(256), lds, s, a,
                        pb.B, pb.P, pb.Tp, pb.Td, pb.L, G, smax);
@@ -540,7 +572,7 @@ hipError_t launch_rbuild_herm(const Problem& pb, const MstepArgs& a, hipStream_t
     // staged phases per block <= min(P, pairs per block + 1) (two p-major index segments)
     if (pb.NT == 4) {
         const int smax = pb.P < 257 ? pb.P : 257;
-        return smax <= 130 ? launch_herm<4, 4, 16>(pb, a, smax, s) : launch_herm<4, 4, 8>(pb, a, smax, s);
+        return smax <= 130 ? launch_herm<4, 4, 32>(pb, a, smax, s) : launch_herm<4, 4, 8>(pb, a, smax, s);
     }
     if (pb.NT == 8) {
         const int smax = pb.P < 65 ? pb.P : 65;
