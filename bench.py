@@ -17,7 +17,8 @@ after the timed region, as in the reference's Monte-Carlo average
 
 Also reported (one JSON line on rank 0):
   roofline      the dominant phase (E-step or M-step, whichever is longer per
-                EM iteration) timed live with HIP events on the launch stream;
+                EM iteration; "kernels" lists the launches it consists of) timed live
+                with HIP events on the launch stream;
                 M-step: algorithmic flops per launch; E-step: the
                 FP64 MFMAs it issued (device counter; its exact bounds skip
                 provably negligible hypothesis tiles), with the full-enumeration
@@ -55,6 +56,15 @@ CONFIGS = {
 # (lstsq-like, PM.py:108) solve; cfg 4 is a throughput-only workload.
 ESTEP = {"cfg1": ("soft", 0, "chol"), "plumbing": ("soft", 0, "chol"),
          "cfg2": ("pm_soft", 1, "drop"), "cfg4": ("soft", 0, "drop")}
+
+
+# kernels of one E-step / M-step launch sequence (rocprofv3 names, tools/pmc_summary.py keys)
+ESTEP_KERNELS = ["estep_prep_kernel", "estep_mfma_kernel_occ3", "estep_mfma_kernel"]
+MSTEP_KERNELS = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_kernel", "rhs_kernel",
+                 "chol_mfma_kernel"]
+MSTEP_KERNELS_LARGE = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_wide_kernel",
+                       "rhs_kernel", "diag_tol_kernel", "chol_mfma_kernel", "tile_inverse_kernel",
+                       "tile_gemm_kernel", "trisolve_kernel"]
 
 
 def mstep_flops_per_trial_iter(n_tx, n_rx, N, T_p, T_d):
@@ -144,7 +154,8 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_estep_latest.json"))
+    ap.add_argument("--pmc", default=None,
+                    help="PMC summary (default: profiles/pmc_<config>_latest.json)")
     args = ap.parse_args()
 
     import torch
@@ -238,46 +249,56 @@ def main():
     mstep_ms = e0.elapsed_time(e1) / args.kernel_reps
 
     P = N + 1
-    pmc = load_pmc_traffic(args.pmc)
-    traffic = None
+    pmc = load_pmc_traffic(args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}_latest.json"))
+    pmc_ok = bool(pmc and pmc.get("config") == args.config and pmc.get("trials") == B)
+
+    def traffic_of(kernels, anchor):
+        """HBM bytes of ONE phase execution from the committed PMC summary of the same config
+        and trial count (tools/pmc_summary.py): total FETCH / WRITE bytes of the phase's
+        kernels divided by the launches of its once-per-phase anchor kernel; else None."""
+        if not pmc_ok:
+            return None
+        ks = pmc.get("kernels", {})
+        anc = next((ks[a] for a in anchor if a in ks), None)
+        if not anc or not anc["launches_fetch"] or not anc["launches_write"]:
+            return None
+        ents = [v for k, v in ks.items() if k in kernels]
+        return (sum(e["fetch_bytes_total"] for e in ents) / anc["launches_fetch"] +
+                sum(e["write_bytes_total"] for e in ents) / anc["launches_write"])
+
     mflops = mstep_flops_per_trial_iter(n_tx, n_rx, N, T_p, T_d) * B
     mbytes = mstep_bytes_per_trial_iter(n_tx, n_rx, N, T_p, T_d) * B
-    mstep_roof = {"kernel": "M-step (R build + Cholesky + solves)", "ms": mstep_ms,
+    m_kern = MSTEP_KERNELS_LARGE if n_tx * P > 512 else MSTEP_KERNELS
+    mstep_roof = {"bound": "mfma", "pipe": "FP64 MFMA v_mfma_f64_16x16x4f64 (+ FP64 VALU)",
+                  "phase": "M-step", "kernels": m_kern, "ms": mstep_ms,
                   "achieved": mflops / (mstep_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
                   "unit": "TFLOP/s", "frac": mflops / (mstep_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-                  "algorithmic_bytes": mbytes,
+                  "traffic": traffic_of(m_kern, ["rhs_kernel"]), "algorithmic_bytes": mbytes,
                   "hbm_frac_algorithmic": mbytes / (mstep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                   "flops_per_launch": mflops}
     if mode in ("soft", "hard"):
         flops = estep_flops_per_trial_iter(n_tx, n_rx, T_d, M) * B
         algo_bytes = estep_bytes_per_trial_iter(n_tx, n_rx, P, T_d) * B
-        if pmc and pmc.get("config") == args.config and pmc.get("trials") == B:
-            traffic = pmc.get("hbm_bytes_per_launch")
         # executed work: the MFMAs issued (16x16x4 f64 = 2048 flop each); the full
         # enumeration's flops are reported next to it ("enumeration_*")
         executed = mfma_issued * 2048 if mfma_issued is not None else flops
         achieved_tf = executed / (estep_ms * 1e-3) / 1e12
         estep_roof = {"bound": "mfma", "pipe": "FP64 MFMA v_mfma_f64_16x16x4f64 (+ FP64 VALU)",
-                      "kernel": "estep_mfma_kernel", "ms": estep_ms,
+                      "phase": "E-step", "kernels": ESTEP_KERNELS, "ms": estep_ms,
                       "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic_of(ESTEP_KERNELS, ESTEP_KERNELS),
                       "flops_per_launch": executed,
                       "enumeration_flops_per_launch": flops,
                       "enumeration_fraction_issued": executed / flops,
                       "algorithmic_bytes": algo_bytes,
                       "hbm_GBps_algorithmic": algo_bytes / (estep_ms * 1e-3) / 1e9,
                       "hbm_frac_algorithmic": algo_bytes / (estep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
-        # the dominant kernel (longest per EM iteration) carries the roofline object
-        if estep_ms >= mstep_ms:
-            roofline = estep_roof
-        else:
-            roofline = dict(mstep_roof, bound="mfma", traffic=None,
-                            pipe="FP64 MFMA v_mfma_f64_16x16x4f64 (+ FP64 VALU)")
+        # the dominant phase (longest per EM iteration) carries the roofline object
+        roofline = estep_roof if estep_ms >= mstep_ms else mstep_roof
     else:
         estep_roof = None
         # list-detector workloads: the M-step (MFMA tile build + blocked Cholesky) dominates
-        roofline = dict(mstep_roof, bound="mfma", traffic=None,
-                        pipe="FP64 MFMA v_mfma_f64_16x16x4f64")
+        roofline = mstep_roof
 
     value = world * B * iters * args.steps / elapsed
     line = {

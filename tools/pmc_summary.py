@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Summarise two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) into per-launch HBM
-bytes per kernel, and write the E-step entry bench.py reads for roofline.traffic.
+bytes per kernel (bench.py sums the kernels of the roofline phase into roofline.traffic).
 
   python tools/pmc_summary.py --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write \
-      --config cfg1 --trials 1000 --out profiles/pmc_estep_latest.json
+      --config cfg1 --trials 1000 --out profiles/pmc_cfg1_latest.json
 
 Corrections (MI355X_MICROARCH.md, "HBM [CDNA4]"): rocprofv3 reports FETCH_SIZE and
 WRITE_SIZE in KiB; on gfx950 FETCH_SIZE counts wide coalesced reads at half their
@@ -62,24 +62,21 @@ def main():
     kernels = {}
     for name in sorted(set(fetch) | set(write)):
         f, w = fetch.get(name, []), write.get(name, [])
-        k = _short(name)
+        k = _short(name)          # template instantiations of one kernel are summed
         ent = kernels.setdefault(k, {"launches_fetch": 0, "launches_write": 0,
-                                     "fetch_bytes_per_launch": None,
-                                     "write_bytes_per_launch": None})
-        if f:
-            ent["launches_fetch"] += len(f)
-            ent["fetch_bytes_per_launch"] = 2.0 * 1024.0 * sum(f) / len(f)
-        if w:
-            ent["launches_write"] += len(w)
-            ent["write_bytes_per_launch"] = 1024.0 * sum(w) / len(w)
+                                     "fetch_bytes_total": 0.0, "write_bytes_total": 0.0})
+        ent["launches_fetch"] += len(f)
+        ent["fetch_bytes_total"] += 2.0 * 1024.0 * sum(f)
+        ent["launches_write"] += len(w)
+        ent["write_bytes_total"] += 1024.0 * sum(w)
     for ent in kernels.values():
-        fb, wb = ent["fetch_bytes_per_launch"], ent["write_bytes_per_launch"]
-        ent["hbm_bytes_per_launch"] = (fb or 0.0) + (wb or 0.0)
-    est = kernels.get("estep_mfma_kernel") or kernels.get("estep_kernel")
+        fb = ent["fetch_bytes_total"] / ent["launches_fetch"] if ent["launches_fetch"] else 0.0
+        wb = ent["write_bytes_total"] / ent["launches_write"] if ent["launches_write"] else 0.0
+        ent["fetch_bytes_per_launch"], ent["write_bytes_per_launch"] = fb, wb
+        ent["hbm_bytes_per_launch"] = fb + wb
     out = {"config": a.config, "trials": a.trials,
            "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; "
                      "FETCH_SIZE x2 (gfx950), KiB -> bytes",
-           "hbm_bytes_per_launch": est["hbm_bytes_per_launch"] if est else None,
            "kernels": kernels}
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
