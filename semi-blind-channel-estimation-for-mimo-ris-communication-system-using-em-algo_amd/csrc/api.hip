@@ -54,11 +54,10 @@ Carve carve(const Problem& pb) {
         c.pflag = align_up(c.pS + (size_t)pb.B * pb.Tp * pb.NT * pb.NT * sizeof(cd));
         c.total = align_up(c.pflag + (size_t)pb.B * sizeof(int32_t));
     }
-    if (pb.L > kLargeL) {                    // tiled large-L M-step (mstep_large.hip)
-        c.tol = c.total;
-        c.winv = align_up(c.tol + (size_t)pb.B * sizeof(double));
+    c.tol = c.total;                         // per-trial pivot threshold
+    c.winv = c.total = align_up(c.tol + (size_t)pb.B * sizeof(double));
+    if (pb.L > kLargeL)                      // tiled large-L M-step (mstep_large.hip)
         c.total = align_up(c.winv + (size_t)pb.B * 64 * 64 * sizeof(cd));
-    }
     return c;
 }
 
@@ -147,7 +146,7 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     MstepArgs ma;
     ma.yd = ea.yd; ma.yp = (const cd*)p->y_p; ma.psid = ea.psid; ma.up = (const cd*)p->u_p;
     ma.mom = ea.mom; ma.R = (cd*)(ws + c.R); ma.rhs = (cd*)(ws + c.rhs); ma.theta = (cd*)p->theta;
-    ma.status = p->status; ma.done = ea.done; ma.solve_mode = solve_mode;
+    ma.status = p->status; ma.done = ea.done; ma.solve_mode = solve_mode; ma.nbatch = pb.B;
     set_large(ma, ws, c);
 
     EstepArgs eas = ea;                      // superimposed pilots: E-step on y - H x_p
@@ -227,7 +226,7 @@ int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int 
     ma.yd = (const cd*)p->y_d; ma.yp = (const cd*)p->y_p; ma.psid = (const cd*)p->psi_d;
     ma.up = (const cd*)p->u_p; ma.mom = (const cd*)moments; ma.R = (cd*)(ws + c.R);
     ma.rhs = (cd*)(ws + c.rhs); ma.theta = (cd*)p->theta; ma.status = p->status; ma.done = nullptr;
-    ma.solve_mode = solve_mode;
+    ma.solve_mode = solve_mode; ma.nbatch = pb.B;
     set_large(ma, ws, c);
     if ((rc = hip_rc(launch_mstep_build(pb, ma, s)))) return rc;
     if (r_out &&

@@ -378,22 +378,30 @@ __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double t
 // Blocked back substitution L^H x = y for the MFMA kernel: every thread owns column
 // k = tid (+ nth) of the update and loads its 16 factor entries BEFORE the barrier that
 // publishes the block solution, so each block pays one memory latency, not three.
+template <int H = 2>     // rows k of the update per thread (H * nth >= L)
 __device__ __forceinline__ void back_substitute_pf(const cd* R, cd* y, int L, int NR, int tid,
                                                    int nth, int lane, int wave, int kb_stop,
-                                                   int ld) {
+                                                   int ld, cd* dblk) {
+    // dblk: LDS [NB][NB] scratch for the diagonal block (its rows hold L[c][c] on the
+    // diagonal and conj(Di[c2][c]) above it), loaded by the whole workgroup at once
     const int nblk = (L + NB - 1) / NB;
     for (int kb = nblk - 1; kb >= kb_stop; --kb) {
         const int k0 = kb * NB;
         const int w = (L - k0) < NB ? (L - k0) : NB;
         // prefetch: conj(L[k0+c][k]) for this thread's columns k < k0
-        cd lv[2][NB];
+        cd lv[H][NB];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < H; ++h) {
             const int k = tid + h * nth;
 #pragma unroll
             for (int c = 0; c < NB; ++c)
                 lv[h][c] = (k < k0 && c < w) ? R[(size_t)(k0 + c) * ld + k] : czero();
         }
+        for (int e = tid; e < NB * NB; e += nth) {
+            const int c = e >> 4, c2 = e & 15;
+            dblk[e] = (c < w && c2 < w && c2 >= c) ? R[(size_t)(k0 + c) * ld + k0 + c2] : czero();
+        }
+        __syncthreads();
         if (wave == 0) {
             // x_blk = D^{-H} z_blk:  x[c] = z[c] / L[c][c] + sum_{c2>c} conj(Di[c2][c]) z[c2]
             const int e0 = lane, e1 = lane + 64;
@@ -403,7 +411,7 @@ __device__ __forceinline__ void back_substitute_pf(const cd* R, cd* y, int L, in
                 const int e = h ? e1 : e0;
                 if (e < w * NR) {
                     const int c = e / NR, r = e - c * NR;
-                    const cd* Rc = R + (size_t)(k0 + c) * ld + k0;
+                    const cd* Rc = dblk + c * NB;
                     const double lcc = Rc[c].x;
                     cd acc = (lcc > 0.0) ? cscale(y[(k0 + c) * NR + r], 1.0 / lcc) : czero();
                     for (int c2 = c + 1; c2 < w; ++c2) acc = cfma(acc, Rc[c2], y[(k0 + c2) * NR + r]);
@@ -416,7 +424,7 @@ __device__ __forceinline__ void back_substitute_pf(const cd* R, cd* y, int L, in
         }
         __syncthreads();
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < H; ++h) {
             const int k = tid + h * nth;
             if (k < k0) {
                 for (int r = 0; r < NR; ++r) {
@@ -631,13 +639,257 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip, CholGeom g) {
     }
     if (SOLVE) {
         back_substitute_pf(R, y, L, NR, tid, nth, lane, wave, (skip & 16) ? (L + NB - 1) / NB : 0,
-                           ld);
+                           ld, Di);
         SBCE_CLK(5)
         cd* th = a.theta + (size_t)b * L * NR;
         for (int e = tid; e < L * NR; e += nth) th[e] = cconj(y[e]);
     }
 #undef SBCE_CLK
     if (tid == 0 && a.status) a.status[b] |= *flag ? SBCE_STATUS_NONHPD : 0;
+}
+
+// ---------------------------------------------------------------- batched panel kernels
+// The same left-looking blocked factorisation and fused forward substitution as
+// chol_mfma_kernel, but one LAUNCH per panel step over every trial instead of one
+// workgroup walking all panels of its trial: the panel update is a batched GEMM with one
+// wave per 16-row tile (high occupancy hides the streamed rows' latency), the serial
+// diagonal factor of ~1000 trials runs side by side in the factor launch, and nothing
+// needs the register budget of a whole trial's tiles.  y lives in the rhs buffer.
+//
+// panel_update_kernel (jb > 0): C_tau = A[rows tau, jb:jb+16] - L[rows tau, 0:jb] L[jb:jb+16, 0:jb]^H
+// for the row tiles tau = 0.. of panel jb; block = 4 waves = 4 row tiles of ONE trial, the
+// panel's top rows staged per KBU-column chunk in LDS (shared B operand), each wave's rows
+// streamed from R with the next 16 columns in flight.  Blocks of one trial sit on one XCD.
+constexpr int KBU = 64;
+__global__ __launch_bounds__(256) void panel_update_kernel(MstepArgs a, int L, int jb, int ntile,
+                                                           int gpt, int skip) {
+    // skip: DIAGNOSTIC (timing only, results invalid): 1 no update
+    __shared__ __attribute__((aligned(16))) cd Bp[NB * (KBU + 1)];
+    const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
+    const int b = (slot / gpt) * 8 + xcd, grp = slot - (slot / gpt) * gpt;
+    if (b >= a.nbatch) return;
+    if (a.done && a.done[b]) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    const int tau = grp * 4 + wave;
+    const bool active = tau < ntile;                         // wave-uniform
+    const int w = (L - jb) < NB ? (L - jb) : NB;
+    cd* R = a.R + (size_t)b * L * L;
+    const int row0 = jb + tau * NB;
+    int r = row0 + li;
+    r = r < L ? r : L - 1;                                   // rows past L: harmless reads
+    const cd* arow = R + (size_t)r * L + lk;
+    d4v cre = {0.0, 0.0, 0.0, 0.0}, cim = {0.0, 0.0, 0.0, 0.0};
+    if (active) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int rr = row0 + lk + 4 * q;
+            if (rr < L && li < w) {
+                const cd v = R[(size_t)rr * L + jb + li];
+                cre[q] = v.x;
+                cim[q] = v.y;
+            }
+        }
+    }
+    for (int kb0 = 0; kb0 < ((skip & 1) ? 0 : jb); kb0 += KBU) {
+        const int kbs = (jb - kb0) < KBU ? (jb - kb0) : KBU;        // multiple of 16
+        cd av[4];
+        if (active) {
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) av[s2] = arow[kb0 + 4 * s2];
+        }
+        __syncthreads();
+        // panel top rows by LDS-DMA: one wave-instruction per row (64 lanes = the row's KBU
+        // slots, never crossing into the pad); lanes past kbs / rows past w read row jb
+#pragma unroll
+        for (int c4 = 0; c4 < NB / 4; ++c4) {
+            const int c = wave * (NB / 4) + c4;
+            const cd* src = R + (size_t)jb * L + kb0;
+            if (c < w && lane < kbs) src = R + (size_t)(jb + c) * L + kb0 + lane;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)(Bp + c * (KBU + 1)),
+                                             16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (active) {
+            for (int k0 = 0; k0 < kbs; k0 += 16) {
+                cd an[4];
+                const bool more = k0 + 16 < kbs;
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) an[s2] = more ? arow[kb0 + k0 + 16 + 4 * s2] : czero();
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) {
+                    const cd t = Bp[li * (KBU + 1) + k0 + 4 * s2 + lk];
+                    const cd v = av[s2];
+                    // C -= A conj(B)^T:  re -= ar tr + ai ti ;  im -= ai tr - ar ti
+                    cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre, 0, 0, 0);
+                    cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre, 0, 0, 0);
+                    cim = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim, 0, 0, 0);
+                    cim = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim, 0, 0, 0);
+                }
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) av[s2] = an[s2];
+            }
+        }
+    }
+    if (active) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int rr = row0 + lk + 4 * q;
+            if (rr < L && li < w) R[(size_t)rr * L + jb + li] = cmk(cre[q], cim[q]);
+        }
+    }
+}
+
+// panel_factor_kernel: one workgroup (4 waves) per trial.  Wave 0 factors the updated
+// diagonal tile in LDS (factor_diag_lds: L_kk and conj(D^-1) into R's diagonal block) and
+// applies D^-1 to the y block; then the waves TRSM the row tiles below round-robin,
+// X = C D^{-H} (16 MFMAs per tile), write L back and update their y rows.
+__global__ __launch_bounds__(256) void panel_factor_kernel(MstepArgs a, int L, int NR, int jb,
+                                                           int ntile, int skip) {
+    // skip: DIAGNOSTIC phase mask (timing only, results invalid): 2 diag factor, 8 trsm tiles
+    __shared__ cd Di[NB * NB];
+    __shared__ cd Xs[4 * NB * NB];
+    __shared__ cd yb[NB * 8];                   // the panel's y block after D^-1 (NR <= 8)
+    __shared__ double dinv[NB];
+    __shared__ int flag;
+    const int b = blockIdx.x;
+    if (a.done && a.done[b]) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    const int w = (L - jb) < NB ? (L - jb) : NB;
+    cd* R = a.R + (size_t)b * L * L;
+    cd* y = a.rhs + (size_t)b * L * NR;
+    cd* X = Xs + wave * NB * NB;
+    // this wave's first row tile below the diagonal: loads in flight during the diagonal
+    // factor (lane holds entries e = lane + 64 h of the 16 x 16 tile, row e >> 4)
+    auto load_tile = [&](int tau, cd* v) {
+        const int row0 = jb + tau * NB;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const int e = lane + 64 * h, rr = e >> 4, c = e & 15;
+            v[h] = (tau < ntile && row0 + rr < L && c < w) ? R[(size_t)(row0 + rr) * L + jb + c]
+                                                            : czero();
+        }
+    };
+    cd cur[4];
+    load_tile(1 + wave, cur);
+    if (tid == 0) flag = 0;
+    __syncthreads();
+    if (wave == 0) {
+        for (int e = lane; e < NB * NB; e += 64) {
+            const int rr = e >> 4, c = e & 15;
+            X[e] = (rr < w && c <= rr) ? R[(size_t)(jb + rr) * L + jb + c] : czero();
+        }
+        wave_sync();
+        if (!(skip & 2)) {
+            factor_diag_lds(X, w, lane, a.tol[b], a.solve_mode, Di, dinv, &flag,
+                            R + (size_t)jb * L + jb, L);
+            forward_y_block(Di, y + jb * NR, w, NR, lane);
+        }
+        wave_sync();
+        for (int e = lane; e < NB * NR; e += 64) yb[e] = (e < w * NR) ? y[jb * NR + e] : czero();
+    }
+    __syncthreads();
+    for (int tau = 1 + wave; tau < ((skip & 8) ? 0 : ntile); tau += 4) {
+        const int row0 = jb + tau * NB;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) X[lane + 64 * h] = cur[h];
+        cd nxt[4];
+        load_tile(tau + 4, nxt);                       // next tile of this wave in flight
+        wave_sync();
+        d4v xre = {0.0, 0.0, 0.0, 0.0}, xim = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s2 = 0; s2 < NB / 4; ++s2) {
+            const cd d = Di[li * NB + 4 * s2 + lk];    // A[j][k] = conj(Di[j][4s+k])
+            const cd c = X[li * NB + 4 * s2 + lk];     // B[k][i] = C[i][4s+k]
+            // X^T = conj(Di) C^T:  re += dr cr + di ci ;  im += dr ci - di cr
+            xre = __builtin_amdgcn_mfma_f64_16x16x4f64(d.x, c.x, xre, 0, 0, 0);
+            xre = __builtin_amdgcn_mfma_f64_16x16x4f64(d.y, c.y, xre, 0, 0, 0);
+            xim = __builtin_amdgcn_mfma_f64_16x16x4f64(d.x, c.y, xim, 0, 0, 0);
+            xim = __builtin_amdgcn_mfma_f64_16x16x4f64(-d.y, c.x, xim, 0, 0, 0);
+        }
+        const bool live = row0 + li < L;
+        cd* crow = R + (size_t)(live ? row0 + li : L - 1) * L + jb;
+        cd xv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = lk + 4 * q;
+            xv[q] = cmk(xre[q], xim[q]);
+            if (live && j < w) crow[j] = xv[q];
+        }
+        // y[row0+li] -= sum_j X[li][j] y_blk[j]: 4 columns per lane, reduced over lk; all
+        // right-hand sides of the row read and written together
+        cd p[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            p[r] = czero();
+            if (r < NR) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) p[r] = cfma(p[r], xv[q], yb[(lk + 4 * q) * NR + r]);
+                p[r].x += shfl_xor_d(p[r].x, 16); p[r].y += shfl_xor_d(p[r].y, 16);
+                p[r].x += shfl_xor_d(p[r].x, 32); p[r].y += shfl_xor_d(p[r].y, 32);
+            }
+        }
+        if (lk == 0 && live) {
+            cd* yr = y + (size_t)(row0 + li) * NR;
+            cd yo[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) yo[r] = (r < NR) ? yr[r] : czero();
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                if (r < NR) yr[r] = csub(yo[r], p[r]);
+        }
+#pragma unroll
+        for (int h = 0; h < 4; ++h) cur[h] = nxt[h];
+        wave_sync();
+    }
+    if (tid == 0 && flag && a.status) atomicOr(&a.status[b], SBCE_STATUS_NONHPD);
+}
+
+// Back substitution L^H x = y (y staged in LDS) and theta = conj(x), one workgroup per trial.
+__global__ __launch_bounds__(256) void backsub_kernel(MstepArgs a, int L, int NR, int skip) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cd* y = reinterpret_cast<cd*>(smem);
+    const int b = blockIdx.x;
+    if (a.done && a.done[b]) return;
+    const int tid = threadIdx.x, lane = tid & 63, nth = blockDim.x;     // 2 nth >= L
+    const int wave = tid >> 6;
+    const cd* R = a.R + (size_t)b * L * L;
+    const cd* yg = a.rhs + (size_t)b * L * NR;
+    for (int e = tid; e < L * NR; e += nth) y[e] = yg[e];
+    __syncthreads();
+    back_substitute_pf<2>(R, y, L, NR, tid, nth, lane, wave, (skip & 16) ? (L + NB - 1) / NB : 0, L,
+                          y + L * NR);
+    cd* th = a.theta + (size_t)b * L * NR;
+    for (int e = tid; e < L * NR; e += nth) th[e] = cconj(y[e]);
+}
+
+hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_t s) {
+    const char* sk = getenv("SBCE_CHOL_SKIP");      // diagnostic only (see kernels)
+    const int skip = sk ? atoi(sk) : 0;
+    hipError_t e = launch_diag_tol(pb, a, s);
+    if (e != hipSuccess) return e;
+    const int ntile = (pb.L + NB - 1) / NB;
+    for (int j = 0; j < ntile; ++j) {
+        const int jb = j * NB, rem = ntile - j;
+        if (j > 0) {
+            const int gpt = (rem + 3) / 4;
+            const long nblk = 8L * ((pb.B + 7) / 8) * gpt;
+            hipLaunchKernelGGL(panel_update_kernel, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L,
+                               jb, rem, gpt, skip);
+        }
+        hipLaunchKernelGGL(panel_factor_kernel, dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR, jb, rem,
+                           skip);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(backsub_kernel, dim3(pb.B), dim3(256),
+                       ((size_t)pb.L * pb.NR + NB * NB) * sizeof(cd), s,
+                       a, pb.L, pb.NR, skip);
+    return hipGetLastError();
 }
 
 template <int RPT, bool YLDS>
@@ -729,6 +981,9 @@ hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t 
     const char* impl = getenv("SBCE_CHOL_IMPL");    // "valu" forces the VALU kernel (A/B runs)
     const bool force_valu = impl && impl[0] == 'v';
     if (!force_valu && pb.L <= 512) {
+        // default: batched panel launches; SBCE_CHOL_IMPL=fused keeps the one-workgroup-per-
+        // trial kernel (A/B runs)
+        if (!(impl && impl[0] == 'f')) return launch_chol_batched(pb, a, s);
         if (ybytes <= 24 * 1024) return launch_mfma<true>(pb, a, ybytes, s);
         return launch_mfma<false>(pb, a, ybytes, s);
     }

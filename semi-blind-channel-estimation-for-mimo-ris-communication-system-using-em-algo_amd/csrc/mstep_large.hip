@@ -581,10 +581,14 @@ hipError_t launch_rbuild_herm(const Problem& pb, const MstepArgs& a, hipStream_t
     return hipErrorInvalidValue;
 }
 
+hipError_t launch_diag_tol(const Problem& pb, const MstepArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(diag_tol_kernel, dim3(pb.B), dim3(256), 0, s, a, pb.L);
+    return hipGetLastError();
+}
+
 hipError_t launch_chol_large(const Problem& pb, const MstepArgs& a, hipStream_t s) {
     if (pb.NR > 8) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(diag_tol_kernel, dim3(pb.B), dim3(256), 0, s, a, pb.L);
-    hipError_t e = hipGetLastError();
+    hipError_t e = launch_diag_tol(pb, a, s);
     if (e != hipSuccess) return e;
     const int nb = (pb.L + TB - 1) / TB;
     for (int k = 0; k < nb; ++k) {

@@ -134,6 +134,7 @@ struct MstepArgs {
     int32_t* status;   // [B] or null
     const int32_t* done;
     int solve_mode;
+    int nbatch;        // B (kernels whose grid is padded past the batch)
     // MFMA R build (NT in {4, 8}) workspace
     cd* ppsi;          // [B][Tp][P]  pilot phases psi' (Kronecker factor of u_p)
     cd* pS;            // [B][Tp][NT*NT] pilot x' x'^H
@@ -158,6 +159,7 @@ bool rbuild_herm_supported(const Problem& pb);   // MFMA build of the Hermitian 
 hipError_t launch_pilot_factor(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_rbuild_herm(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_chol_large(const Problem& pb, const MstepArgs& a, hipStream_t s);
+hipError_t launch_diag_tol(const Problem& pb, const MstepArgs& a, hipStream_t s);  // a.tol[b]
 hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w, hipStream_t s);
 hipError_t chol_debug_clock(unsigned long long* out);   // diagnostic (SBCE_CHOL_SKIP & 64)
 hipError_t chol_debug_clock_reset();

@@ -64,7 +64,7 @@ def test_workspace_and_validation_without_gpu(sbce):
               + 1000 * 256 * 4 * 16                       # moments, R, rhs, shifted y
               + 1000 * 256 * (4 + 2 * 16 + 16) * 8        # E-step sweep prep (H_eff, bounds)
               + 1000 * 16 * 65 * 16 + 1000 * 16 * 16 * 16  # factored pilots psi', x' x'^H
-              + 1000 * 4)                                 # pilot flags
+              + 1000 * 4 + 1000 * 8)                      # pilot flags, pivot thresholds
     assert expect <= n <= expect + 8 * 256 + 4000
     bad = L.Dims(1, 9, 4, 65, 16, 256, 16, 0, 0.1)     # n_tx > 8
     nb = ctypes.c_size_t(0)

@@ -351,26 +351,27 @@ def test_pm_soft_full_em_cfg2_geometry_vs_oracle(sbce):
     (1, 1, 40, 8, 80),        # L = 41, single RHS
 ])
 def test_mfma_and_valu_cholesky_agree(sbce, shape, monkeypatch):
-    """The MFMA and the VALU blocked Cholesky solve the same normal equations, and both
-    match numpy.linalg.solve of the R, rhs the device built."""
+    """The batched-panel MFMA, the fused MFMA and the VALU blocked Cholesky solve the same
+    normal equations, and all match numpy.linalg.solve of the R, rhs the device built."""
     n_tx, n_rx, N, T_p, T_d = shape
     b = sbce.signal_model.synthetic_batch(2, n_tx, n_rx, N, T_p, T_d, 4, 0.05, seed=4)
     x = b["x_d"]
     m = x
     S = x[..., :, None] * np.conj(x[..., None, :]) + 0.1 * np.eye(n_tx)
     out = {}
-    for impl in ("mfma", "valu"):
+    # default = batched panel launches; "fused" = one workgroup per trial; "valu"
+    for impl in ("batched", "fused", "valu"):
         monkeypatch.setenv("SBCE_CHOL_IMPL", impl)
         out[impl] = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], m, S, 0.05)
-    th_m, R, rhs, st = out["mfma"]
-    th_v = out["valu"][0]
+    th_m, R, rhs, st = out["batched"]
     assert not st.any()
     for i in range(2):
         X = np.linalg.solve(R[i], rhs[i])                     # R X = B^H, theta = conj(X)
         ref = np.conj(X).reshape(-1)
-        assert rel(th_m[i], ref) < 1e-9
-        assert rel(th_v[i], ref) < 1e-9
-    assert rel(th_m, th_v) < 1e-9
+        for impl in out:
+            assert rel(out[impl][0][i], ref) < 1e-9, impl
+    assert rel(th_m, out["fused"][0]) < 1e-9
+    assert rel(th_m, out["valu"][0]) < 1e-9
 
 
 # ---------------------------------------------------------------- large-L M-step (L > 512)
