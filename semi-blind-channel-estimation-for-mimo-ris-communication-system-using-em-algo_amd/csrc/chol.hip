@@ -650,21 +650,24 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip, CholGeom g) {
 
 // ---------------------------------------------------------------- batched panel kernels
 // The same left-looking blocked factorisation and fused forward substitution as
-// chol_mfma_kernel, but one LAUNCH per panel step over every trial instead of one
-// workgroup walking all panels of its trial: the panel update is a batched GEMM with one
-// wave per 16-row tile (high occupancy hides the streamed rows' latency), the serial
-// diagonal factor of ~1000 trials runs side by side in the factor launch, and nothing
+// chol_mfma_kernel, but one LAUNCH per 32-column panel step over every trial instead of
+// one workgroup walking all panels of its trial: the panel update is a batched GEMM with
+// one wave per 16-row tile (high occupancy hides the streamed rows' latency), the serial
+// diagonal factors of ~1000 trials run side by side in the factor launch, and no kernel
 // needs the register budget of a whole trial's tiles.  y lives in the rhs buffer.
 //
-// panel_update_kernel (jb > 0): C_tau = A[rows tau, jb:jb+16] - L[rows tau, 0:jb] L[jb:jb+16, 0:jb]^H
-// for the row tiles tau = 0.. of panel jb; block = 4 waves = 4 row tiles of ONE trial, the
-// panel's top rows staged per KBU-column chunk in LDS (shared B operand), each wave's rows
-// streamed from R with the next 16 columns in flight.  Blocks of one trial sit on one XCD.
+// panel_update_kernel (jb > 0): C_tau = A[rows tau, jb:jb+32] - L[rows tau, 0:jb] L[jb:jb+32, 0:jb]^H
+// for the 16-row tiles tau = 0.. of panel jb; block = 4 waves = 4 row tiles of ONE trial,
+// the panel's top rows staged per KBU-column chunk in LDS by LDS-DMA (shared B operand),
+// each wave's rows streamed from R with the next 16 columns in flight; every A value
+// feeds both 16-column halves (the left-looking re-reads of a 16-column panel halved).
+// Blocks of one trial sit on one XCD.
 constexpr int KBU = 64;
+constexpr int PW = 32;    // panel width: two 16-column sub-panels
 __global__ __launch_bounds__(256) void panel_update_kernel(MstepArgs a, int L, int jb, int ntile,
                                                            int gpt, int skip) {
     // skip: DIAGNOSTIC (timing only, results invalid): 1 no update
-    __shared__ __attribute__((aligned(16))) cd Bp[NB * (KBU + 1)];
+    __shared__ __attribute__((aligned(16))) cd Bp[PW * (KBU + 1)];
     const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
     const int b = (slot / gpt) * 8 + xcd, grp = slot - (slot / gpt) * gpt;
     if (b >= a.nbatch) return;
@@ -674,21 +677,28 @@ __global__ __launch_bounds__(256) void panel_update_kernel(MstepArgs a, int L, i
     const int li = lane & 15, lk = lane >> 4;
     const int tau = grp * 4 + wave;
     const bool active = tau < ntile;                         // wave-uniform
-    const int w = (L - jb) < NB ? (L - jb) : NB;
+    const int w2 = (L - jb) < PW ? (L - jb) : PW;
     cd* R = a.R + (size_t)b * L * L;
     const int row0 = jb + tau * NB;
     int r = row0 + li;
     r = r < L ? r : L - 1;                                   // rows past L: harmless reads
     const cd* arow = R + (size_t)r * L + lk;
-    d4v cre = {0.0, 0.0, 0.0, 0.0}, cim = {0.0, 0.0, 0.0, 0.0};
-    if (active) {
+    // tile 0's right half lies in the strict upper triangle: neither loaded nor stored
+    const int nv = tau == 0 ? 1 : 2;
+    d4v cre[2], cim[2];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int rr = row0 + lk + 4 * q;
-            if (rr < L && li < w) {
-                const cd v = R[(size_t)rr * L + jb + li];
-                cre[q] = v.x;
-                cim[q] = v.y;
+    for (int v = 0; v < 2; ++v) {
+        cre[v] = d4v{0.0, 0.0, 0.0, 0.0};
+        cim[v] = d4v{0.0, 0.0, 0.0, 0.0};
+        if (active && v < nv) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rr = row0 + lk + 4 * q, c = 16 * v + li;
+                if (rr < L && c < w2) {
+                    const cd x = R[(size_t)rr * L + jb + c];
+                    cre[v][q] = x.x;
+                    cim[v][q] = x.y;
+                }
             }
         }
     }
@@ -701,12 +711,12 @@ __global__ __launch_bounds__(256) void panel_update_kernel(MstepArgs a, int L, i
         }
         __syncthreads();
         // panel top rows by LDS-DMA: one wave-instruction per row (64 lanes = the row's KBU
-        // slots, never crossing into the pad); lanes past kbs / rows past w read row jb
+        // slots, never crossing into the pad); lanes past kbs / rows past w2 read row jb
 #pragma unroll
-        for (int c4 = 0; c4 < NB / 4; ++c4) {
-            const int c = wave * (NB / 4) + c4;
+        for (int c8 = 0; c8 < PW / 4; ++c8) {
+            const int c = wave * (PW / 4) + c8;
             const cd* src = R + (size_t)jb * L + kb0;
-            if (c < w && lane < kbs) src = R + (size_t)(jb + c) * L + kb0 + lane;
+            if (c < w2 && lane < kbs) src = R + (size_t)(jb + c) * L + kb0 + lane;
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                              (__attribute__((address_space(3))) void*)(Bp + c * (KBU + 1)),
                                              16, 0, 0);
@@ -721,13 +731,17 @@ __global__ __launch_bounds__(256) void panel_update_kernel(MstepArgs a, int L, i
                 for (int s2 = 0; s2 < 4; ++s2) an[s2] = more ? arow[kb0 + k0 + 16 + 4 * s2] : czero();
 #pragma unroll
                 for (int s2 = 0; s2 < 4; ++s2) {
-                    const cd t = Bp[li * (KBU + 1) + k0 + 4 * s2 + lk];
                     const cd v = av[s2];
-                    // C -= A conj(B)^T:  re -= ar tr + ai ti ;  im -= ai tr - ar ti
-                    cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre, 0, 0, 0);
-                    cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre, 0, 0, 0);
-                    cim = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim, 0, 0, 0);
-                    cim = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim, 0, 0, 0);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        if (h >= nv) break;                  // wave-uniform
+                        const cd t = Bp[(16 * h + li) * (KBU + 1) + k0 + 4 * s2 + lk];
+                        // C -= A conj(B)^T:  re -= ar tr + ai ti ;  im -= ai tr - ar ti
+                        cre[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre[h], 0, 0, 0);
+                        cre[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre[h], 0, 0, 0);
+                        cim[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim[h], 0, 0, 0);
+                        cim[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim[h], 0, 0, 0);
+                    }
                 }
 #pragma unroll
                 for (int s2 = 0; s2 < 4; ++s2) av[s2] = an[s2];
@@ -736,23 +750,94 @@ __global__ __launch_bounds__(256) void panel_update_kernel(MstepArgs a, int L, i
     }
     if (active) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int rr = row0 + lk + 4 * q;
-            if (rr < L && li < w) R[(size_t)rr * L + jb + li] = cmk(cre[q], cim[q]);
+        for (int v = 0; v < 2; ++v) {
+            if (v >= nv) break;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rr = row0 + lk + 4 * q, c = 16 * v + li;
+                if (rr < L && c < w2) R[(size_t)rr * L + jb + c] = cmk(cre[v][q], cim[v][q]);
+            }
         }
     }
 }
 
-// panel_factor_kernel: one workgroup (4 waves) per trial.  Wave 0 factors the updated
-// diagonal tile in LDS (factor_diag_lds: L_kk and conj(D^-1) into R's diagonal block) and
-// applies D^-1 to the y block; then the waves TRSM the row tiles below round-robin,
-// X = C D^{-H} (16 MFMAs per tile), write L back and update their y rows.
-__global__ __launch_bounds__(256) void panel_factor_kernel(MstepArgs a, int L, int NR, int jb,
-                                                           int ntile, int skip) {
-    // skip: DIAGNOSTIC phase mask (timing only, results invalid): 2 diag factor, 8 trsm tiles
-    __shared__ cd Di[NB * NB];
+// 16 x 16 tile of R (rows row0.., columns c0.., w valid columns) into per-lane registers:
+// lane holds entries e = lane + 64 h, row e >> 4, column e & 15
+__device__ __forceinline__ void load_tile16(const cd* R, int L, int row0, int c0, int w, int lane,
+                                            bool on, cd* v) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const int e = lane + 64 * h, rr = e >> 4, c = e & 15;
+        v[h] = (on && row0 + rr < L && c < w) ? R[(size_t)(row0 + rr) * L + c0 + c] : czero();
+    }
+}
+
+// TRSM of one 16-row tile (values in X, LDS) against the factored diagonal block of the
+// sub-panel at column c0 (inverse Di): L = C D^{-H}, written to R; y rows updated with the
+// sub-panel's y block yb.  Returns X[li][lk + 4q] in xv (the A-operand layout of k-step q).
+__device__ __forceinline__ void trsm_tile16(cd* R, cd* y, const cd* Di, const cd* X, const cd* yb,
+                                            int L, int NR, int row0, int c0, int w, int li,
+                                            int lk, cd* xv) {
+    d4v xre = {0.0, 0.0, 0.0, 0.0}, xim = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s2 = 0; s2 < NB / 4; ++s2) {
+        const cd d = Di[li * NB + 4 * s2 + lk];    // A[j][k] = conj(Di[j][4s+k])
+        const cd c = X[li * NB + 4 * s2 + lk];     // B[k][i] = C[i][4s+k]
+        // X^T = conj(Di) C^T:  re += dr cr + di ci ;  im += dr ci - di cr
+        xre = __builtin_amdgcn_mfma_f64_16x16x4f64(d.x, c.x, xre, 0, 0, 0);
+        xre = __builtin_amdgcn_mfma_f64_16x16x4f64(d.y, c.y, xre, 0, 0, 0);
+        xim = __builtin_amdgcn_mfma_f64_16x16x4f64(d.x, c.y, xim, 0, 0, 0);
+        xim = __builtin_amdgcn_mfma_f64_16x16x4f64(-d.y, c.x, xim, 0, 0, 0);
+    }
+    const bool live = row0 + li < L;
+    cd* crow = R + (size_t)(live ? row0 + li : L - 1) * L + c0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int j = lk + 4 * q;
+        xv[q] = cmk(xre[q], xim[q]);
+        if (live && j < w) crow[j] = xv[q];
+    }
+    // y[row0+li] -= sum_j X[li][j] y_blk[j]: 4 columns per lane, reduced over lk; all
+    // right-hand sides of the row read and written together
+    for (int r0 = 0; r0 < NR; r0 += 4) {                     // 4 right-hand sides per pass
+        cd p[4];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int r = r0 + rr;
+            p[rr] = czero();
+            if (r < NR) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) p[rr] = cfma(p[rr], xv[q], yb[(lk + 4 * q) * NR + r]);
+                p[rr].x += shfl_xor_d(p[rr].x, 16); p[rr].y += shfl_xor_d(p[rr].y, 16);
+                p[rr].x += shfl_xor_d(p[rr].x, 32); p[rr].y += shfl_xor_d(p[rr].y, 32);
+            }
+        }
+        if (lk == 0 && live) {
+            cd* yr = y + (size_t)(row0 + li) * NR + r0;
+            cd yo[4];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) yo[rr] = (r0 + rr < NR) ? yr[rr] : czero();
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+                if (r0 + rr < NR) yr[rr] = csub(yo[rr], p[rr]);
+        }
+    }
+}
+
+// panel_factor_kernel: one workgroup (4 waves) per trial, panel [jb, jb+32) as sub-panels
+// A = [jb, jb+16) and B = [jb+16, jb+32):
+//   wave 0: factor A's diagonal tile (factor_diag_lds), D_A^-1 y_A, TRSM of row tile 1
+//           (X_A1, kept in LDS);                                                 barrier
+//   wave 0: C_B1 -= X_A1 X_A1^H, factor it (B's diagonal tile), D_B^-1 y_B;
+//   waves 1-3, row tiles tau >= 2: TRSM against D_A, then the in-panel rank-16 update
+//           C_B,tau -= X_A,tau X_A1^H written back to R;                          barrier
+//   all waves, tau >= 2: TRSM of C_B,tau against D_B.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip) {
+    // skip: DIAGNOSTIC phase mask (timing only, results invalid): 2 diag factors, 8 trsm tiles
+    __shared__ cd DiA[NB * NB], DiB[NB * NB], XA1[NB * NB];
     __shared__ cd Xs[4 * NB * NB];
-    __shared__ cd yb[NB * 8];                   // the panel's y block after D^-1 (NR <= 8)
+    __shared__ cd ybA[NB * 8], ybB[NB * 8];     // the sub-panels' y blocks after D^-1
     __shared__ double dinv[NB];
     __shared__ int flag;
     const int b = blockIdx.x;
@@ -760,92 +845,132 @@ __global__ __launch_bounds__(256) void panel_factor_kernel(MstepArgs a, int L, i
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
-    const int w = (L - jb) < NB ? (L - jb) : NB;
+    const int w2 = (L - jb) < PW ? (L - jb) : PW;
+    const int wA = w2 < NB ? w2 : NB, wB = w2 - NB;          // wB <= 0: no sub-panel B
+    const int jbB = jb + NB;
+    const double tol = a.tol[b];
     cd* R = a.R + (size_t)b * L * L;
     cd* y = a.rhs + (size_t)b * L * NR;
     cd* X = Xs + wave * NB * NB;
-    // this wave's first row tile below the diagonal: loads in flight during the diagonal
-    // factor (lane holds entries e = lane + 64 h of the 16 x 16 tile, row e >> 4)
-    auto load_tile = [&](int tau, cd* v) {
-        const int row0 = jb + tau * NB;
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            const int e = lane + 64 * h, rr = e >> 4, c = e & 15;
-            v[h] = (tau < ntile && row0 + rr < L && c < w) ? R[(size_t)(row0 + rr) * L + jb + c]
-                                                            : czero();
-        }
-    };
-    cd cur[4];
-    load_tile(1 + wave, cur);
+    const bool trsm = !(skip & 8);
     if (tid == 0) flag = 0;
     __syncthreads();
+    cd xv[4];
     if (wave == 0) {
+        cd t1[4];
+        load_tile16(R, L, jbB, jb, wA, lane, ntile > 1, t1);        // row tile 1, A part
         for (int e = lane; e < NB * NB; e += 64) {
             const int rr = e >> 4, c = e & 15;
-            X[e] = (rr < w && c <= rr) ? R[(size_t)(jb + rr) * L + jb + c] : czero();
+            X[e] = (rr < wA && c <= rr) ? R[(size_t)(jb + rr) * L + jb + c] : czero();
         }
         wave_sync();
         if (!(skip & 2)) {
-            factor_diag_lds(X, w, lane, a.tol[b], a.solve_mode, Di, dinv, &flag,
+            factor_diag_lds(X, wA, lane, tol, a.solve_mode, DiA, dinv, &flag,
                             R + (size_t)jb * L + jb, L);
-            forward_y_block(Di, y + jb * NR, w, NR, lane);
+            forward_y_block(DiA, y + jb * NR, wA, NR, lane);
         }
         wave_sync();
-        for (int e = lane; e < NB * NR; e += 64) yb[e] = (e < w * NR) ? y[jb * NR + e] : czero();
+        for (int e = lane; e < NB * NR; e += 64) ybA[e] = (e < wA * NR) ? y[jb * NR + e] : czero();
+        wave_sync();
+        if (ntile > 1 && trsm) {
+#pragma unroll
+            for (int h = 0; h < 4; ++h) X[lane + 64 * h] = t1[h];
+            wave_sync();
+            trsm_tile16(R, y, DiA, X, ybA, L, NR, jbB, jb, wA, li, lk, xv);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) XA1[li * NB + lk + 4 * q] = xv[q];
+        }
     }
     __syncthreads();
-    for (int tau = 1 + wave; tau < ((skip & 8) ? 0 : ntile); tau += 4) {
-        const int row0 = jb + tau * NB;
+    if (wave == 0) {
+        if (wB > 0) {
+            // B's diagonal tile: C_B1 -= X_A1 X_A1^H, then factor
+            d4v cre = {0.0, 0.0, 0.0, 0.0}, cim = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int h = 0; h < 4; ++h) X[lane + 64 * h] = cur[h];
-        cd nxt[4];
-        load_tile(tau + 4, nxt);                       // next tile of this wave in flight
-        wave_sync();
-        d4v xre = {0.0, 0.0, 0.0, 0.0}, xim = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int s2 = 0; s2 < NB / 4; ++s2) {
-            const cd d = Di[li * NB + 4 * s2 + lk];    // A[j][k] = conj(Di[j][4s+k])
-            const cd c = X[li * NB + 4 * s2 + lk];     // B[k][i] = C[i][4s+k]
-            // X^T = conj(Di) C^T:  re += dr cr + di ci ;  im += dr ci - di cr
-            xre = __builtin_amdgcn_mfma_f64_16x16x4f64(d.x, c.x, xre, 0, 0, 0);
-            xre = __builtin_amdgcn_mfma_f64_16x16x4f64(d.y, c.y, xre, 0, 0, 0);
-            xim = __builtin_amdgcn_mfma_f64_16x16x4f64(d.x, c.y, xim, 0, 0, 0);
-            xim = __builtin_amdgcn_mfma_f64_16x16x4f64(-d.y, c.x, xim, 0, 0, 0);
-        }
-        const bool live = row0 + li < L;
-        cd* crow = R + (size_t)(live ? row0 + li : L - 1) * L + jb;
-        cd xv[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int j = lk + 4 * q;
-            xv[q] = cmk(xre[q], xim[q]);
-            if (live && j < w) crow[j] = xv[q];
-        }
-        // y[row0+li] -= sum_j X[li][j] y_blk[j]: 4 columns per lane, reduced over lk; all
-        // right-hand sides of the row read and written together
-        cd p[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            p[r] = czero();
-            if (r < NR) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) p[r] = cfma(p[r], xv[q], yb[(lk + 4 * q) * NR + r]);
-                p[r].x += shfl_xor_d(p[r].x, 16); p[r].y += shfl_xor_d(p[r].y, 16);
-                p[r].x += shfl_xor_d(p[r].x, 32); p[r].y += shfl_xor_d(p[r].y, 32);
+            for (int q = 0; q < 4; ++q) {
+                const int rr = lk + 4 * q;
+                if (rr < wB && li < wB) {
+                    const cd x = R[(size_t)(jbB + rr) * L + jbB + li];
+                    cre[q] = x.x;
+                    cim[q] = x.y;
+                }
             }
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const cd v = xv[s2], t = XA1[li * NB + 4 * s2 + lk];
+                cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre, 0, 0, 0);
+                cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre, 0, 0, 0);
+                cim = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim, 0, 0, 0);
+                cim = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim, 0, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = cmk(cre[q], cim[q]);
+            wave_sync();
+            if (!(skip & 2)) {
+                factor_diag_lds(X, wB, lane, tol, a.solve_mode, DiB, dinv, &flag,
+                                R + (size_t)jbB * L + jbB, L);
+                forward_y_block(DiB, y + jbB * NR, wB, NR, lane);
+            }
+            wave_sync();
+            for (int e = lane; e < NB * NR; e += 64) ybB[e] = (e < wB * NR) ? y[jbB * NR + e] : czero();
         }
-        if (lk == 0 && live) {
-            cd* yr = y + (size_t)(row0 + li) * NR;
-            cd yo[8];
+    } else if (trsm) {
+        // row tiles tau >= 2: TRSM against D_A, in-panel update of their B part
+        cd cur[4];
+        int tau = 1 + wave;
+        load_tile16(R, L, jb + tau * NB, jb, wA, lane, tau < ntile, cur);
+        for (; tau < ntile; tau += 3) {
+            const int row0 = jb + tau * NB;
 #pragma unroll
-            for (int r = 0; r < 8; ++r) yo[r] = (r < NR) ? yr[r] : czero();
+            for (int h = 0; h < 4; ++h) X[lane + 64 * h] = cur[h];
+            d4v cre = {0.0, 0.0, 0.0, 0.0}, cim = {0.0, 0.0, 0.0, 0.0};
+            if (wB > 0) {
 #pragma unroll
-            for (int r = 0; r < 8; ++r)
-                if (r < NR) yr[r] = csub(yo[r], p[r]);
+                for (int q = 0; q < 4; ++q) {
+                    const int rr = row0 + lk + 4 * q;
+                    if (rr < L && li < wB) {
+                        const cd x = R[(size_t)rr * L + jbB + li];
+                        cre[q] = x.x;
+                        cim[q] = x.y;
+                    }
+                }
+            }
+            load_tile16(R, L, row0 + 3 * NB, jb, wA, lane, tau + 3 < ntile, cur);   // next
+            wave_sync();
+            trsm_tile16(R, y, DiA, X, ybA, L, NR, row0, jb, wA, li, lk, xv);
+            if (wB > 0) {
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) {
+                    const cd v = xv[s2], t = XA1[li * NB + 4 * s2 + lk];
+                    cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre, 0, 0, 0);
+                    cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre, 0, 0, 0);
+                    cim = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim, 0, 0, 0);
+                    cim = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim, 0, 0, 0);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int rr = row0 + lk + 4 * q;
+                    if (rr < L && li < wB) R[(size_t)rr * L + jbB + li] = cmk(cre[q], cim[q]);
+                }
+            }
+            wave_sync();
         }
+    }
+    __syncthreads();
+    if (wB > 0 && trsm) {
+        // row tiles tau >= 2: TRSM of the updated B part against D_B
+        cd cur[4];
+        int tau = 2 + wave;
+        load_tile16(R, L, jb + tau * NB, jbB, wB, lane, tau < ntile, cur);
+        for (; tau < ntile; tau += 4) {
+            const int row0 = jb + tau * NB;
 #pragma unroll
-        for (int h = 0; h < 4; ++h) cur[h] = nxt[h];
-        wave_sync();
+            for (int h = 0; h < 4; ++h) X[lane + 64 * h] = cur[h];
+            load_tile16(R, L, row0 + 4 * NB, jbB, wB, lane, tau + 4 < ntile, cur);
+            wave_sync();
+            trsm_tile16(R, y, DiB, X, ybB, L, NR, row0, jbB, wB, li, lk, xv);
+            wave_sync();
+        }
     }
     if (tid == 0 && flag && a.status) atomicOr(&a.status[b], SBCE_STATUS_NONHPD);
 }
@@ -873,9 +998,10 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
     const int skip = sk ? atoi(sk) : 0;
     hipError_t e = launch_diag_tol(pb, a, s);
     if (e != hipSuccess) return e;
-    const int ntile = (pb.L + NB - 1) / NB;
-    for (int j = 0; j < ntile; ++j) {
-        const int jb = j * NB, rem = ntile - j;
+    const int npan = (pb.L + PW - 1) / PW;
+    for (int j = 0; j < npan; ++j) {
+        const int jb = j * PW;
+        const int rem = (pb.L - jb + NB - 1) / NB;               // 16-row tiles from jb
         if (j > 0) {
             const int gpt = (rem + 3) / 4;
             const long nblk = 8L * ((pb.B + 7) / 8) * gpt;
