@@ -515,6 +515,7 @@ struct MfmaConst {
     int prune;                 // column-tile bounds on (SBCE_ESTEP_PRUNE=0 disables: A/B runs)
     int count;                 // diagnostic MFMA count (SBCE_ESTEP_COUNT=1)
     int prep_stride;           // doubles per symbol of EstepArgs::prep
+    int red_old;               // A/B: six-step butterfly per value (SBCE_ESTEP_RED=old)
 };
 
 // V16 (M == 16, NA == 2): the A operand's V term, V[kk][i & 15] = V[kk][lane & 15], is the
@@ -966,24 +967,80 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     int xa[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) xa[i] = (lane ^ (32 >> i)) << 2;
-    auto wsum = [&](double v) {
+    if (c.red_old) {
+        auto wsum = [&](double v) {
 #pragma unroll
-        for (int i = 0; i < 6; ++i) v += bperm_d(v, xa[i]);
-        return v;
-    };
-    auto wsumc = [&](cd v) { return cmk(wsum(v.x), wsum(v.y)); };
-    tot_c = wsum(tot_c);
-    kap = wsumc(kap);
-    tot_kB = wsumc(tot_kB);
+            for (int i = 0; i < 6; ++i) v += bperm_d(v, xa[i]);
+            return v;
+        };
+        auto wsumc = [&](cd v) { return cmk(wsum(v.x), wsum(v.y)); };
+        tot_c = wsum(tot_c);
+        kap = wsumc(kap);
+        tot_kB = wsumc(tot_kB);
 #pragma unroll
-    for (int q = 0; q < NA; ++q) {
-        tot_muA[q] = wsumc(tot_muA[q]);
-        nu[q] = wsum(nu[q]);
+        for (int q = 0; q < NA; ++q) {
+            tot_muA[q] = wsumc(tot_muA[q]);
+            nu[q] = wsum(nu[q]);
 #pragma unroll
-        for (int bb = 0; bb < NB; ++bb) tot_X[q][bb] = wsumc(tot_X[q][bb]);
+            for (int bb = 0; bb < NB; ++bb) tot_X[q][bb] = wsumc(tot_X[q][bb]);
+        }
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) { tot_mB[bb] = wsumc(tot_mB[bb]); tot_nB[bb] = wsum(tot_nB[bb]); }
+    } else {
+        // Reduce-scatter by recursive halving: at the step with lane offset o a lane keeps the
+        // half of the remaining values selected by its bit o and receives the partner's copy
+        // of that half (32 + 16 + ... doubles moved instead of 6 per value); value j ends in
+        // the lanes whose bits 5..1 spell j, and is gathered through LDS.
+        constexpr int NV = 1 + 2 * NPA + 2 * NPB + 3 * NA + 2 * NA * NB + 3 * NB;
+        static_assert(NV <= 32, "reduce-scatter holds at most 32 values");
+        double v[32];
+        int n = 0;
+        auto put = [&](double x) { v[n++] = x; };
+        put(tot_c);
+        if (NPA) { put(kap.x); put(kap.y); }
+        if (NPB) { put(tot_kB.x); put(tot_kB.y); }
+#pragma unroll
+        for (int q = 0; q < NA; ++q) {
+            put(tot_muA[q].x); put(tot_muA[q].y); put(nu[q]);
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb) { put(tot_X[q][bb].x); put(tot_X[q][bb].y); }
+        }
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) { put(tot_mB[bb].x); put(tot_mB[bb].y); put(tot_nB[bb]); }
+#pragma unroll
+        for (int i = NV; i < 32; ++i) v[i] = 0.0;
+#pragma unroll
+        for (int st = 0; st < 5; ++st) {
+            const int h = 16 >> st;
+            const bool hi = (lane >> (5 - st)) & 1;
+#pragma unroll
+            for (int i = 0; i < h; ++i) {
+                const double snd = hi ? v[i] : v[h + i];
+                const double kp = hi ? v[h + i] : v[i];
+                v[i] = kp + bperm_d(snd, xa[st]);
+            }
+        }
+        v[0] += bperm_d(v[0], xa[5]);
+        double* red = s_tab;                 // wave scratch (>= 32 doubles)
+        const int j = ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 +
+                      ((lane >> 2) & 1) * 2 + ((lane >> 1) & 1);
+        wave_sync();
+        if (!(lane & 1)) red[j] = v[0];
+        wave_sync();
+        n = 0;
+        auto get = [&]() { return red[n++]; };
+        tot_c = get();
+        if (NPA) { kap.x = get(); kap.y = get(); }
+        if (NPB) { tot_kB.x = get(); tot_kB.y = get(); }
+#pragma unroll
+        for (int q = 0; q < NA; ++q) {
+            tot_muA[q].x = get(); tot_muA[q].y = get(); nu[q] = get();
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb) { tot_X[q][bb].x = get(); tot_X[q][bb].y = get(); }
+        }
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) { tot_mB[bb].x = get(); tot_mB[bb].y = get(); tot_nB[bb] = get(); }
     }
-#pragma unroll
-    for (int bb = 0; bb < NB; ++bb) { tot_mB[bb] = wsumc(tot_mB[bb]); tot_nB[bb] = wsum(tot_nB[bb]); }
     if (lane == 0) {
         const double iz = 1.0 / tot_c;
         cd m[NT];
@@ -1023,6 +1080,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
 // ============================================================================
 struct PrepConst {
     int B, Td, P, M, lm, nkt, stride;
+    int uni;           // wave-uniform theta loads (SBCE_PREP_UNI=0 disables: A/B runs)
     double reg;
 };
 
@@ -1041,14 +1099,28 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
     for (int q = 0; q < NT; ++q)
 #pragma unroll
         for (int r = 0; r < NR; ++r) H[q][r] = czero();
-    const cd* th = a.theta + (size_t)b * c.P * NO;
     const cd* ps = a.psid + (size_t)gsym * c.P;
-    for (int p = 0; p < c.P; ++p) {
-        const cd psi = ps[p];
+    // the wave's 64 symbols normally belong to one trial: theta's address is then
+    // wave-uniform and its loads go through the scalar cache (one vector load per p)
+    const int b0 = __builtin_amdgcn_readfirstlane(b);
+    if (c.uni && __all(b == b0)) {
+        const cd* th = a.theta + (size_t)b0 * c.P * NO;
+        for (int p = 0; p < c.P; ++p) {
+            const cd psi = ps[p];
 #pragma unroll
-        for (int q = 0; q < NT; ++q)
+            for (int q = 0; q < NT; ++q)
 #pragma unroll
-            for (int r = 0; r < NR; ++r) H[q][r] = cfma(H[q][r], psi, th[p * NO + q * NR + r]);
+                for (int r = 0; r < NR; ++r) H[q][r] = cfma(H[q][r], psi, th[p * NO + q * NR + r]);
+        }
+    } else {
+        const cd* th = a.theta + (size_t)b * c.P * NO;
+        for (int p = 0; p < c.P; ++p) {
+            const cd psi = ps[p];
+#pragma unroll
+            for (int q = 0; q < NT; ++q)
+#pragma unroll
+                for (int r = 0; r < NR; ++r) H[q][r] = cfma(H[q][r], psi, th[p * NO + q * NR + r]);
+        }
     }
     cd y[NR];
 #pragma unroll
@@ -1239,6 +1311,8 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     c.prune = !(pr && pr[0] == '0');
     const char* cnt = getenv("SBCE_ESTEP_COUNT");
     c.count = cnt && cnt[0] == '1';
+    const char* rd = getenv("SBCE_ESTEP_RED");
+    c.red_old = rd && rd[0] == 'o';
     c.tab_d = (c.tab_d + 1) / 2 * 2;          // keep 16-B alignment per wave
     c.inv_s2 = 1.0 / (pb.varn * pb.varn);
     c.thr_d = kSkipThr * pb.varn * pb.varn;
@@ -1419,6 +1493,8 @@ hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStre
             PrepConst pc;
             pc.B = pb.B; pc.Td = pb.Td; pc.P = pb.P; pc.M = pb.M; pc.lm = mc.lm;
             pc.nkt = mc.JB >> 4; pc.stride = mc.prep_stride; pc.reg = mc.reg;
+            const char* un = getenv("SBCE_PREP_UNI");
+            pc.uni = !(un && un[0] == '0');
             const long nsym = (long)pb.B * pb.Td;
             const dim3 pg((unsigned)((nsym + 255) / 256)), pblk(256);
             hipError_t e = hipErrorInvalidValue;
