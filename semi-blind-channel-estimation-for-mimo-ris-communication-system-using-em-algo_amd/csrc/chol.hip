@@ -777,7 +777,7 @@ __device__ __forceinline__ void load_tile16(const cd* R, int L, int row0, int c0
 // sub-panel's y block yb.  Returns X[li][lk + 4q] in xv (the A-operand layout of k-step q).
 __device__ __forceinline__ void trsm_tile16(cd* R, cd* y, const cd* Di, const cd* X, const cd* yb,
                                             int L, int NR, int row0, int c0, int w, int li,
-                                            int lk, cd* xv) {
+                                            int lk, cd* xv, const cd* yv) {
     d4v xre = {0.0, 0.0, 0.0, 0.0}, xim = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int s2 = 0; s2 < NB / 4; ++s2) {
@@ -797,8 +797,8 @@ __device__ __forceinline__ void trsm_tile16(cd* R, cd* y, const cd* Di, const cd
         xv[q] = cmk(xre[q], xim[q]);
         if (live && j < w) crow[j] = xv[q];
     }
-    // y[row0+li] -= sum_j X[li][j] y_blk[j]: 4 columns per lane, reduced over lk; all
-    // right-hand sides of the row read and written together
+    // y[row0+li] -= sum_j X[li][j] y_blk[j]: 4 columns per lane, reduced over lk; lane
+    // (li, lk) then owns right-hand sides r = lk + 4m of row li, prefetched in yv[m]
     for (int r0 = 0; r0 < NR; r0 += 4) {                     // 4 right-hand sides per pass
         cd p[4];
 #pragma unroll
@@ -812,15 +812,21 @@ __device__ __forceinline__ void trsm_tile16(cd* R, cd* y, const cd* Di, const cd
                 p[rr].x += shfl_xor_d(p[rr].x, 32); p[rr].y += shfl_xor_d(p[rr].y, 32);
             }
         }
-        if (lk == 0 && live) {
-            cd* yr = y + (size_t)(row0 + li) * NR + r0;
-            cd yo[4];
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) yo[rr] = (r0 + rr < NR) ? yr[rr] : czero();
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr)
-                if (r0 + rr < NR) yr[rr] = csub(yo[rr], p[rr]);
+        const int r = r0 + lk;
+        if (live && r < NR) {
+            const cd pm = csel(lk == 0, p[0], csel(lk == 1, p[1], csel(lk == 2, p[2], p[3])));
+            y[(size_t)(row0 + li) * NR + r] = csub(yv[r0 >> 2], pm);
         }
+    }
+}
+
+// the y rows of a 16-row tile for trsm_tile16: lane (li, lk) holds r = lk + 4m of row li
+__device__ __forceinline__ void load_yrows(const cd* y, int L, int NR, int row0, int li, int lk,
+                                           bool on, cd* yv) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const int r = lk + 4 * m;
+        yv[m] = (on && row0 + li < L && r < NR) ? y[(size_t)(row0 + li) * NR + r] : czero();
     }
 }
 
@@ -857,8 +863,9 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
     __syncthreads();
     cd xv[4];
     if (wave == 0) {
-        cd t1[4];
+        cd t1[4], y1[2];
         load_tile16(R, L, jbB, jb, wA, lane, ntile > 1, t1);        // row tile 1, A part
+        load_yrows(y, L, NR, jbB, li, lk, ntile > 1, y1);
         for (int e = lane; e < NB * NB; e += 64) {
             const int rr = e >> 4, c = e & 15;
             X[e] = (rr < wA && c <= rr) ? R[(size_t)(jb + rr) * L + jb + c] : czero();
@@ -876,7 +883,7 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
 #pragma unroll
             for (int h = 0; h < 4; ++h) X[lane + 64 * h] = t1[h];
             wave_sync();
-            trsm_tile16(R, y, DiA, X, ybA, L, NR, jbB, jb, wA, li, lk, xv);
+            trsm_tile16(R, y, DiA, X, ybA, L, NR, jbB, jb, wA, li, lk, xv, y1);
 #pragma unroll
             for (int q = 0; q < 4; ++q) XA1[li * NB + lk + 4 * q] = xv[q];
         }
@@ -916,9 +923,10 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
         }
     } else if (trsm) {
         // row tiles tau >= 2: TRSM against D_A, in-panel update of their B part
-        cd cur[4];
+        cd cur[4], ycur[2];
         int tau = 1 + wave;
         load_tile16(R, L, jb + tau * NB, jb, wA, lane, tau < ntile, cur);
+        load_yrows(y, L, NR, jb + tau * NB, li, lk, tau < ntile, ycur);
         for (; tau < ntile; tau += 3) {
             const int row0 = jb + tau * NB;
 #pragma unroll
@@ -935,9 +943,12 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
                     }
                 }
             }
+            const cd yv0 = ycur[0], yv1 = ycur[1];
             load_tile16(R, L, row0 + 3 * NB, jb, wA, lane, tau + 3 < ntile, cur);   // next
+            load_yrows(y, L, NR, row0 + 3 * NB, li, lk, tau + 3 < ntile, ycur);
             wave_sync();
-            trsm_tile16(R, y, DiA, X, ybA, L, NR, row0, jb, wA, li, lk, xv);
+            const cd yv[2] = {yv0, yv1};
+            trsm_tile16(R, y, DiA, X, ybA, L, NR, row0, jb, wA, li, lk, xv, yv);
             if (wB > 0) {
 #pragma unroll
                 for (int s2 = 0; s2 < 4; ++s2) {
@@ -959,16 +970,19 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
     __syncthreads();
     if (wB > 0 && trsm) {
         // row tiles tau >= 2: TRSM of the updated B part against D_B
-        cd cur[4];
+        cd cur[4], ycur[2];
         int tau = 2 + wave;
         load_tile16(R, L, jb + tau * NB, jbB, wB, lane, tau < ntile, cur);
+        load_yrows(y, L, NR, jb + tau * NB, li, lk, tau < ntile, ycur);
         for (; tau < ntile; tau += 4) {
             const int row0 = jb + tau * NB;
 #pragma unroll
             for (int h = 0; h < 4; ++h) X[lane + 64 * h] = cur[h];
+            const cd yv[2] = {ycur[0], ycur[1]};
             load_tile16(R, L, row0 + 4 * NB, jbB, wB, lane, tau + 4 < ntile, cur);
+            load_yrows(y, L, NR, row0 + 4 * NB, li, lk, tau + 4 < ntile, ycur);
             wave_sync();
-            trsm_tile16(R, y, DiB, X, ybB, L, NR, row0, jbB, wB, li, lk, xv);
+            trsm_tile16(R, y, DiB, X, ybB, L, NR, row0, jbB, wB, li, lk, xv, yv);
             wave_sync();
         }
     }
