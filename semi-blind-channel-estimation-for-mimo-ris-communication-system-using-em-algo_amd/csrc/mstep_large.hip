@@ -125,7 +125,10 @@ __device__ __forceinline__ void pair_of(int pi, int& p, int& q) {
     q = pi - x * (x + 1) / 2;
 }
 
-template <int NT, int TPW, int TC>
+// STR > 0: compile-time LDS row stride (every block stages <= STR phases per symbol):
+// the main loop's LDS reads take immediate offsets and the staging needs no index division.
+// STR = 0: row stride = the block's phase count (any P).
+template <int NT, int TPW, int TC, int STR>
 __global__ __launch_bounds__(256) void rbuild_herm_kernel(MstepArgs a, int B, int P, int Tp,
                                                           int Td, int L, int G, int smax) {
     constexpr int NC = NT * NT;                 // real columns of the Hermitian S
@@ -134,8 +137,8 @@ __global__ __launch_bounds__(256) void rbuild_herm_kernel(MstepArgs a, int B, in
     constexpr int MS = NT + NT * NT;
     static_assert(NC % 16 == 0, "rbuild_herm: NT in {4, 8}");
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    cd* s_psi = reinterpret_cast<cd*>(smem);                    // [TC][cnt] + 64 pad
-    double* s_S = reinterpret_cast<double*>(s_psi + TC * smax + 64);   // [TC][NC]
+    cd* s_psi = reinterpret_cast<cd*>(smem);                    // [TC][STR or cnt] + 64 pad
+    double* s_S = reinterpret_cast<double*>(s_psi + (STR > 0 ? TC * STR : TC * smax + 64));
 
     const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
     const int b = (slot / G) * 8 + xcd, g = slot - (slot / G) * G;
@@ -176,6 +179,10 @@ __global__ __launch_bounds__(256) void rbuild_herm_kernel(MstepArgs a, int B, in
         pair_of(pi, p, q);
         sp[u] = (p <= hi1 ? p - lo1 : n1 + p - lo2) * (int)sizeof(cd);
         sq[u] = (q <= hi1 ? q - lo1 : n1 + q - lo2) * (int)sizeof(cd);
+        if (STR > 0) {                            // + this lane's symbol row lk
+            sp[u] += lk * STR * (int)sizeof(cd);
+            sq[u] += lk * STR * (int)sizeof(cd);
+        }
     }
     // S staging: thread -> fixed (symbol-in-chunk, column) slots; its source offset in S_t
     constexpr int SR = (TC * NC + 255) / 256;
@@ -209,24 +216,43 @@ __global__ __launch_bounds__(256) void rbuild_herm_kernel(MstepArgs a, int B, in
     const int ne = TC * cnt;
     for (int t0 = 0; t0 < T; t0 += TC) {
         __syncthreads();
-        // phases: LDS image linear in e = tt cnt + k, filled by LDS-DMA (global_load_lds,
-        // lane-linear destination, per-lane source): every load of the chunk in flight at
-        // once instead of a chain of L2 round trips; lanes past the image end land in the
-        // 64-entry pad, symbols past T read a valid dummy (their S columns are 0)
-        for (int e0 = wave * 64; e0 < ne; e0 += 256) {
-            const int e = e0 + lane;
-            int tt = (int)((float)e * rcnt);
-            int k = e - tt * cnt;
-            if (k < 0) { --tt; k += cnt; }
-            if (k >= cnt) { ++tt; k -= cnt; }
-            const int x = k < n1 ? lo1 + k : lo2 + (k - n1);
-            const int t = t0 + tt;
-            const cd* src = psd;
-            if (e < ne && t < Td) src = psd + (size_t)t * P + x;
-            else if (e < ne && t < T) src = psp + (size_t)(t - Td) * P + x;
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                             (__attribute__((address_space(3))) void*)(s_psi + e0),
-                                             16, 0, 0);
+        if constexpr (STR > 0) {
+            // phases: row tt of the LDS image holds the block's cnt (<= STR) phases of symbol
+            // t0 + tt; one LDS-DMA wave-instruction per (row, 64-slot segment), the second
+            // segment ending at cnt (overlapping the first: identical values)
+            for (int sg = 0; sg < (cnt > 64 ? 2 : 1); ++sg) {
+                const int kb = sg ? cnt - 64 : 0;
+                const int kk = min(kb + lane, cnt - 1);
+                const int x = kk < n1 ? lo1 + kk : lo2 + (kk - n1);
+                for (int tt = wave; tt < TC; tt += 4) {
+                    const int t = t0 + tt;
+                    const cd* rowp = t < Td ? psd + (size_t)t * P
+                                            : (t < T ? psp + (size_t)(t - Td) * P : psd);
+                    __builtin_amdgcn_global_load_lds(
+                        (const __attribute__((address_space(1))) void*)(rowp + x),
+                        (__attribute__((address_space(3))) void*)(s_psi + tt * STR + kb), 16, 0, 0);
+                }
+            }
+        } else {
+            // phases: LDS image linear in e = tt cnt + k, filled by LDS-DMA (global_load_lds,
+            // lane-linear destination, per-lane source): every load of the chunk in flight at
+            // once instead of a chain of L2 round trips; lanes past the image end land in the
+            // 64-entry pad, symbols past T read a valid dummy (their S columns are 0)
+            for (int e0 = wave * 64; e0 < ne; e0 += 256) {
+                const int e = e0 + lane;
+                int tt = (int)((float)e * rcnt);
+                int k = e - tt * cnt;
+                if (k < 0) { --tt; k += cnt; }
+                if (k >= cnt) { ++tt; k -= cnt; }
+                const int x = k < n1 ? lo1 + k : lo2 + (k - n1);
+                const int t = t0 + tt;
+                const cd* src = psd;
+                if (e < ne && t < Td) src = psd + (size_t)t * P + x;
+                else if (e < ne && t < T) src = psp + (size_t)(t - Td) * P + x;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                 (__attribute__((address_space(3))) void*)(s_psi + e0),
+                                                 16, 0, 0);
+            }
         }
 #pragma unroll
         for (int r = 0; r < SR; ++r) {
@@ -249,7 +275,9 @@ __global__ __launch_bounds__(256) void rbuild_herm_kernel(MstepArgs a, int B, in
 #pragma unroll
         for (int s4 = 0; s4 < TC / 4; ++s4) {
             const int tt = 4 * s4 + lk;
-            const char* row = s_psib + tt * cnt * (int)sizeof(cd);
+            // STR > 0: lane base + a compile-time offset per s4
+            const char* row = STR > 0 ? s_psib + 4 * s4 * STR * (int)sizeof(cd)
+                                      : s_psib + tt * cnt * (int)sizeof(cd);
             double bv[NCT];
 #pragma unroll
             for (int v = 0; v < NCT; ++v) bv[v] = s_S[tt * NC + 16 * v + li];
@@ -265,7 +293,22 @@ __global__ __launch_bounds__(256) void rbuild_herm_kernel(MstepArgs a, int B, in
             }
         }
     }
-    // epilogue: lane holds pairs lk + 4 q4 of each tile, column li
+    // epilogue: lane holds pairs lk + 4 q4 of each tile, column li (p, q stepped from one
+    // pair_of: consecutive rows of the p-major pair order)
+    int ep[TPW][4], eq[TPW][4];
+    {
+        int p, q;
+        pair_of(min(pi0 + wave * TPW * 16 + lk, pi1), p, q);
+#pragma unroll
+        for (int u = 0; u < TPW; ++u)
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                ep[u][q4] = p;
+                eq[u][q4] = q;
+                q += 4;
+                while (q > p) { q -= p + 1; ++p; }
+            }
+    }
     cd* R = a.R + (size_t)b * L * L;
     const int comp = li >> 3;
 #pragma unroll
@@ -287,11 +330,8 @@ __global__ __launch_bounds__(256) void rbuild_herm_kernel(MstepArgs a, int B, in
                     im = comp ? pim - orr : oi + pr;
                 }
                 const int pi = pi0 + (wave * TPW + u) * 16 + lk + 4 * q4;
-                if (pi <= pi1) {
-                    int p, q;
-                    pair_of(pi, p, q);
-                    R[(size_t)(p * NT + ri) * L + q * NT + cj] = cmk(re, im);
-                }
+                if (pi <= pi1)
+                    R[(size_t)(ep[u][q4] * NT + ri) * L + eq[u][q4] * NT + cj] = cmk(re, im);
             }
     }
 }
@@ -555,15 +595,17 @@ hipError_t launch_pilot_factor(const Problem& pb, const MstepArgs& a, hipStream_
     return hipGetLastError();
 }
 
-template <int NT, int TPW, int TC>
+template <int NT, int TPW, int TC, int STR>
 static hipError_t launch_herm(const Problem& pb, const MstepArgs& a, int smax, hipStream_t s) {
     constexpr int PPB = 4 * TPW * 16;
     const int npairs = pb.P * (pb.P + 1) / 2;
     const int G = (npairs + PPB - 1) / PPB;
     const long nblk = 8L * ((pb.B + 7) / 8) * G;
-    const size_t lds = (size_t)(TC * smax + 64) * sizeof(cd) + (size_t)TC * NT * NT * sizeof(double);
+    const size_t lds = (size_t)(STR > 0 ? TC * STR : TC * smax + 64) * sizeof(cd) +
+                       (size_t)TC * NT * NT * sizeof(double);
+    if (STR > 0 && smax > STR) return hipErrorInvalidValue;
     if (nblk > 0x7fffffffL || lds > 160 * 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((rbuild_herm_kernel<NT, TPW, TC>), dim3((unsigned)nblk), dim3(256), lds, s, a,
+    hipLaunchKernelGGL((rbuild_herm_kernel<NT, TPW, TC, STR>), dim3((unsigned)nblk), dim3(256), lds, s, a,
                        pb.B, pb.P, pb.Tp, pb.Td, pb.L, G, smax);
     return hipGetLastError();
 }
@@ -572,11 +614,13 @@ hipError_t launch_rbuild_herm(const Problem& pb, const MstepArgs& a, hipStream_t
     // staged phases per block <= min(P, pairs per block + 1) (two p-major index segments)
     if (pb.NT == 4) {
         const int smax = pb.P < 257 ? pb.P : 257;
-        return smax <= 130 ? launch_herm<4, 4, 32>(pb, a, smax, s) : launch_herm<4, 4, 8>(pb, a, smax, s);
+        if (smax <= 68) return launch_herm<4, 4, 32, 68>(pb, a, smax, s);
+        return smax <= 130 ? launch_herm<4, 4, 32, 0>(pb, a, smax, s)
+                           : launch_herm<4, 4, 8, 0>(pb, a, smax, s);
     }
     if (pb.NT == 8) {
         const int smax = pb.P < 65 ? pb.P : 65;
-        return launch_herm<8, 1, 16>(pb, a, smax, s);
+        return launch_herm<8, 1, 16, 68>(pb, a, smax, s);
     }
     return hipErrorInvalidValue;
 }
