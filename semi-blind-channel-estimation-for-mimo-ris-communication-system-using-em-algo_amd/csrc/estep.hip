@@ -515,7 +515,6 @@ struct MfmaConst {
     int prune;                 // column-tile bounds on (SBCE_ESTEP_PRUNE=0 disables: A/B runs)
     int count;                 // diagnostic MFMA count (SBCE_ESTEP_COUNT=1)
     int prep_stride;           // doubles per symbol of EstepArgs::prep
-    int red_old;               // A/B: six-step butterfly per value (SBCE_ESTEP_RED=old)
 };
 
 // V16 (M == 16, NA == 2): the A operand's V term, V[kk][i & 15] = V[kk][lane & 15], is the
@@ -721,7 +720,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     {
         wave_sync();
         for (int e = lane; e < c.M * 4 * STEPS; e += 64) {
-            const int kk = e / c.M, sx = e - kk * c.M;
+            const int kk = e >> c.lm, sx = e & mask;
             double u = 0.0, v = 0.0, q2 = 0.0;
             if (kk < K2) {
                 const int r = kk >> 1;
@@ -815,6 +814,36 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
         bool touched = false;       // wave-uniform: an exp was taken in this column tile
 
         for (int i0 = 0; i0 < c.JA; i0 += c.chunk) {
+            if (!table_ready && V16) {
+                // ---- alpha[s0*16 + s1] = 0.25 ||U_s0 + V_s1||^2
+                //      = 0.25 (|U_s0|^2 + |V_s1|^2) + 0.5 U_s0 . V_s1: the cross terms are a
+                //      16 x 16 x K2 real GEMM (STEPS MFMAs, B operand = vreg); stored as
+                //      s_al[s0*16 + (s1 & 3)*4 + (s1 >> 2)] so that a tile's accumulator init
+                //      (rows rq + 4j) is two 16-byte reads ----
+                wave_sync();
+                double nrm = 0.0;
+                const double* T = lane < 16 ? s_U : s_V;
+#pragma unroll
+                for (int kk = 0; kk < K2; ++kk) {
+                    const double v = T[kk * 16 + (lane & 15)];
+                    nrm = fma(v, v, nrm);
+                }
+                if (lane < 32) s_tab[lane] = nrm;
+                d4v cx = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int s = 0; s < STEPS; ++s)
+                    cx = __builtin_amdgcn_mfma_f64_16x16x4f64(s_U[(4 * s + rq) * 16 + col], vreg[s],
+                                                              cx, 0, 0, 0);
+                wave_sync();
+                const double nvv = s_tab[16 + col];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int s0 = rq + 4 * j;
+                    s_al[s0 * 16 + (col & 3) * 4 + (col >> 2)] = 0.25 * (s_tab[s0] + nvv) + 0.5 * cx[j];
+                }
+                wave_sync();
+                table_ready = true;
+            }
             if (!table_ready) {
                 // ---- alpha_i = ||p_i||^2 for entries i0 .. i0+chunk-1 from U, V ----
                 wave_sync();
@@ -840,9 +869,16 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                 ++groups;
                 d4v acc[TU];
 #pragma unroll
-                for (int u = 0; u < TU; ++u)
+                for (int u = 0; u < TU; ++u) {
+                    if (V16) {            // rows rq + 4j of tile tg + u: 4 consecutive doubles
+                        const cd lo = *reinterpret_cast<const cd*>(s_al + (tg + u) * 16 + rq * 4);
+                        const cd hi = *reinterpret_cast<const cd*>(s_al + (tg + u) * 16 + rq * 4 + 2);
+                        acc[u] = d4v{lo.x, lo.y, hi.x, hi.y};
+                    } else {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[u][j] = s_al[(tg + u) * 16 + rq + 4 * j];
+                        for (int j = 0; j < 4; ++j) acc[u][j] = s_al[(tg + u) * 16 + rq + 4 * j];
+                    }
+                }
 #pragma unroll
                 for (int s = 0; s < STEPS; ++s)
 #pragma unroll
@@ -967,26 +1003,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     int xa[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) xa[i] = (lane ^ (32 >> i)) << 2;
-    if (c.red_old) {
-        auto wsum = [&](double v) {
-#pragma unroll
-            for (int i = 0; i < 6; ++i) v += bperm_d(v, xa[i]);
-            return v;
-        };
-        auto wsumc = [&](cd v) { return cmk(wsum(v.x), wsum(v.y)); };
-        tot_c = wsum(tot_c);
-        kap = wsumc(kap);
-        tot_kB = wsumc(tot_kB);
-#pragma unroll
-        for (int q = 0; q < NA; ++q) {
-            tot_muA[q] = wsumc(tot_muA[q]);
-            nu[q] = wsum(nu[q]);
-#pragma unroll
-            for (int bb = 0; bb < NB; ++bb) tot_X[q][bb] = wsumc(tot_X[q][bb]);
-        }
-#pragma unroll
-        for (int bb = 0; bb < NB; ++bb) { tot_mB[bb] = wsumc(tot_mB[bb]); tot_nB[bb] = wsum(tot_nB[bb]); }
-    } else {
+    {
         // Reduce-scatter by recursive halving: at the step with lane offset o a lane keeps the
         // half of the remaining values selected by its bit o and receives the partner's copy
         // of that half (32 + 16 + ... doubles moved instead of 6 per value); value j ends in
@@ -1027,46 +1044,34 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
         wave_sync();
         if (!(lane & 1)) red[j] = v[0];
         wave_sync();
-        n = 0;
-        auto get = [&]() { return red[n++]; };
-        tot_c = get();
-        if (NPA) { kap.x = get(); kap.y = get(); }
-        if (NPB) { tot_kB.x = get(); tot_kB.y = get(); }
-#pragma unroll
-        for (int q = 0; q < NA; ++q) {
-            tot_muA[q].x = get(); tot_muA[q].y = get(); nu[q] = get();
-#pragma unroll
-            for (int bb = 0; bb < NB; ++bb) { tot_X[q][bb].x = get(); tot_X[q][bb].y = get(); }
-        }
-#pragma unroll
-        for (int bb = 0; bb < NB; ++bb) { tot_mB[bb].x = get(); tot_mB[bb].y = get(); tot_nB[bb] = get(); }
-    }
-    if (lane == 0) {
-        const double iz = 1.0 / tot_c;
-        cd m[NT];
-        cd Sm[NT][NT];
-#pragma unroll
-        for (int q = 0; q < NA; ++q) { m[q] = cscale(tot_muA[q], iz); Sm[q][q] = cmk(nu[q] * iz, 0.0); }
-#pragma unroll
-        for (int bb = 0; bb < NB; ++bb) {
-            m[NA + bb] = cscale(tot_mB[bb], iz);
-            Sm[NA + bb][NA + bb] = cmk(tot_nB[bb] * iz, 0.0);
-        }
-        if (NPA) { Sm[0][NA > 1 ? 1 : 0] = cscale(kap, iz); Sm[NA > 1 ? 1 : 0][0] = cconj(cscale(kap, iz)); }
-        if (NPB) { Sm[NA][NT - 1] = cscale(tot_kB, iz); Sm[NT - 1][NA] = cconj(cscale(tot_kB, iz)); }
-#pragma unroll
-        for (int q = 0; q < NA; ++q)
-#pragma unroll
-            for (int bb = 0; bb < NB; ++bb) {
-                const cd v = cscale(tot_X[q][bb], iz);
-                Sm[q][NA + bb] = v;
-                Sm[NA + bb][q] = cconj(v);
+        // lane o < NT + NT^2 writes output o (m_t, then S_t row-major) from the gathered
+        // totals: numerator at red[ire] (+ i red[iim]), conjugated when cj, times 1/Z
+        if (lane < NT + NT * NT) {
+            constexpr int OFF_KA = 1, OFF_KB = 1 + 2 * NPA;
+            constexpr int BQ = 1 + 2 * NPA + 2 * NPB, SQ = 3 + 2 * NB;
+            constexpr int BB = BQ + NA * SQ;
+            int ire, iim = -1;
+            bool cj = false;
+            if (lane < NT) {
+                ire = lane < NA ? BQ + lane * SQ : BB + 3 * (lane - NA);
+                iim = ire + 1;
+            } else {
+                const int i = (lane - NT) / NT, j = (lane - NT) - (lane - NT) / NT * NT;
+                if (i == j) {
+                    ire = i < NA ? BQ + i * SQ + 2 : BB + 3 * (i - NA) + 2;
+                } else if (i < NA && j < NA) {
+                    ire = OFF_KA; iim = OFF_KA + 1; cj = i > j;
+                } else if (i >= NA && j >= NA) {
+                    ire = OFF_KB; iim = OFF_KB + 1; cj = i > j;
+                } else if (i < NA) {
+                    ire = BQ + i * SQ + 3 + 2 * (j - NA); iim = ire + 1;
+                } else {
+                    ire = BQ + j * SQ + 3 + 2 * (i - NA); iim = ire + 1; cj = true;
+                }
             }
-#pragma unroll
-        for (int s2 = 0; s2 < NT; ++s2) {
-            out[s2] = m[s2];
-#pragma unroll
-            for (int s3 = 0; s3 < NT; ++s3) out[NT + s2 * NT + s3] = Sm[s2][s3];
+            const double iz = 1.0 / red[0];
+            const double re = red[ire], im = iim >= 0 ? red[iim] : 0.0;
+            out[lane] = cmk(re * iz, (cj ? -im : im) * iz);
         }
     }
 }
@@ -1311,8 +1316,6 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     c.prune = !(pr && pr[0] == '0');
     const char* cnt = getenv("SBCE_ESTEP_COUNT");
     c.count = cnt && cnt[0] == '1';
-    const char* rd = getenv("SBCE_ESTEP_RED");
-    c.red_old = rd && rd[0] == 'o';
     c.tab_d = (c.tab_d + 1) / 2 * 2;          // keep 16-B alignment per wave
     c.inv_s2 = 1.0 / (pb.varn * pb.varn);
     c.thr_d = kSkipThr * pb.varn * pb.varn;
