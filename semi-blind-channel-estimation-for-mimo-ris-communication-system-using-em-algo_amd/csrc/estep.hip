@@ -515,6 +515,8 @@ struct MfmaConst {
     int prune;                 // column-tile bounds on (SBCE_ESTEP_PRUNE=0 disables: A/B runs)
     int count;                 // diagnostic MFMA count (SBCE_ESTEP_COUNT=1)
     int prep_stride;           // doubles per symbol of EstepArgs::prep
+    int rowb_off;              // offset of the row-tile bound vectors in a prep record
+    int rowb;                  // row-tile bounds on (NT = 4 with a prep record)
 };
 
 // V16 (M == 16, NA == 2): the A operand's V term, V[kk][i & 15] = V[kk][lane & 15], is the
@@ -692,6 +694,12 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                                               c.JB >> 4, s_lb, reinterpret_cast<cd*>(s_tab), lane);
     }
     const double lb_margin = c.prune ? 1e-9 * lb_scale : INFINITY;
+    // row-tile bounds (NT = 4): lane s0 < 16 of a surviving column tile kt evaluates
+    // ||Py - x_s0 Ph_0 - x_kt Ph_2||^2, a lower bound of every hypothesis with first streams
+    // (s0, kt); tile groups whose four bounds all exceed the skip bound are not swept
+    const bool rowb = NT == 4 && V16 && prep && c.rowb;
+    double* s_rb = s_tab + 64;       // [3][NR] complex: P y, P h_0, P h_2 (scratch upper half)
+    if (rowb && lane < 6 * NR) s_rb[lane] = prep[c.rowb_off + lane];
 
     // lane-level accumulators (see VALU kernel)
     double mshift = d0;              // a real hypothesis' distance (candidate_distance)
@@ -807,6 +815,20 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                 bop[s] = v;
             }
         }
+        unsigned rowmask = 0xffffu;
+        if (rowb) {
+            double bnd = INFINITY;
+            if (lane < 16) {
+                const cd x0 = s_cons[lane], x2 = s_cons[kt];
+                const cd* rbv = reinterpret_cast<const cd*>(s_rb);
+                bnd = 0.0;
+#pragma unroll
+                for (int r = 0; r < NR; ++r)
+                    bnd += cabs2(csub(csub(rbv[r], cmul(rbv[NR + r], x0)), cmul(rbv[2 * NR + r], x2)));
+            }
+            const double lim = ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin;
+            rowmask = (unsigned)__ballot(bnd <= lim);
+        }
         double ck = 0.0;
         cd mu[NA];
 #pragma unroll
@@ -866,6 +888,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
             for (int tg = 0; tg < ntile_chunk; tg += TU) {
                 // TU independent 16x16 tiles in flight: STEPS*TU MFMAs per group;
                 // accumulators start at alpha_i, gamma_k (lane constant) stays outside
+                if (V16 && !((rowmask >> tg) & ((1u << TU) - 1u))) continue;
                 ++groups;
                 d4v acc[TU];
 #pragma unroll
@@ -1282,6 +1305,58 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
             lbo[kt] = ok ? lbm : 0.0;
         }
     }
+    // ---- row-tile bound vectors (NT = 4): the block of hypotheses with first streams
+    //      (x_0, x_2) fixed has d >= ||P (y - h_0 x_0 - h_2 x_2)||^2, P = projector onto
+    //      span(h_1, h_3)^perp (x_1, x_3 continuous); a degenerate basis gives P = 0 ----
+    if constexpr (NT == 4) {
+        cd u[2][NR];
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            cd v[NR];
+            double h2 = 0.0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) { v[r] = H[2 * q + 1][r]; h2 += cabs2(v[r]); }
+#pragma unroll
+            for (int rep = 0; rep < 2; ++rep)
+#pragma unroll
+                for (int j = 0; j < q; ++j) {
+                    cd pj = czero();
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) pj = cfmac(pj, v[r], u[j][r]);
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) v[r] = csub(v[r], cmul(u[j][r], pj));
+                }
+            double n2 = 0.0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) n2 += cabs2(v[r]);
+            ok = ok && h2 > 0.0 && n2 > 1e-6 * h2;
+            const double inv = ok ? fast_rsqrt(n2) : 0.0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) u[q][r] = cscale(v[r], inv);
+        }
+        cd w[3][NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) { w[0][r] = y[r]; w[1][r] = H[0][r]; w[2][r] = H[2][r]; }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                cd pw = czero();
+#pragma unroll
+                for (int r = 0; r < NR; ++r) pw = cfmac(pw, w[m][r], u[j][r]);
+#pragma unroll
+                for (int r = 0; r < NR; ++r) w[m][r] = csub(w[m][r], cmul(u[j][r], pw));
+            }
+        double* rbo = out + 4 + 2 * NO + ((c.nkt + 1) / 2 * 2);
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                rbo[2 * (m * NR + r)] = ok ? w[m][r].x : 0.0;
+                rbo[2 * (m * NR + r) + 1] = ok ? w[m][r].y : 0.0;
+            }
+    }
 }
 
 template <int NT, int NR, int MODE, int TU, bool V16 = false>
@@ -1320,7 +1395,12 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     c.inv_s2 = 1.0 / (pb.varn * pb.varn);
     c.thr_d = kSkipThr * pb.varn * pb.varn;
     c.reg = 0.1 * pb.varn * pb.varn;
-    c.prep_stride = 4 + 2 * NO + c.nkt_pad;
+    // NT = 4: + the row-tile bound vectors P y, P h_0, P h_2 (P = projector onto
+    // span(h_1, h_3)^perp), 3 NR complex
+    c.rowb_off = 4 + 2 * NO + c.nkt_pad;
+    c.prep_stride = c.rowb_off + (pb.NT == 4 ? 6 * pb.NR : 0);
+    const char* rb = getenv("SBCE_ESTEP_ROWB");          // "0": off (A/B runs)
+    c.rowb = pb.NT == 4 && c.prune && !(rb && rb[0] == '0');
     lds = 64 * sizeof(cd) + (size_t)kMfmaWaves * c.tab_d * sizeof(double);
     const long nsym = (long)pb.B * pb.Td;
     blocks = (nsym + kMfmaWaves - 1) / kMfmaWaves;
