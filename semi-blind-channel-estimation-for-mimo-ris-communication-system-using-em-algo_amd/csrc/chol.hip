@@ -385,6 +385,15 @@ __device__ __forceinline__ void back_substitute_pf(const cd* R, cd* y, int L, in
     // dblk: LDS [NB][NB] scratch for the diagonal block (its rows hold L[c][c] on the
     // diagonal and conj(Di[c2][c]) above it), loaded by the whole workgroup at once
     const int nblk = (L + NB - 1) / NB;
+    // diagonal blocks are prefetched one step ahead (one entry per thread when nth >= 256)
+    const bool pf = nth >= NB * NB;
+    auto dload = [&](int kb) {
+        const int k0 = kb * NB, w = (L - k0) < NB ? (L - k0) : NB;
+        const int c = (tid >> 4) & 15, c2 = tid & 15;
+        return (kb >= 0 && tid < NB * NB && c < w && c2 < w && c2 >= c)
+                   ? R[(size_t)(k0 + c) * ld + k0 + c2] : czero();
+    };
+    cd dnext = pf ? dload(nblk - 1) : czero();
     for (int kb = nblk - 1; kb >= kb_stop; --kb) {
         const int k0 = kb * NB;
         const int w = (L - k0) < NB ? (L - k0) : NB;
@@ -397,9 +406,14 @@ __device__ __forceinline__ void back_substitute_pf(const cd* R, cd* y, int L, in
             for (int c = 0; c < NB; ++c)
                 lv[h][c] = (k < k0 && c < w) ? R[(size_t)(k0 + c) * ld + k] : czero();
         }
-        for (int e = tid; e < NB * NB; e += nth) {
-            const int c = e >> 4, c2 = e & 15;
-            dblk[e] = (c < w && c2 < w && c2 >= c) ? R[(size_t)(k0 + c) * ld + k0 + c2] : czero();
+        if (pf) {
+            if (tid < NB * NB) dblk[tid] = dnext;
+            dnext = dload(kb - 1);
+        } else {
+            for (int e = tid; e < NB * NB; e += nth) {
+                const int c = e >> 4, c2 = e & 15;
+                dblk[e] = (c < w && c2 < w && c2 >= c) ? R[(size_t)(k0 + c) * ld + k0 + c2] : czero();
+            }
         }
         __syncthreads();
         if (wave == 0) {

@@ -10,6 +10,8 @@
 // and B^H = sum_p u_p y_p^H + sum_t (psi_t (x) m_t) y_t^H  (L x n_rx).
 // The pilot terms are rebuilt every iteration by the reference (:72-74); here
 // they are summed in the same pass as the data terms (never stored).
+#include <stdlib.h>
+
 #include "sbce_internal.h"
 
 namespace sbce {
@@ -143,6 +145,58 @@ __global__ __launch_bounds__(256) void rhs_kernel(MstepArgs a, int B, int P, int
     cd* rhs = a.rhs + ((size_t)b * L + l) * NR;
 #pragma unroll
     for (int r = 0; r < NR; ++r) rhs[r] = acc[r];
+}
+
+// L <= 512: one block per trial, one thread per row l; the phases, moments and observations
+// of TCR symbols at a time are staged in LDS (coalesced), so the symbol loop reads LDS only.
+template <int NR>
+__global__ __launch_bounds__(512) void rhs_lds_kernel(MstepArgs a, int P, int NT, int Tp, int Td,
+                                                      int L, int TCR) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cd* s_ps = reinterpret_cast<cd*>(smem);          // [TCR][P]
+    cd* s_m = s_ps + TCR * P;                        // [TCR][NT]
+    cd* s_y = s_m + TCR * NT;                        // [TCR][NR]
+    const int b = blockIdx.x;
+    if (a.done && a.done[b]) return;
+    const int tid = threadIdx.x, nth = blockDim.x;
+    const bool live = tid < L;
+    const int l = live ? tid : L - 1;
+    const int p = l / NT, ai = l - p * NT;
+    const int MS = NT + NT * NT;
+    cd acc[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc[r] = czero();
+    const cd* up = a.up + (size_t)b * Tp * L;
+    const cd* yp = a.yp + (size_t)b * Tp * NR;
+    for (int tp = 0; tp < Tp; ++tp) {
+        const cd u = up[tp * L + l];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) acc[r] = cfmac(acc[r], u, yp[tp * NR + r]);
+    }
+    const cd* ps = a.psid + (size_t)b * Td * P;
+    const cd* mom = a.mom + (size_t)b * Td * MS;
+    const cd* yd = a.yd + (size_t)b * Td * NR;
+    for (int t0 = 0; t0 < Td; t0 += TCR) {
+        const int tc = (Td - t0) < TCR ? (Td - t0) : TCR;
+        __syncthreads();
+        for (int e = tid; e < tc * P; e += nth) s_ps[e] = ps[(size_t)t0 * P + e];
+        for (int e = tid; e < tc * NT; e += nth) {
+            const int tt = e / NT;
+            s_m[e] = mom[(size_t)(t0 + tt) * MS + (e - tt * NT)];
+        }
+        for (int e = tid; e < tc * NR; e += nth) s_y[e] = yd[(size_t)t0 * NR + e];
+        __syncthreads();
+        for (int tt = 0; tt < tc; ++tt) {
+            const cd w = cmul(s_ps[tt * P + p], s_m[tt * NT + ai]);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) acc[r] = cfmac(acc[r], w, s_y[tt * NR + r]);
+        }
+    }
+    if (live) {
+        cd* rhs = a.rhs + ((size_t)b * L + l) * NR;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) rhs[r] = acc[r];
+    }
 }
 
 // ------------------------------------------------------------------ small per-trial kernels
@@ -392,6 +446,19 @@ hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a0, hipStream_
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    const char* rimpl = getenv("SBCE_RHS_IMPL");        // "row": thread-per-row kernel (A/B)
+    if (pb.L <= 512 && !(rimpl && rimpl[0] == 'r')) {
+        const int nth = (pb.L + 63) / 64 * 64;
+        const int tcr = pb.P <= 128 ? 16 : 4;             // <= 33 KB of phases per chunk
+        const size_t lds = (size_t)tcr * (pb.P + pb.NT + pb.NR) * sizeof(cd);
+        switch (pb.NR) {
+#define SBCE_RHSL(n) case n: hipLaunchKernelGGL(rhs_lds_kernel<n>, dim3(pb.B), dim3(nth), lds, s, a, pb.P, pb.NT, pb.Tp, pb.Td, pb.L, tcr); break;
+            SBCE_RHSL(1) SBCE_RHSL(2) SBCE_RHSL(3) SBCE_RHSL(4) SBCE_RHSL(5) SBCE_RHSL(6) SBCE_RHSL(7) SBCE_RHSL(8)
+#undef SBCE_RHSL
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     dim3 g2((pb.L + 255) / 256, pb.B);
     switch (pb.NR) {
 #define SBCE_RHS(n) case n: hipLaunchKernelGGL(rhs_kernel<n>, g2, dim3(256), 0, s, a, pb.B, pb.P, pb.NT, pb.Tp, pb.Td, pb.L); break;
