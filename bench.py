@@ -60,11 +60,14 @@ ESTEP = {"cfg1": ("soft", 0, "chol"), "plumbing": ("soft", 0, "chol"),
 
 # kernels of one E-step / M-step launch sequence (rocprofv3 names, tools/pmc_summary.py keys)
 ESTEP_KERNELS = ["estep_prep_kernel", "estep_mfma_kernel_occ3", "estep_mfma_kernel"]
-MSTEP_KERNELS = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_kernel", "rhs_kernel",
-                 "chol_mfma_kernel"]
+MSTEP_KERNELS = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_kernel", "rhs_lds_kernel",
+                 "rhs_kernel", "diag_tol_kernel", "panel_update_kernel", "panel_factor_kernel",
+                 "backsub_kernel", "chol_mfma_kernel"]
 MSTEP_KERNELS_LARGE = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_wide_kernel",
                        "rhs_kernel", "diag_tol_kernel", "chol_mfma_kernel", "tile_inverse_kernel",
                        "tile_gemm_kernel", "trisolve_kernel"]
+# launched exactly once per M-step (the divisor of the phase's PMC totals)
+MSTEP_ANCHORS = ["pilot_factor_kernel", "rhs_lds_kernel", "rhs_kernel"]
 
 
 def mstep_flops_per_trial_iter(n_tx, n_rx, N, T_p, T_d):
@@ -273,7 +276,7 @@ def main():
                   "phase": "M-step", "kernels": m_kern, "ms": mstep_ms,
                   "achieved": mflops / (mstep_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
                   "unit": "TFLOP/s", "frac": mflops / (mstep_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-                  "traffic": traffic_of(m_kern, ["rhs_kernel"]), "algorithmic_bytes": mbytes,
+                  "traffic": traffic_of(m_kern, MSTEP_ANCHORS), "algorithmic_bytes": mbytes,
                   "hbm_frac_algorithmic": mbytes / (mstep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                   "flops_per_launch": mflops}
     if mode in ("soft", "hard"):

@@ -62,7 +62,8 @@ def test_workspace_and_validation_without_gpu(sbce):
     Lw = 65 * 4
     expect = (1000 * 256 * 20 * 16 + 1000 * Lw * Lw * 16 + 1000 * Lw * 4 * 16
               + 1000 * 256 * 4 * 16                       # moments, R, rhs, shifted y
-              + 1000 * 256 * (4 + 2 * 16 + 16) * 8        # E-step sweep prep (H_eff, bounds)
+              + 1000 * 256 * (4 + 2 * 16 + 16 + 6 * 4) * 8  # E-step prep (H_eff, bounds,
+                                                            # row-bound vectors)
               + 1000 * 16 * 65 * 16 + 1000 * 16 * 16 * 16  # factored pilots psi', x' x'^H
               + 1000 * 4 + 1000 * 8)                      # pilot flags, pivot thresholds
     assert expect <= n <= expect + 8 * 256 + 4000
