@@ -1287,6 +1287,32 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
         for (int s = 0; s < c.M; ++s) cmax2 = fmax(cmax2, cabs2(a.cons[s]));
         out[2] = sc + NB * cmax2 * g2;
         double* lbo = out + 4 + 2 * NO;
+        if (NB == 2 && c.M == 16) {
+            // tile kt = first B stream b0 fixed, b1 over all 16 symbols:
+            //   ||r0 - g1 x||^2 = ||r0||^2 - 2 Re(conj(x) g1^H r0) + |x|^2 ||g1||^2,
+            //   r0 = w - g0 x_b0  (4 flops per hypothesis instead of NR complex products)
+            double ng = 0.0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) ng += cabs2(g[NB - 1][r]);
+            for (int kt = 0; kt < c.nkt; ++kt) {
+                const cd xb0 = a.cons[kt];
+                double n0 = 0.0;
+                cd aa = czero();
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const cd r0 = csub(w[r], cmul(g[0][r], xb0));
+                    n0 += cabs2(r0);
+                    aa = cfmac(aa, r0, g[NB - 1][r]);          // g1^H r0
+                }
+                double lbm = INFINITY;
+                for (int s1 = 0; s1 < 16; ++s1) {
+                    const cd x = a.cons[s1];
+                    const double lb = fma(cabs2(x), ng, n0 - 2.0 * (x.x * aa.x + x.y * aa.y));
+                    lbm = fmin(lbm, lb);
+                }
+                lbo[kt] = ok ? fmax(lbm, 0.0) : 0.0;
+            }
+        } else
         for (int kt = 0; kt < c.nkt; ++kt) {
             double lbm = INFINITY;
             for (int s = 0; s < 16; ++s) {
