@@ -204,7 +204,10 @@ def test_singular_system_flags_and_drop_mode(sbce):
 
 @pytest.mark.parametrize("shape", [(4, 4, 8, 16, 6, 16, 20), (4, 4, 8, 16, 6, 16, -5),
                                    (2, 4, 6, 8, 24, 16, 15), (3, 2, 3, 8, 20, 16, 20),
-                                   (4, 3, 4, 16, 12, 4, 10), (2, 1, 5, 8, 10, 64, 30)])
+                                   (4, 3, 4, 16, 12, 4, 10), (2, 1, 5, 8, 10, 64, 30),
+                                   # n_tx = 4, 16-QAM with row-tile bounds: 8 receive antennas,
+                                   # and 2 (span(h1, h3) is all of C^2: the bounds are 0)
+                                   (4, 8, 6, 16, 8, 16, 25), (4, 2, 6, 16, 8, 16, 30)])
 def test_mfma_and_valu_estep_agree(sbce, shape, monkeypatch):
     """The FP64-MFMA E-step (with its preparation pass, with in-kernel preparation, and
     with the exact tile bounds disabled) and the VALU E-step compute the same posterior
