@@ -1133,6 +1133,7 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
     const int b0 = __builtin_amdgcn_readfirstlane(b);
     if (c.uni && __all(b == b0)) {
         const cd* th = a.theta + (size_t)b0 * c.P * NO;
+#pragma unroll 8
         for (int p = 0; p < c.P; ++p) {
             const cd psi = ps[p];
 #pragma unroll
