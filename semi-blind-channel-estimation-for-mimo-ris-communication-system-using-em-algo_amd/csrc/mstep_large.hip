@@ -424,15 +424,30 @@ __global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int 
             }
         }
     const double sg = HERK ? -1.0 : 1.0;
+    // operand chunks (TB x KS of A and B) are loaded into registers one chunk ahead: the
+    // global latency of chunk kc + KS overlaps the MFMAs of chunk kc
+    constexpr int PF = TB * KS / 256;               // entries per thread and operand
+    cd pa[PF], pbv[PF];
+    auto fetch = [&](int kc) {
+#pragma unroll
+        for (int h = 0; h < PF; ++h) {
+            const int e = tid + 256 * h, r = e / KS, k = e - r * KS;
+            const bool kin = kc + k < kmax;
+            pa[h] = (kin && r0 + r < L) ? Arow[(size_t)r * L + kc + k] : czero();
+            pbv[h] = (kin && (HERK ? c0 + r < L : true)) ? Brow[(size_t)r * ldb + kc + k] : czero();
+        }
+    };
+    fetch(0);
     for (int kc = 0; kc < TB; kc += KS) {
         __syncthreads();
-        for (int e = tid; e < TB * KS; e += 256) {
-            const int r = e / KS, k = e - r * KS;
-            const bool kin = kc + k < kmax;
-            As[r][k] = (kin && r0 + r < L) ? Arow[(size_t)r * L + kc + k] : czero();
-            Bs[r][k] = (kin && (HERK ? c0 + r < L : true)) ? Brow[(size_t)r * ldb + kc + k] : czero();
+#pragma unroll
+        for (int h = 0; h < PF; ++h) {
+            const int e = tid + 256 * h, r = e / KS, k = e - r * KS;
+            As[r][k] = pa[h];
+            Bs[r][k] = pbv[h];
         }
         __syncthreads();
+        if (kc + KS < TB) fetch(kc + KS);
 #pragma unroll
         for (int s = 0; s < KS / 4; ++s) {
             cd av[2], bv[2];
