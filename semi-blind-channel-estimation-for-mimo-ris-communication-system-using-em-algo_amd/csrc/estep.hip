@@ -778,6 +778,21 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
         // exact column-tile bound (column_tile_bounds): wave-uniform skip of the whole tile
         if (s_lb[kt] > ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin)
             continue;
+        unsigned rowmask = 0xffffu;
+        if (rowb) {
+            double bnd = INFINITY;
+            if (lane < 16) {
+                const cd x0 = s_cons[lane], x2 = s_cons[kt];
+                const cd* rbv = reinterpret_cast<const cd*>(s_rb);
+                bnd = 0.0;
+#pragma unroll
+                for (int r = 0; r < NR; ++r)
+                    bnd += cabs2(csub(csub(rbv[r], cmul(rbv[NR + r], x0)), cmul(rbv[2 * NR + r], x2)));
+            }
+            const double lim = ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin;
+            rowmask = (unsigned)__ballot(bnd <= lim);
+            if (!rowmask) continue;                      // no row tile of this column survives
+        }
         const int k = kt * 16 + col;
         cd xb[NB];
 #pragma unroll
@@ -814,20 +829,6 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                 }
                 bop[s] = v;
             }
-        }
-        unsigned rowmask = 0xffffu;
-        if (rowb) {
-            double bnd = INFINITY;
-            if (lane < 16) {
-                const cd x0 = s_cons[lane], x2 = s_cons[kt];
-                const cd* rbv = reinterpret_cast<const cd*>(s_rb);
-                bnd = 0.0;
-#pragma unroll
-                for (int r = 0; r < NR; ++r)
-                    bnd += cabs2(csub(csub(rbv[r], cmul(rbv[NR + r], x0)), cmul(rbv[2 * NR + r], x2)));
-            }
-            const double lim = ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin;
-            rowmask = (unsigned)__ballot(bnd <= lim);
         }
         double ck = 0.0;
         cd mu[NA];
