@@ -65,7 +65,7 @@ MSTEP_KERNELS = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_kernel", "
                  "backsub_kernel", "chol_mfma_kernel"]
 MSTEP_KERNELS_LARGE = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_wide_kernel",
                        "rhs_kernel", "diag_tol_kernel", "chol_mfma_kernel", "tile_inverse_kernel",
-                       "tile_gemm_kernel", "trisolve_kernel"]
+                       "tile_gemm_kernel", "backdiag_kernel", "backupd_kernel"]
 # launched exactly once per M-step (the divisor of the phase's PMC totals)
 MSTEP_ANCHORS = ["pilot_factor_kernel", "rhs_lds_kernel", "rhs_kernel"]
 

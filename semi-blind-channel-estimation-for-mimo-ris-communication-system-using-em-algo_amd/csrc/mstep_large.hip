@@ -19,8 +19,10 @@
 //     tile_inverse_kernel            W = L_kk^{-1} (64 x 64, workspace);
 //     tile_gemm_kernel<TRSM>         L_ik = A_ik W^H             (i > k);
 //     tile_gemm_kernel<HERK>         A_ij -= L_ik L_jk^H          (i >= j > k);
-//   trisolve_kernel      forward L y = B^H and back L^H x = y, blocked by 16 with the
-//                        diagonal inverses kept in R's strict upper 16 x 16 blocks.
+//   forward L y = B^H fused: tile_inverse_kernel applies W to y_k, each TRSM tile block
+//   subtracts L_ik y_k from its rows; back L^H x = y by column blocks from the last:
+//   backdiag_kernel (diagonal tile, 16-blocks through the inverses kept in R's strict upper
+//   16 x 16 blocks) then backupd_kernel (all earlier row blocks in parallel).
 #include "sbce_internal.h"
 
 namespace sbce {
@@ -353,7 +355,7 @@ __global__ __launch_bounds__(256) void diag_tol_kernel(MstepArgs a, int L) {
 // ---------------------------------------------------------------- W = L_kk^{-1}
 // One wave per trial: lane j forward-substitutes column j of the inverse of the factored
 // w x w diagonal tile (uniform loads of L, column in LDS).  Dropped pivots (0) give 0.
-__global__ __launch_bounds__(64) void tile_inverse_kernel(MstepArgs a, int L, int k0, int w) {
+__global__ __launch_bounds__(64) void tile_inverse_kernel(MstepArgs a, int L, int k0, int w, int NR) {
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -369,6 +371,19 @@ __global__ __launch_bounds__(64) void tile_inverse_kernel(MstepArgs a, int L, in
     }
     cd* W = a.winv + (size_t)b * TB * TB;
     for (int r = 0; r < TB; ++r) W[r * TB + j] = (r < w && j < w) ? col[r][j] : czero();
+    // fused forward substitution: y_k <- W y_k (every earlier block's L_ik y_i has been
+    // subtracted by that block's TRSM launch); lane j owns row j
+    cd* yk = a.rhs + ((size_t)b * L + k0) * NR;
+    cd* ys = reinterpret_cast<cd*>(col + TB);                // [TB][8]
+    for (int e = j; e < w * NR; e += 64) ys[e] = yk[e];
+    __syncthreads();
+    if (j < w) {
+        for (int c = 0; c < NR; ++c) {
+            cd acc = czero();
+            for (int m = 0; m <= j; ++m) acc = cfma(acc, col[j][m], ys[m * NR + c]);
+            yk[j * NR + c] = acc;
+        }
+    }
 }
 
 // ---------------------------------------------------------------- tile GEMM
@@ -377,7 +392,7 @@ __global__ __launch_bounds__(64) void tile_inverse_kernel(MstepArgs a, int L, in
 //   HERK (HERK = true):  tile (i, j), C = A_ij - L_ik L_jk^H.
 // 4 waves, wave w owns the 32 x 32 quadrant (w >> 1, w & 1) = 2 x 2 MFMA tiles.
 template <bool HERK>
-__global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int kb) {
+__global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int kb, int NR) {
     __shared__ cd As[TB][KS + 1], Bs[TB][KS + 1];
     const int b = blockIdx.y;
     if (a.done && a.done[b]) return;
@@ -478,14 +493,28 @@ __global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int 
                 if (r < L && c < L && (HERK || c < k0 + kmax))
                     R[(size_t)r * L + c] = cmk(cre[u][v][q], cim[u][v][q]);
             }
+    if (!HERK) {
+        // fused forward substitution: rows r0.. of y -= L_ik y_k (the tile just written)
+        __syncthreads();
+        cd* y = a.rhs + (size_t)b * L * NR;
+        for (int e = tid; e < TB * NR; e += 256) {
+            const int rr = e / NR, c = e - rr * NR;
+            if (r0 + rr >= L) continue;
+            const cd* lrow = R + (size_t)(r0 + rr) * L + k0;
+            cd acc = czero();
+            for (int m = 0; m < kmax; ++m) acc = cfma(acc, lrow[m], y[(size_t)(k0 + m) * NR + c]);
+            y[(size_t)(r0 + rr) * NR + c] = csub(y[(size_t)(r0 + rr) * NR + c], acc);
+        }
+    }
 }
 
-// ---------------------------------------------------------------- triangular solves
-// One workgroup (256 threads = 16 rows x 16 k-lanes) per trial.  Forward L y = B^H and
-// back L^H x = y blocked by 16; the 16 x 16 diagonal blocks are applied through their
-// inverses: Di[c][c] = 1 / L[c][c], Di[c2][c] = conj(R[c][c2]) (c2 > c, chol.hip).
-// y lives in the rhs buffer (L x NR, too large for LDS at cfg 2); theta = conj(x).
-__global__ __launch_bounds__(256) void trisolve_kernel(MstepArgs a, int L, int NR) {
+// ---------------------------------------------------------------- back substitution
+// L^H x = y by 64-column blocks from the last: backdiag_kernel (one workgroup per trial)
+// solves the diagonal tile, x_k = L_kk^{-H} y_k, in 16-row blocks through the inverses kept
+// in R's strict upper 16 x 16 blocks (Di[c][c] = 1 / L[c][c], Di[c2][c] = conj(R[c][c2])),
+// y_k already holding y_k - sum_{i > k} L_ik^H x_i; backupd_kernel then subtracts
+// L_kj^H x_k from every earlier block j in parallel.  theta = conj(x) after the first block.
+__global__ __launch_bounds__(256) void backdiag_kernel(MstepArgs a, int L, int NR, int k0, int w) {
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
     __shared__ cd z[16][8];
@@ -493,108 +522,83 @@ __global__ __launch_bounds__(256) void trisolve_kernel(MstepArgs a, int L, int N
     const cd* R = a.R + (size_t)b * L * L;
     cd* y = a.rhs + (size_t)b * L * NR;
     const int tid = threadIdx.x, rr = tid >> 4, kl = tid & 15;
-    const int nblk = (L + 15) / 16;
-    // ---- forward ----
-    for (int bk = 0; bk < nblk; ++bk) {
-        const int k0 = bk * 16, w = (L - k0) < 16 ? (L - k0) : 16;
+    const int kend = k0 + w;
+    for (int c0 = k0 + (w - 1) / 16 * 16; c0 >= k0; c0 -= 16) {
+        const int wb = (kend - c0) < 16 ? (kend - c0) : 16;
+        const int c = rr;                                   // column of this 16-block
         cd acc[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) acc[r] = czero();
-        if (rr < w) {
-            const cd* row = R + (size_t)(k0 + rr) * L;
-            for (int k = kl; k < k0; k += 16) {
-                const cd l = row[k];
-#pragma unroll
-                for (int r = 0; r < 8; ++r)
-                    if (r < NR) acc[r] = cfma(acc[r], l, y[(size_t)k * NR + r]);
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            for (int off = 8; off >= 1; off >>= 1) {
-                acc[r].x += __shfl_xor(acc[r].x, off);
-                acc[r].y += __shfl_xor(acc[r].y, off);
-            }
-        }
-        // Di of this block (lower): diag 1/L[c][c], strict lower conj(R[c][c2]) transposed
-        {
-            const int c = tid >> 4, c2 = tid & 15;
-            cd v = czero();
-            if (c < w && c2 < w) {
-                if (c2 == c) {
-                    const double d = R[(size_t)(k0 + c) * L + k0 + c].x;
-                    v = cmk(d > 0.0 ? 1.0 / d : 0.0, 0.0);
-                } else if (c2 < c) {
-                    v = cconj(R[(size_t)(k0 + c2) * L + k0 + c]);
-                }
-            }
-            Dl[c][c2] = v;
-        }
-        if (kl == 0 && rr < w) {
-#pragma unroll
-            for (int r = 0; r < 8; ++r)
-                if (r < NR) z[rr][r] = csub(y[(size_t)(k0 + rr) * NR + r], acc[r]);
-        }
-        __syncthreads();
-        if (tid < w * NR) {
-            const int c = tid / NR, r = tid - c * NR;
-            cd s = czero();
-            for (int c2 = 0; c2 <= c; ++c2) s = cfma(s, Dl[c][c2], z[c2][r]);
-            y[(size_t)(k0 + c) * NR + r] = s;
-        }
-        __syncthreads();
-    }
-    // ---- back: x_b = Di_b^H (y_b - sum_{m > b} L[m][b]^H x_m) ----
-    for (int bk = nblk - 1; bk >= 0; --bk) {
-        const int k0 = bk * 16, w = (L - k0) < 16 ? (L - k0) : 16;
-        const int c = rr;                                   // column of this block
-        cd acc[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) acc[r] = czero();
-        if (c < w) {
-            for (int m = k0 + 16 + kl; m < L; m += 16) {
-                const cd l = R[(size_t)m * L + k0 + c];
+        if (c < wb) {
+            for (int m = c0 + 16 + kl; m < kend; m += 16) {
+                const cd l = R[(size_t)m * L + c0 + c];
 #pragma unroll
                 for (int r = 0; r < 8; ++r)
                     if (r < NR) acc[r] = cfmac(acc[r], y[(size_t)m * NR + r], l);
             }
         }
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
+        for (int r = 0; r < 8; ++r)
             for (int off = 8; off >= 1; off >>= 1) {
                 acc[r].x += __shfl_xor(acc[r].x, off);
                 acc[r].y += __shfl_xor(acc[r].y, off);
             }
-        }
         {
             const int cc = tid >> 4, c2 = tid & 15;
             cd v = czero();
-            if (cc < w && c2 < w) {
+            if (cc < wb && c2 < wb) {
                 if (c2 == cc) {
-                    const double d = R[(size_t)(k0 + cc) * L + k0 + cc].x;
+                    const double d = R[(size_t)(c0 + cc) * L + c0 + cc].x;
                     v = cmk(d > 0.0 ? 1.0 / d : 0.0, 0.0);
                 } else if (c2 < cc) {
-                    v = cconj(R[(size_t)(k0 + c2) * L + k0 + cc]);
+                    v = cconj(R[(size_t)(c0 + c2) * L + c0 + cc]);
                 }
             }
             Dl[cc][c2] = v;                                 // Di[cc][c2]
         }
-        if (kl == 0 && c < w) {
+        if (kl == 0 && c < wb) {
 #pragma unroll
             for (int r = 0; r < 8; ++r)
-                if (r < NR) z[c][r] = csub(y[(size_t)(k0 + c) * NR + r], acc[r]);
+                if (r < NR) z[c][r] = csub(y[(size_t)(c0 + c) * NR + r], acc[r]);
         }
         __syncthreads();
-        if (tid < w * NR) {
+        if (tid < wb * NR) {
             const int c1 = tid / NR, r = tid - c1 * NR;
             cd s = czero();                                 // x[c1] = sum_{c2 >= c1} conj(Di[c2][c1]) z[c2]
-            for (int c2 = c1; c2 < w; ++c2) s = cfmac(s, z[c2][r], Dl[c2][c1]);
-            y[(size_t)(k0 + c1) * NR + r] = s;
+            for (int c2 = c1; c2 < wb; ++c2) s = cfmac(s, z[c2][r], Dl[c2][c1]);
+            y[(size_t)(c0 + c1) * NR + r] = s;
         }
         __syncthreads();
     }
-    cd* th = a.theta + (size_t)b * L * NR;
-    for (int e = tid; e < L * NR; e += 256) th[e] = cconj(y[e]);
+    if (k0 == 0) {
+        cd* th = a.theta + (size_t)b * L * NR;
+        for (int e = tid; e < L * NR; e += 256) th[e] = cconj(y[e]);
+    }
+}
+
+// Block (j, trial): y_j -= L_kj^H x_k for row block j < k: the tile (k, j) and x_k staged in
+// LDS (coalesced rows), thread per (row r of y_j, right-hand side).
+__global__ __launch_bounds__(256) void backupd_kernel(MstepArgs a, int L, int NR, int k0, int w) {
+    const int j = blockIdx.x, b = blockIdx.y;
+    if (a.done && a.done[b]) return;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cd(*T)[TB + 1] = reinterpret_cast<cd(*)[TB + 1]>(smem);  // [TB][TB + 1]: T[m][r] = L[k0+m][j0+r]
+    cd* xs = reinterpret_cast<cd*>(smem + (size_t)TB * (TB + 1) * sizeof(cd));   // [TB][NR]
+    const cd* R = a.R + (size_t)b * L * L;
+    cd* y = a.rhs + (size_t)b * L * NR;
+    const int j0 = j * TB, tid = threadIdx.x;
+    for (int e = tid; e < w * TB; e += 256) {
+        const int m = e / TB, r = e - m * TB;
+        T[m][r] = R[(size_t)(k0 + m) * L + j0 + r];
+    }
+    for (int e = tid; e < w * NR; e += 256) xs[e] = y[(size_t)k0 * NR + e];
+    __syncthreads();
+    for (int e = tid; e < TB * NR; e += 256) {
+        const int r = e / NR, c = e - r * NR;
+        cd acc = czero();
+        for (int m = 0; m < w; ++m) acc = cfmac(acc, xs[m * NR + c], T[m][r]);
+        y[(size_t)(j0 + r) * NR + c] = csub(y[(size_t)(j0 + r) * NR + c], acc);
+    }
 }
 
 }  // namespace
@@ -650,19 +654,30 @@ hipError_t launch_chol_large(const Problem& pb, const MstepArgs& a, hipStream_t 
     hipError_t e = launch_diag_tol(pb, a, s);
     if (e != hipSuccess) return e;
     const int nb = (pb.L + TB - 1) / TB;
+    const size_t inv_lds = (size_t)TB * TB * sizeof(cd) + (size_t)TB * 8 * sizeof(cd);
     for (int k = 0; k < nb; ++k) {
         const int k0 = k * TB, w = (pb.L - k0) < TB ? (pb.L - k0) : TB;
         if ((e = launch_chol_tile(pb, a, k0, w, s)) != hipSuccess) return e;
+        // W = L_kk^-1 and the fused forward substitution y_k <- W y_k
+        hipLaunchKernelGGL(tile_inverse_kernel, dim3(pb.B), dim3(64), inv_lds, s, a, pb.L, k0, w,
+                           pb.NR);
         const int below = nb - k - 1;
         if (below == 0) break;
-        hipLaunchKernelGGL(tile_inverse_kernel, dim3(pb.B), dim3(64), TB * TB * sizeof(cd), s, a,
-                           pb.L, k0, w);
-        hipLaunchKernelGGL(tile_gemm_kernel<false>, dim3(below, pb.B), dim3(256), 0, s, a, pb.L, k);
+        hipLaunchKernelGGL(tile_gemm_kernel<false>, dim3(below, pb.B), dim3(256), 0, s, a, pb.L, k,
+                           pb.NR);
         hipLaunchKernelGGL(tile_gemm_kernel<true>, dim3(below * (below + 1) / 2, pb.B), dim3(256),
-                           0, s, a, pb.L, k);
+                           0, s, a, pb.L, k, pb.NR);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(trisolve_kernel, dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR);
+    const size_t upd_lds = (size_t)TB * (TB + 1) * sizeof(cd) + (size_t)TB * 8 * sizeof(cd);
+    for (int k = nb - 1; k >= 0; --k) {
+        const int k0 = k * TB, w = (pb.L - k0) < TB ? (pb.L - k0) : TB;
+        hipLaunchKernelGGL(backdiag_kernel, dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR, k0, w);
+        if (k > 0)
+            hipLaunchKernelGGL(backupd_kernel, dim3(k, pb.B), dim3(256), upd_lds, s, a, pb.L, pb.NR,
+                               k0, w);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     return hipGetLastError();
 }
 
