@@ -151,6 +151,9 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
 
     EstepArgs eas = ea;                      // superimposed pilots: E-step on y - H x_p
     if (p->x_sup) eas.yd = (const cd*)(ws + c.ysh);
+    // the Kronecker factors of the pilot regressors do not change across iterations
+    const bool prefactor = rbuild_herm_supported(pb);
+    if (prefactor && (rc = hip_rc(launch_pilot_factor(pb, ma, s)))) return rc;
     for (int it = 0; it < iters; ++it) {
         if (p->x_sup) {
             if ((rc = hip_rc(launch_sup_shift_y(pb, ea.yd, ea.psid, ea.theta, (const cd*)p->x_sup,
@@ -162,7 +165,7 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
         } else if ((rc = hip_rc(launch_estep(pb, ea, estep_mode, s)))) {
             return rc;
         }
-        if ((rc = hip_rc(launch_mstep_build(pb, ma, s)))) return rc;
+        if ((rc = hip_rc(launch_mstep_build(pb, ma, s, prefactor)))) return rc;
         // Gaussian prior, n_rx = 1: the reference's all-ones covariance term stays in A
         // (MIMO_Gaussian_proposed.py:73-76): R += c 1 1^T
         if (gauss && pb.NR == 1 && (rc = hip_rc(launch_gauss_rank1(pb, ma, s)))) return rc;

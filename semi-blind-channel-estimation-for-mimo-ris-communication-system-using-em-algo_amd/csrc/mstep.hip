@@ -421,14 +421,16 @@ __global__ __launch_bounds__(256) void early_stop_kernel(const cd* theta, const 
 
 }  // namespace
 
-hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a0, hipStream_t s) {
+hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a0, hipStream_t s,
+                              bool pilots_factored) {
     const int npairs = pb.P * (pb.P + 1) / 2;
     MstepArgs a = a0;
-    // NT in {4, 8}: MFMA build from Kronecker-factored pilots (mstep_large.hip), then the
-    // VALU build below re-runs only the trials whose u_p is not a Kronecker product
+    // NT in {4, 8}: MFMA build from Kronecker-factored pilots (mstep_large.hip; the factors
+    // depend on u_p only, so an EM run computes them once), then the VALU build below
+    // re-runs only the trials whose u_p is not a Kronecker product
     const bool herm = rbuild_herm_supported(pb);
     if (herm) {
-        hipError_t e0 = launch_pilot_factor(pb, a, s);
+        hipError_t e0 = pilots_factored ? hipSuccess : launch_pilot_factor(pb, a, s);
         if (e0 == hipSuccess) e0 = launch_rbuild_herm(pb, a, s);
         if (e0 != hipSuccess) return e0;
         a.gate = a.pflag;

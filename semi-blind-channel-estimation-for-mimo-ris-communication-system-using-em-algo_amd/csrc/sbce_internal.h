@@ -151,7 +151,9 @@ hipError_t launch_estep_pm(const Problem& pb, const EstepArgs& a, int mode, int 
 bool estep_pm_supported(const Problem& pb, int partition_r, int mode);
 bool estep_supported(const Problem& pb, int mode);
 int estep_prep_stride(const Problem& pb);   // doubles per symbol, 0 if no MFMA sweep
-hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t s);
+// pilots_factored: launch_pilot_factor already ran for these u_p (ppsi, pS, pflag valid)
+hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t s,
+                              bool pilots_factored = false);
 hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s);
 bool chol_supported(const Problem& pb);
 constexpr int kLargeL = 512;   // L above this: tiled build + blocked right-looking Cholesky
