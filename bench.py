@@ -66,8 +66,9 @@ MSTEP_KERNELS = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_kernel", "
 MSTEP_KERNELS_LARGE = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_wide_kernel",
                        "rhs_kernel", "diag_tol_kernel", "chol_mfma_kernel", "tile_inverse_kernel",
                        "tile_gemm_kernel", "backdiag_kernel", "backupd_kernel"]
-# launched exactly once per M-step (the divisor of the phase's PMC totals)
-MSTEP_ANCHORS = ["pilot_factor_kernel", "rhs_lds_kernel", "rhs_kernel"]
+# launched exactly once per M-step (the divisor of the phase's PMC totals; the pilot
+# factorisation runs once per EM run, so its bytes are spread over the run's M-steps)
+MSTEP_ANCHORS = ["rhs_lds_kernel", "rhs_kernel"]
 
 
 def mstep_flops_per_trial_iter(n_tx, n_rx, N, T_p, T_d):
