@@ -658,6 +658,8 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     // ---------------- H_eff(t) ----------------
     if (prep) {
         if (lane < NO) s_heff[lane] = cmk(prep[4 + 2 * lane], prep[5 + 2 * lane]);
+        // y_t beside the prep record (one memory round trip for both); s_tab[112..127]
+        if (lane < NR) reinterpret_cast<cd*>(s_tab + 112)[lane] = a.yd[(size_t)gsym * NR + lane];
         wave_sync();
     } else {
         const cd* th = a.theta + (size_t)b * c.P * NO;
@@ -733,7 +735,8 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
             if (kk < K2) {
                 const int r = kk >> 1;
                 const cd x = s_cons[sx];
-                const cd yv = a.yd[(size_t)gsym * NR + r];
+                const cd yv = prep ? reinterpret_cast<const cd*>(s_tab + 112)[r]
+                                   : a.yd[(size_t)gsym * NR + r];
                 const cd pu = csub(yv, cmul(H[0 * NR + r], x));
                 u = -2.0 * ((kk & 1) ? pu.y : pu.x);
                 if (NA == 2) {
