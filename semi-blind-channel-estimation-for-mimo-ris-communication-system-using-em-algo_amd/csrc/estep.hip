@@ -700,8 +700,35 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     // ||Py - x_s0 Ph_0 - x_kt Ph_2||^2, a lower bound of every hypothesis with first streams
     // (s0, kt); tile groups whose four bounds all exceed the skip bound are not swept
     const bool rowb = NT == 4 && V16 && prep && c.rowb;
-    double* s_rb = s_tab + 64;       // [3][NR] complex: P y, P h_0, P h_2 (scratch upper half)
-    if (rowb && lane < 6 * NR) s_rb[lane] = prep[c.rowb_off + lane];
+    // row-tile bound tables (scratch s_tab[63..111], free on the prep path): per column tile kt (= x_2 index)
+    //   n_kt = ||v_kt||^2 and a_kt = (P h_0)^H v_kt, v_kt = P y - x_kt P h_2, and ||P h_0||^2,
+    // so the bound of row tile s0 is n_kt - 2 Re(conj(x_s0) a_kt) + |x_s0|^2 ||P h_0||^2
+    double* s_rk = s_tab + 64;       // [16][3]
+    if (rowb) {
+        const double* rbp = prep + c.rowb_off;      // [3][NR] complex: P y, P h_0, P h_2
+        double n = 0.0, nb0 = 0.0;
+        cd av = czero();
+        if (lane < 16) {
+            const cd x2 = s_cons[lane];
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const cd py = cmk(rbp[2 * r], rbp[2 * r + 1]);
+                const cd p0 = cmk(rbp[2 * (NR + r)], rbp[2 * (NR + r) + 1]);
+                const cd p2 = cmk(rbp[2 * (2 * NR + r)], rbp[2 * (2 * NR + r) + 1]);
+                const cd v = csub(py, cmul(p2, x2));
+                n += cabs2(v);
+                nb0 += cabs2(p0);
+                av = cfmac(av, v, p0);                 // p0^H v
+            }
+        }
+        if (lane < 16) {
+            s_rk[3 * lane] = n;
+            s_rk[3 * lane + 1] = av.x;
+            s_rk[3 * lane + 2] = av.y;
+        }
+        if (lane == 0) s_tab[63] = nb0;
+        wave_sync();
+    }
 
     // lane-level accumulators (see VALU kernel)
     double mshift = d0;              // a real hypothesis' distance (candidate_distance)
@@ -785,12 +812,9 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
         if (rowb) {
             double bnd = INFINITY;
             if (lane < 16) {
-                const cd x0 = s_cons[lane], x2 = s_cons[kt];
-                const cd* rbv = reinterpret_cast<const cd*>(s_rb);
-                bnd = 0.0;
-#pragma unroll
-                for (int r = 0; r < NR; ++r)
-                    bnd += cabs2(csub(csub(rbv[r], cmul(rbv[NR + r], x0)), cmul(rbv[2 * NR + r], x2)));
+                const cd x0 = s_cons[lane];
+                const double* rk = s_rk + 3 * kt;
+                bnd = fma(cabs2(x0), s_tab[63], rk[0] - 2.0 * (x0.x * rk[1] + x0.y * rk[2]));
             }
             const double lim = ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin;
             rowmask = (unsigned)__ballot(bnd <= lim);
