@@ -804,8 +804,20 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
 
     const double hard_bound = d0 + 1e-10 * cscale_d + 1e-300;
     unsigned groups = 0;             // wave-uniform count of issued tile groups
+    // column tiles whose exact bound (column_tile_bounds) admits the skip bound as it stands
+    // now; the bound only falls during the sweep, so each is checked again when reached
+    unsigned long long ktmask = ~0ull;
+    if (nktile <= 64) {
+        const double lim0 = ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin;
+        ktmask = __ballot(lane < nktile && !(s_lb[lane < nktile ? lane : 0] > lim0));
+    }
     for (int kt = 0; kt < nktile; ++kt) {
-        // exact column-tile bound (column_tile_bounds): wave-uniform skip of the whole tile
+        if (nktile <= 64) {
+            const unsigned long long m = ktmask >> kt;
+            if (!m) break;
+            kt += __builtin_ctzll(m);
+        }
+        // exact column-tile bound: wave-uniform skip of the whole tile
         if (s_lb[kt] > ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin)
             continue;
         unsigned rowmask = 0xffffu;

@@ -33,6 +33,9 @@ def main():
             for c in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_LDS"):
                 if c in v:
                     line.append(f"{c[3:].lower()}={v[c] / wc:.3f}")
+        for c in sorted(v):                  # instruction counts etc.: per-launch values
+            if c.startswith("SQ_INSTS") or c == "SQ_WAVES":
+                line.append(f"{c[3:].lower()}={v[c]:.4g}")
         if "SQ_LDS_BANK_CONFLICT" in v:
             line.append(f"lds_conf={v['SQ_LDS_BANK_CONFLICT']:.3g}")
         print("  ".join(line))
