@@ -517,6 +517,8 @@ struct MfmaConst {
     int prep_stride;           // doubles per symbol of EstepArgs::prep
     int rowb_off;              // offset of the row-tile bound vectors in a prep record
     int rowb;                  // row-tile bounds on (NT = 4 with a prep record)
+    int rec_words;             // prep record + y_t, doubles (staged per symbol in LDS)
+    int spw;                   // symbols per wave (consecutive; the next record prefetched)
 };
 
 // V16 (M == 16, NA == 2): the A operand's V term, V[kk][i & 15] = V[kk][lane & 15], is the
@@ -632,7 +634,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     cd* s_cons = reinterpret_cast<cd*>(smem);
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: SGPR addresses
     const int lane = threadIdx.x & 63;
     double* wbase = reinterpret_cast<double*>(s_cons + 64) + (size_t)wave * c.tab_d;
     cd* s_heff = reinterpret_cast<cd*>(wbase);                 // NO
@@ -642,25 +644,68 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     double* s_Q2 = s_V + 4 * STEPS * c.M;                      // [KPAD][M]   (V16)
     double* s_lb = s_Q2 + 4 * STEPS * c.M;                     // [nkt] column-tile bounds
     double* s_tab = s_lb + c.nkt_pad;                          // scratch: 64 cd
+    double* s_recb = s_tab + 128;                  // 2 x [prep record | y_t (128) | done (32)]
 
     for (int i = threadIdx.x; i < c.M; i += blockDim.x) s_cons[i] = a.cons[i];
     __syncthreads();
 
     const long nsym = (long)c.B * c.Td;
-    long gsym = (long)blockIdx.x * kMfmaWaves + wave;
-    if (gsym >= nsym) return;
+    const long g0 = ((long)blockIdx.x * kMfmaWaves + wave) * c.spw;
+    if (g0 >= nsym) return;
+    const long g1 = g0 + c.spw < nsym ? g0 + c.spw : nsym;
+    const bool prep = a.prep != nullptr;
+    // The wave's symbols g0 .. g1-1 in turn.  With a prep record, the next symbol's record,
+    // y_t and done flag travel by LDS-DMA (global_load_lds: no VGPRs) into the other half of
+    // a double buffer while the current symbol is swept; the sweep reads no global memory,
+    // so the wait at the next symbol finds them landed.
+    const bool dma = prep && c.rec_words <= 128;
+    auto issue = [&](long g, double* dst) {
+        const int hs = c.prep_stride >> 1;                      // 16-byte words of the record
+        const double* src = a.prep + (size_t)g * c.prep_stride;
+        if (lane < hs) src += 2 * lane;
+        else if (lane < (c.rec_words >> 1))
+            src = reinterpret_cast<const double*>(a.yd) + (size_t)g * 2 * NR + 2 * (lane - hs);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        if (a.done)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(a.done + g / c.Td),
+                (__attribute__((address_space(3))) void*)(dst + 128), 4, 0, 0);
+    };
+    if (dma) issue(g0, s_recb);
+    for (long gsym = g0; gsym < g1; ++gsym) {
+    const int cur = (int)((gsym - g0) & 1);
+    double* s_rec = s_recb + cur * 160;
+    int dn;
+    if (dma) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this symbol's record has landed
+        wave_sync();
+        dn = a.done ? reinterpret_cast<const int*>(s_rec + 128)[0] : 0;
+        if (gsym + 1 < g1) issue(gsym + 1, s_recb + (cur ^ 1) * 160);
+    } else {
+        dn = a.done ? a.done[gsym / c.Td] : 0;
+        if (prep && !dn) {
+            wave_sync();
+            for (int e = lane; e < c.rec_words; e += 64)
+                s_rec[e] = e < c.prep_stride
+                    ? a.prep[(size_t)gsym * c.prep_stride + e]
+                    : reinterpret_cast<const double*>(a.yd)[(size_t)gsym * 2 * NR + e - c.prep_stride];
+            wave_sync();
+        }
+    }
+    if (dn) continue;
+    // lane index opaque per symbol: values derived from it (constellation points, LDS
+    // addresses) are recomputed per symbol instead of being hoisted and held across the loop
+    int lane_s = lane;
+    asm volatile("" : "+v"(lane_s));
+    [&, lane = lane_s]() {
     const int b = (int)(gsym / c.Td);
     const int t = (int)(gsym - (long)b * c.Td);
-    if (a.done && a.done[b]) return;
     const int mask = c.M - 1;
 
-    const double* prep = a.prep ? a.prep + (size_t)gsym * c.prep_stride : nullptr;
     // ---------------- H_eff(t) ----------------
     if (prep) {
-        if (lane < NO) s_heff[lane] = cmk(prep[4 + 2 * lane], prep[5 + 2 * lane]);
-        // y_t beside the prep record (one memory round trip for both); s_tab[112..127]
-        if (lane < NR) reinterpret_cast<cd*>(s_tab + 112)[lane] = a.yd[(size_t)gsym * NR + lane];
-        wave_sync();
+        // H_eff, bounds and y_t are read from the staged record (s_rec)
     } else {
         const cd* th = a.theta + (size_t)b * c.P * NO;
         const cd* ps = a.psid + (size_t)gsym * c.P;
@@ -680,15 +725,14 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
         }
         wave_sync();
     }
-    const cd* H = s_heff;
+    const cd* H = prep ? reinterpret_cast<const cd*>(s_rec + 4) : s_heff;
+    const double* lbp = prep ? s_rec + 4 + 2 * NO : s_lb;        // column-tile bounds
     const double inv_s2 = c.inv_s2;
     double cscale_d, d0, lb_scale;
     if (prep) {                      // estep_prep_kernel did these per symbol
-        d0 = prep[0];
-        cscale_d = prep[1];
-        lb_scale = prep[2];
-        for (int e = lane; e < (c.JB >> 4); e += 64) s_lb[e] = prep[4 + 2 * NO + e];
-        wave_sync();
+        d0 = s_rec[0];
+        cscale_d = s_rec[1];
+        lb_scale = s_rec[2];
     } else {
         d0 = candidate_distance<NT, NR>(H, a.yd + (size_t)gsym * NR, s_cons, c.M, c.reg,
                                         reinterpret_cast<cd*>(s_tab), lane, cscale_d);
@@ -705,7 +749,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     // so the bound of row tile s0 is n_kt - 2 Re(conj(x_s0) a_kt) + |x_s0|^2 ||P h_0||^2
     double* s_rk = s_tab + 64;       // [16][3]
     if (rowb) {
-        const double* rbp = prep + c.rowb_off;      // [3][NR] complex: P y, P h_0, P h_2
+        const double* rbp = s_rec + c.rowb_off;     // [3][NR] complex: P y, P h_0, P h_2
         double n = 0.0, nb0 = 0.0;
         cd av = czero();
         if (lane < 16) {
@@ -762,7 +806,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
             if (kk < K2) {
                 const int r = kk >> 1;
                 const cd x = s_cons[sx];
-                const cd yv = prep ? reinterpret_cast<const cd*>(s_tab + 112)[r]
+                const cd yv = prep ? reinterpret_cast<const cd*>(s_rec + c.prep_stride)[r]
                                    : a.yd[(size_t)gsym * NR + r];
                 const cd pu = csub(yv, cmul(H[0 * NR + r], x));
                 u = -2.0 * ((kk & 1) ? pu.y : pu.x);
@@ -809,7 +853,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     unsigned long long ktmask = ~0ull;
     if (nktile <= 64) {
         const double lim0 = ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin;
-        ktmask = __ballot(lane < nktile && !(s_lb[lane < nktile ? lane : 0] > lim0));
+        ktmask = __ballot(lane < nktile && !(lbp[lane < nktile ? lane : 0] > lim0));
     }
     for (int kt = 0; kt < nktile; ++kt) {
         if (nktile <= 64) {
@@ -818,7 +862,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
             kt += __builtin_ctzll(m);
         }
         // exact column-tile bound: wave-uniform skip of the whole tile
-        if (s_lb[kt] > ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin)
+        if (lbp[kt] > ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin)
             continue;
         unsigned rowmask = 0xffffu;
         if (rowb) {
@@ -1136,6 +1180,8 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
             const double re = red[ire], im = iim >= 0 ? red[iim] : 0.0;
             out[lane] = cmk(re * iz, (cj ? -im : im) * iz);
         }
+    }
+    }();
     }
 }
 
@@ -1466,11 +1512,17 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     // span(h_1, h_3)^perp), 3 NR complex
     c.rowb_off = 4 + 2 * NO + c.nkt_pad;
     c.prep_stride = c.rowb_off + (pb.NT == 4 ? 6 * pb.NR : 0);
+    c.rec_words = c.prep_stride + 2 * pb.NR;
+    c.tab_d += 2 * (c.rec_words <= 128 ? 160 : (c.rec_words + 1) / 2 * 2 + 32);
+    const char* sw = getenv("SBCE_ESTEP_SPW");           // symbols per wave (A/B runs)
+    c.spw = sw ? atoi(sw) : 4;
+    if (c.spw < 1) c.spw = 1;
     const char* rb = getenv("SBCE_ESTEP_ROWB");          // "0": off (A/B runs)
     c.rowb = pb.NT == 4 && c.prune && !(rb && rb[0] == '0');
     lds = 64 * sizeof(cd) + (size_t)kMfmaWaves * c.tab_d * sizeof(double);
     const long nsym = (long)pb.B * pb.Td;
-    blocks = (nsym + kMfmaWaves - 1) / kMfmaWaves;
+    const long per_block = (long)kMfmaWaves * c.spw;
+    blocks = (nsym + per_block - 1) / per_block;
     return lds <= 160 * 1024;
 }
 
