@@ -505,6 +505,13 @@ __device__ double candidate_distance(const cd* H, const cd* yg, const cd* s_cons
 constexpr int kMfmaWaves = 2;
 constexpr int kChunk = 256;
 
+// Per-wave LDS doubles of the MFMA sweep: heff | alpha | U | V | Q2 | lb | scratch (128) |
+// 2 x staged record (DMA double buffer: 128 + 32 done words, or the record itself)
+constexpr int mfma_tab_d(int NO, int chunk, int steps, int M, int nkt_pad, int rec_words) {
+    return (2 * NO + chunk + 3 * (4 * steps) * M + nkt_pad + 128 + 1) / 2 * 2 +
+           2 * (rec_words <= 128 ? 160 : (rec_words + 1) / 2 * 2 + 32);
+}
+
 struct MfmaConst {
     int B, Td, P, M, lm;
     int JA, JB, chunk, nparts;
@@ -623,6 +630,18 @@ __device__ unsigned long long g_estep_mfma;
 
 template <int NT, int NR, int MODE, int TU, bool V16>
 __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaConst& c) {
+    // V16 (n_tx = 4, M = 16): the layout constants are compile-time (LDS offsets fold into
+    // immediates, one SGPR wave base); otherwise they come from MfmaConst
+    const int k_M = V16 ? 16 : c.M;
+    const int k_lm = V16 ? 4 : c.lm;
+    const int k_JA = V16 ? 256 : c.JA;
+    const int k_JB = V16 ? 256 : c.JB;
+    const int k_chunk = V16 ? 256 : c.chunk;
+    const int k_nkt_pad = V16 ? 16 : c.nkt_pad;
+    const int k_rowb_off = V16 ? 4 + 2 * NT * NR + 16 : c.rowb_off;
+    const int k_prep_stride = V16 ? k_rowb_off + 6 * NR : c.prep_stride;
+    const int k_rec_words = V16 ? k_prep_stride + 2 * NR : c.rec_words;
+    const int k_tab_d = V16 ? mfma_tab_d(NT * NR, 256, (2 * NR + 3) / 4, 16, 16, k_rec_words) : c.tab_d;
     constexpr int NA = NT / 2;
     constexpr int NB = NT - NA;
     constexpr int NO = NT * NR;
@@ -636,17 +655,17 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     cd* s_cons = reinterpret_cast<cd*>(smem);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: SGPR addresses
     const int lane = threadIdx.x & 63;
-    double* wbase = reinterpret_cast<double*>(s_cons + 64) + (size_t)wave * c.tab_d;
+    double* wbase = reinterpret_cast<double*>(s_cons + 64) + (size_t)wave * k_tab_d;
     cd* s_heff = reinterpret_cast<cd*>(wbase);                 // NO
     double* s_al = wbase + 2 * NO;                             // chunk
-    double* s_U = s_al + c.chunk;                              // [KPAD][M]
-    double* s_V = s_U + 4 * STEPS * c.M;                       // [KPAD][M]   (NA == 2)
-    double* s_Q2 = s_V + 4 * STEPS * c.M;                      // [KPAD][M]   (V16)
-    double* s_lb = s_Q2 + 4 * STEPS * c.M;                     // [nkt] column-tile bounds
-    double* s_tab = s_lb + c.nkt_pad;                          // scratch: 64 cd
+    double* s_U = s_al + k_chunk;                              // [KPAD][M]
+    double* s_V = s_U + 4 * STEPS * k_M;                       // [KPAD][M]   (NA == 2)
+    double* s_Q2 = s_V + 4 * STEPS * k_M;                      // [KPAD][M]   (V16)
+    double* s_lb = s_Q2 + 4 * STEPS * k_M;                     // [nkt] column-tile bounds
+    double* s_tab = s_lb + k_nkt_pad;                          // scratch: 64 cd
     double* s_recb = s_tab + 128;                  // 2 x [prep record | y_t (128) | done (32)]
 
-    for (int i = threadIdx.x; i < c.M; i += blockDim.x) s_cons[i] = a.cons[i];
+    for (int i = threadIdx.x; i < k_M; i += blockDim.x) s_cons[i] = a.cons[i];
     __syncthreads();
 
     const long nsym = (long)c.B * c.Td;
@@ -658,13 +677,15 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     // y_t and done flag travel by LDS-DMA (global_load_lds: no VGPRs) into the other half of
     // a double buffer while the current symbol is swept; the sweep reads no global memory,
     // so the wait at the next symbol finds them landed.
-    const bool dma = prep && c.rec_words <= 128;
+    const bool dma = prep && k_rec_words <= 128;
     auto issue = [&](long g, double* dst) {
-        const int hs = c.prep_stride >> 1;                      // 16-byte words of the record
-        const double* src = a.prep + (size_t)g * c.prep_stride;
-        if (lane < hs) src += 2 * lane;
-        else if (lane < (c.rec_words >> 1))
-            src = reinterpret_cast<const double*>(a.yd) + (size_t)g * 2 * NR + 2 * (lane - hs);
+        int l = lane;                                           // recomputed per issue, not held
+        asm volatile("" : "+v"(l));
+        const int hs = k_prep_stride >> 1;                      // 16-byte words of the record
+        const double* src = a.prep + (size_t)g * k_prep_stride;
+        if (l < hs) src += 2 * l;
+        else if (l < (k_rec_words >> 1))
+            src = reinterpret_cast<const double*>(a.yd) + (size_t)g * 2 * NR + 2 * (l - hs);
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
         if (a.done)
@@ -686,10 +707,10 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
         dn = a.done ? a.done[gsym / c.Td] : 0;
         if (prep && !dn) {
             wave_sync();
-            for (int e = lane; e < c.rec_words; e += 64)
-                s_rec[e] = e < c.prep_stride
-                    ? a.prep[(size_t)gsym * c.prep_stride + e]
-                    : reinterpret_cast<const double*>(a.yd)[(size_t)gsym * 2 * NR + e - c.prep_stride];
+            for (int e = lane; e < k_rec_words; e += 64)
+                s_rec[e] = e < k_prep_stride
+                    ? a.prep[(size_t)gsym * k_prep_stride + e]
+                    : reinterpret_cast<const double*>(a.yd)[(size_t)gsym * 2 * NR + e - k_prep_stride];
             wave_sync();
         }
     }
@@ -701,7 +722,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     [&, lane = lane_s]() {
     const int b = (int)(gsym / c.Td);
     const int t = (int)(gsym - (long)b * c.Td);
-    const int mask = c.M - 1;
+    const int mask = k_M - 1;
 
     // ---------------- H_eff(t) ----------------
     if (prep) {
@@ -734,10 +755,10 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
         cscale_d = s_rec[1];
         lb_scale = s_rec[2];
     } else {
-        d0 = candidate_distance<NT, NR>(H, a.yd + (size_t)gsym * NR, s_cons, c.M, c.reg,
+        d0 = candidate_distance<NT, NR>(H, a.yd + (size_t)gsym * NR, s_cons, k_M, c.reg,
                                         reinterpret_cast<cd*>(s_tab), lane, cscale_d);
-        lb_scale = column_tile_bounds<NT, NR>(H, a.yd + (size_t)gsym * NR, s_cons, c.M, c.lm,
-                                              c.JB >> 4, s_lb, reinterpret_cast<cd*>(s_tab), lane);
+        lb_scale = column_tile_bounds<NT, NR>(H, a.yd + (size_t)gsym * NR, s_cons, k_M, k_lm,
+                                              k_JB >> 4, s_lb, reinterpret_cast<cd*>(s_tab), lane);
     }
     const double lb_margin = c.prune ? 1e-9 * lb_scale : INFINITY;
     // row-tile bounds (NT = 4): lane s0 < 16 of a surviving column tile kt evaluates
@@ -749,7 +770,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     // so the bound of row tile s0 is n_kt - 2 Re(conj(x_s0) a_kt) + |x_s0|^2 ||P h_0||^2
     double* s_rk = s_tab + 64;       // [16][3]
     if (rowb) {
-        const double* rbp = s_rec + c.rowb_off;     // [3][NR] complex: P y, P h_0, P h_2
+        const double* rbp = s_rec + k_rowb_off;     // [3][NR] complex: P y, P h_0, P h_2
         double n = 0.0, nb0 = 0.0;
         cd av = czero();
         if (lane < 16) {
@@ -800,13 +821,13 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     // (NA == 1: -2 p_i = U_{i}).  Layout [kk][s]: conflict-free per-lane reads.
     {
         wave_sync();
-        for (int e = lane; e < c.M * 4 * STEPS; e += 64) {
-            const int kk = e >> c.lm, sx = e & mask;
+        for (int e = lane; e < k_M * 4 * STEPS; e += 64) {
+            const int kk = e >> k_lm, sx = e & mask;
             double u = 0.0, v = 0.0, q2 = 0.0;
             if (kk < K2) {
                 const int r = kk >> 1;
                 const cd x = s_cons[sx];
-                const cd yv = prep ? reinterpret_cast<const cd*>(s_rec + c.prep_stride)[r]
+                const cd yv = prep ? reinterpret_cast<const cd*>(s_rec + k_prep_stride)[r]
                                    : a.yd[(size_t)gsym * NR + r];
                 const cd pu = csub(yv, cmul(H[0 * NR + r], x));
                 u = -2.0 * ((kk & 1) ? pu.y : pu.x);
@@ -842,8 +863,8 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
         q3reg[s] = q3;
     }
     const int xaddr16 = (lane ^ 16) << 2, xaddr32 = (lane ^ 32) << 2;
-    const int nktile = c.JB >> 4;
-    const int ntile_chunk = c.chunk >> 4;
+    const int nktile = k_JB >> 4;
+    const int ntile_chunk = k_chunk >> 4;
     bool table_ready = false;
 
     const double hard_bound = d0 + 1e-10 * cscale_d + 1e-300;
@@ -879,7 +900,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
         const int k = kt * 16 + col;
         cd xb[NB];
 #pragma unroll
-        for (int bb = 0; bb < NB; ++bb) xb[bb] = s_cons[(k >> (c.lm * (NB - 1 - bb))) & mask];
+        for (int bb = 0; bb < NB; ++bb) xb[bb] = s_cons[(k >> (k_lm * (NB - 1 - bb))) & mask];
         double bop[STEPS];
         double gam = 0.0;
         if constexpr (V16) {
@@ -919,7 +940,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
         for (int q = 0; q < NA; ++q) mu[q] = czero();
         bool touched = false;       // wave-uniform: an exp was taken in this column tile
 
-        for (int i0 = 0; i0 < c.JA; i0 += c.chunk) {
+        for (int i0 = 0; i0 < k_JA; i0 += k_chunk) {
             if (!table_ready && V16) {
                 // ---- alpha[s0*16 + s1] = 0.25 ||U_s0 + V_s1||^2
                 //      = 0.25 (|U_s0|^2 + |V_s1|^2) + 0.5 U_s0 . V_s1: the cross terms are a
@@ -953,21 +974,21 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
             if (!table_ready) {
                 // ---- alpha_i = ||p_i||^2 for entries i0 .. i0+chunk-1 from U, V ----
                 wave_sync();
-                for (int e = lane; e < c.chunk; e += 64) {
+                for (int e = lane; e < k_chunk; e += 64) {
                     const int i = i0 + e;
-                    const int su = (NA == 2) ? (i >> c.lm) : i;
+                    const int su = (NA == 2) ? (i >> k_lm) : i;
                     const int sv = i & mask;
                     double al = 0.0;
 #pragma unroll
                     for (int kk = 0; kk < K2; ++kk) {
-                        double v = s_U[kk * c.M + su];
-                        if (NA == 2) v += s_V[kk * c.M + sv];
+                        double v = s_U[kk * k_M + su];
+                        if (NA == 2) v += s_V[kk * k_M + sv];
                         al = fma(v, v, al);
                     }
                     s_al[e] = 0.25 * al;
                 }
                 wave_sync();
-                table_ready = (c.JA == c.chunk);
+                table_ready = (k_JA == k_chunk);
             }
             for (int tg = 0; tg < ntile_chunk; tg += TU) {
                 // TU independent 16x16 tiles in flight: STEPS*TU MFMAs per group;
@@ -996,8 +1017,8 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                             av = s_U[kk * 16 + (i0 >> 4) + tg + u] + vreg[s];
                         } else {
                             const int ia = i0 + (tg + u) * 16 + col;      // A-operand row
-                            av = s_U[kk * c.M + ((NA == 2) ? (ia >> c.lm) : ia)];
-                            if (NA == 2) av += s_V[kk * c.M + (ia & mask)];
+                            av = s_U[kk * k_M + ((NA == 2) ? (ia >> k_lm) : ia)];
+                            if (NA == 2) av += s_V[kk * k_M + (ia & mask)];
                         }
                         acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bop[s], acc[u], 0, 0, 0);
                     }
@@ -1020,7 +1041,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                         for (int j = 0; j < 4; ++j) {
                             const double dv = acc[u][j];
                             if (dv <= lim) {
-                                const int jj = (i0 + (tg + u) * 16 + rq + 4 * j) * c.JB + k;
+                                const int jj = (i0 + (tg + u) * 16 + rq + 4 * j) * k_JB + k;
                                 const double dd = dv + gam;
                                 if (dd < best_d || (dd == best_d && jj < best_j)) { best_d = dd; best_j = jj; }
                             }
@@ -1056,7 +1077,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                         const double w = fexp_neg((mshift - (acc[u][j] + gam)) * inv_s2);
                         cd xa[NA];
 #pragma unroll
-                        for (int q = 0; q < NA; ++q) xa[q] = s_cons[(i >> (c.lm * (NA - 1 - q))) & mask];
+                        for (int q = 0; q < NA; ++q) xa[q] = s_cons[(i >> (k_lm * (NA - 1 - q))) & mask];
                         ck += w;
 #pragma unroll
                         for (int q = 0; q < NA; ++q) {
@@ -1097,7 +1118,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
         if (lane == 0) {
             cd x[NT];
 #pragma unroll
-            for (int s2 = 0; s2 < NT; ++s2) x[s2] = s_cons[(best_j >> (c.lm * (NT - 1 - s2))) & mask];
+            for (int s2 = 0; s2 < NT; ++s2) x[s2] = s_cons[(best_j >> (k_lm * (NT - 1 - s2))) & mask];
 #pragma unroll
             for (int s2 = 0; s2 < NT; ++s2) {
                 out[s2] = x[s2];
@@ -1499,12 +1520,11 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     c.nparts = NO <= 64 ? 64 / NO : 1;
     const int steps = (2 * pb.NR + 3) / 4;
     c.nkt_pad = (int)((JB / 16 + 1) / 2 * 2);
-    c.tab_d = 2 * NO + c.chunk + 3 * (4 * steps) * pb.M + c.nkt_pad + 128;   // heff|alpha|U|V|Q2|lb|scratch
+
     const char* pr = getenv("SBCE_ESTEP_PRUNE");
     c.prune = !(pr && pr[0] == '0');
     const char* cnt = getenv("SBCE_ESTEP_COUNT");
     c.count = cnt && cnt[0] == '1';
-    c.tab_d = (c.tab_d + 1) / 2 * 2;          // keep 16-B alignment per wave
     c.inv_s2 = 1.0 / (pb.varn * pb.varn);
     c.thr_d = kSkipThr * pb.varn * pb.varn;
     c.reg = 0.1 * pb.varn * pb.varn;
@@ -1513,7 +1533,7 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     c.rowb_off = 4 + 2 * NO + c.nkt_pad;
     c.prep_stride = c.rowb_off + (pb.NT == 4 ? 6 * pb.NR : 0);
     c.rec_words = c.prep_stride + 2 * pb.NR;
-    c.tab_d += 2 * (c.rec_words <= 128 ? 160 : (c.rec_words + 1) / 2 * 2 + 32);
+    c.tab_d = mfma_tab_d(NO, c.chunk, steps, pb.M, c.nkt_pad, c.rec_words);
     const char* sw = getenv("SBCE_ESTEP_SPW");           // symbols per wave (A/B runs)
     c.spw = sw ? atoi(sw) : 4;
     if (c.spw < 1) c.spw = 1;
@@ -1531,6 +1551,10 @@ hipError_t dispatch_mfma_mode(const MfmaConst& c, size_t lds, long blocks, const
                               int mode, hipStream_t s) {
     const bool tu4 = (c.chunk / 16) % 4 == 0;
     if (NT == 4 && c.M == 16 && tu4) {            // cfg1 geometry: hoisted V operand
+        // the V16 body takes these layout constants as compile-time values
+        if (c.JA != 256 || c.JB != 256 || c.chunk != 256 || c.nkt_pad != 16 ||
+            c.prep_stride != 4 + 2 * NT * NR + 16 + 6 * NR)
+            return hipErrorInvalidValue;
         const char* occ = getenv("SBCE_ESTEP_OCC");   // "2": no VGPR cap (A/B runs)
         if constexpr (NR <= 4) {
             if (!(occ && occ[0] == '2')) {
