@@ -1021,6 +1021,83 @@ __global__ __launch_bounds__(256) void backsub_kernel(MstepArgs a, int L, int NR
     for (int e = tid; e < L * NR; e += nth) th[e] = cconj(y[e]);
 }
 
+// Back substitution for L <= 272 (every update column k < k0 <= 256 has one owner thread):
+// the 16 factor entries of block kb-2 are loaded while block kb is solved and applied, so
+// each block step waits on a load issued two steps earlier (two register buffers, the loop
+// unrolled by two so the buffers never need dynamic indexing); the diagonal blocks follow
+// the same two-ahead schedule.
+__device__ __forceinline__ void bs2_load(const cd* R, int L, int kb, int tid, cd* lv) {
+    const int k0 = kb * NB, w = (L - k0) < NB ? (L - k0) : NB;
+#pragma unroll
+    for (int c = 0; c < NB; ++c)
+        lv[c] = (kb >= 0 && tid < k0 && c < w) ? R[(size_t)(k0 + c) * L + tid] : czero();
+}
+__device__ __forceinline__ cd bs2_dload(const cd* R, int L, int kb, int tid) {
+    const int k0 = kb * NB, w = (L - k0) < NB ? (L - k0) : NB;
+    const int c = tid >> 4, c2 = tid & 15;
+    return (kb >= 0 && c < w && c2 < w && c2 >= c) ? R[(size_t)(k0 + c) * L + k0 + c2] : czero();
+}
+// one block step: publish the diagonal block d, solve it (wave 0), apply it to rows k < k0
+__device__ __forceinline__ void bs2_step(cd* y, cd* dblk, int L, int NR, int kb, int tid, int lane,
+                                         int wave, cd d, const cd* lv) {
+    const int k0 = kb * NB, w = (L - k0) < NB ? (L - k0) : NB;
+    dblk[tid] = d;
+    __syncthreads();
+    if (wave == 0) {
+        // x_blk = D^{-H} z_blk:  x[c] = z[c] / L[c][c] + sum_{c2>c} conj(Di[c2][c]) z[c2]
+        cd t0 = czero();
+        if (lane < w * NR) {
+            const int c = lane / NR, r = lane - c * NR;
+            const cd* Rc = dblk + c * NB;
+            const double lcc = Rc[c].x;
+            t0 = (lcc > 0.0) ? cscale(y[(k0 + c) * NR + r], 1.0 / lcc) : czero();
+            for (int c2 = c + 1; c2 < w; ++c2) t0 = cfma(t0, Rc[c2], y[(k0 + c2) * NR + r]);
+        }
+        wave_sync();
+        if (lane < w * NR) y[k0 * NR + lane] = t0;
+    }
+    __syncthreads();
+    if (tid < k0) {
+        for (int r = 0; r < NR; ++r) {
+            cd acc = y[tid * NR + r];
+#pragma unroll
+            for (int c = 0; c < NB; ++c)
+                if (c < w) acc = csub(acc, cmulc(y[(k0 + c) * NR + r], lv[c]));
+            y[tid * NR + r] = acc;
+        }
+    }
+    __syncthreads();
+}
+__global__ __launch_bounds__(256) void backsub2_kernel(MstepArgs a, int L, int NR) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cd* y = reinterpret_cast<cd*>(smem);
+    cd* dblk = y + L * NR;
+    const int b = blockIdx.x;
+    if (a.done && a.done[b]) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const cd* R = a.R + (size_t)b * L * L;
+    const cd* yg = a.rhs + (size_t)b * L * NR;
+    const int nblk = (L + NB - 1) / NB;
+    cd lvA[NB], lvB[NB];
+    bs2_load(R, L, nblk - 1, tid, lvA);
+    cd dA = bs2_dload(R, L, nblk - 1, tid);
+    bs2_load(R, L, nblk - 2, tid, lvB);
+    cd dB = bs2_dload(R, L, nblk - 2, tid);
+    for (int e = tid; e < L * NR; e += 256) y[e] = yg[e];
+    for (int kb = nblk - 1; kb >= 0; kb -= 2) {
+        bs2_step(y, dblk, L, NR, kb, tid, lane, wave, dA, lvA);
+        bs2_load(R, L, kb - 2, tid, lvA);
+        dA = bs2_dload(R, L, kb - 2, tid);
+        if (kb - 1 < 0) break;
+        bs2_step(y, dblk, L, NR, kb - 1, tid, lane, wave, dB, lvB);
+        bs2_load(R, L, kb - 3, tid, lvB);
+        dB = bs2_dload(R, L, kb - 3, tid);
+    }
+    cd* th = a.theta + (size_t)b * L * NR;
+    for (int e = tid; e < L * NR; e += 256) th[e] = cconj(y[e]);
+}
+
 hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_t s) {
     const char* sk = getenv("SBCE_CHOL_SKIP");      // diagnostic only (see kernels)
     const int skip = sk ? atoi(sk) : 0;
@@ -1039,6 +1116,13 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
         hipLaunchKernelGGL(panel_factor_kernel, dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR, jb, rem,
                            skip);
         if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    // SBCE_BACKSUB=1 keeps the one-step-prefetch kernel (A/B runs)
+    const char* bsv = getenv("SBCE_BACKSUB");
+    if (pb.L <= 272 && pb.NR <= 4 && !(bsv && bsv[0] == '1') && !(skip & 16)) {
+        hipLaunchKernelGGL(backsub2_kernel, dim3(pb.B), dim3(256),
+                           ((size_t)pb.L * pb.NR + NB * NB) * sizeof(cd), s, a, pb.L, pb.NR);
+        return hipGetLastError();
     }
     hipLaunchKernelGGL(backsub_kernel, dim3(pb.B), dim3(256),
                        ((size_t)pb.L * pb.NR + NB * NB) * sizeof(cd), s,
