@@ -363,8 +363,11 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape, monkeypatch):
     S = x[..., :, None] * np.conj(x[..., None, :]) + 0.1 * np.eye(n_tx)
     out = {}
     # default = batched panel launches; "fused" = one workgroup per trial; "valu"
-    for impl in ("batched", "fused", "valu"):
-        monkeypatch.setenv("SBCE_CHOL_IMPL", impl)
+    # "batched_bs1": batched, with the one-step-prefetch back substitution instead of the
+    # two-ahead kernel (default for L <= 272, n_rx <= 4)
+    for impl in ("batched", "fused", "valu", "batched_bs1"):
+        monkeypatch.setenv("SBCE_CHOL_IMPL", impl.split("_")[0])
+        monkeypatch.setenv("SBCE_BACKSUB", "1" if impl.endswith("bs1") else "0")
         out[impl] = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], m, S, 0.05)
     th_m, R, rhs, st = out["batched"]
     assert not st.any()
@@ -375,6 +378,7 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape, monkeypatch):
             assert rel(out[impl][0][i], ref) < 1e-9, impl
     assert rel(th_m, out["fused"][0]) < 1e-9
     assert rel(th_m, out["valu"][0]) < 1e-9
+    assert rel(th_m, out["batched_bs1"][0]) < 1e-12
 
 
 # ---------------------------------------------------------------- large-L M-step (L > 512)
