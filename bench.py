@@ -219,7 +219,11 @@ def main():
     if world > 1:
         dist.all_reduce(acc, op=dist.ReduceOp.SUM)
     nmse_mean = float(acc[0] / acc[1])
-    nonhpd = int((eng.status != 0).sum().item())
+    # SBCE_STATUS_NONHPD only: the PILOT / DETECTOR bits are informational
+    nonhpd = int(((eng.status & pkg._lib.SBCE_STATUS_NONHPD) != 0).sum().item())
+    status_bits = {name: int(((eng.status & bit) != 0).sum().item())
+                   for name, bit in (("pilot", pkg._lib.SBCE_STATUS_PILOT),
+                                     ("detector", pkg._lib.SBCE_STATUS_DETECTOR))}
 
     # ---- dominant-kernel timing: E-step launches with HIP events on the launch stream ----
     stream = torch.cuda.current_stream()
@@ -324,6 +328,7 @@ def main():
                    "parallelism": f"trials-sharded x{world}"},
         "nmse_mean": nmse_mean,
         "nonhpd_trials": nonhpd,
+        "status_trials": status_bits,
         "kernels_ms": {"estep": estep_ms, "mstep_build_plus_solve": mstep_ms},
         "roofline": roofline,
         "mstep_roofline": mstep_roof,

@@ -99,6 +99,8 @@ extern "C" {
 #define SBCE_STATUS_DETECTOR 4  /* ZF/MMSE: the reference's flattened argmin indexed past
                                    all_possibleSymbols (IndexError at
                                    all_detectorsvsTd.py:52); row flat mod M^n_tx used */
+#define SBCE_STATUS_DEBUG 8     /* a diagnostic phase-skip mask (sbce_debug_chol_skip, not
+                                   part of this header's API) was active: theta is invalid */
 
 typedef struct sbce_dims {
     int32_t batch;      /* B: independent Monte-Carlo trials */

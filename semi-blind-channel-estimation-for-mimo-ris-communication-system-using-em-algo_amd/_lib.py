@@ -23,6 +23,7 @@ SBCE_SOLVE_CHOL_DROP = 1
 SBCE_STATUS_NONHPD = 1
 SBCE_STATUS_PILOT = 2
 SBCE_STATUS_DETECTOR = 4
+SBCE_STATUS_DEBUG = 8
 
 EXPORTED = ("sbce_abi_version", "sbce_strerror", "sbce_workspace_bytes", "sbce_em",
             "sbce_estep", "sbce_mstep", "sbce_ser", "sbce_gauss_expand", "sbce_nmse")

@@ -115,9 +115,9 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
             void* hip_stream) {
     Problem pb;
     if (!make_problem(d, pb) || iters < 0) return SBCE_EINVAL;
+    if (!estep_supported(pb, estep_mode) || !chol_supported(pb)) return SBCE_EUNSUPPORTED;
     int rc = check_ptrs(p, pb, true);
     if (rc) return rc;
-    if (!estep_supported(pb, estep_mode) || !chol_supported(pb)) return SBCE_EUNSUPPORTED;
     if (solve_mode != SBCE_SOLVE_CHOL && solve_mode != SBCE_SOLVE_CHOL_DROP) return SBCE_EINVAL;
     if (p->llf && !p->x_d_true) return SBCE_EINVAL;
     const bool gauss = estep_mode == SBCE_ESTEP_GAUSS;
@@ -215,10 +215,10 @@ int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int 
                void* r_out, void* rhs_out, void* hip_stream) {
     Problem pb;
     if (!make_problem(d, pb)) return SBCE_EINVAL;
+    if (!chol_supported(pb)) return SBCE_EUNSUPPORTED;
     int rc = check_ptrs(p, pb, true);
     if (rc) return rc;
     if (!moments) return SBCE_EINVAL;
-    if (!chol_supported(pb)) return SBCE_EUNSUPPORTED;
     if (pb.B == 0) return SBCE_OK;
     hipStream_t s = (hipStream_t)hip_stream;
     const Carve c = carve(pb);
@@ -248,6 +248,16 @@ int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int 
 int sbce_debug_chol_clock(unsigned long long* out32, int reset) {
     if (reset) return hip_rc(chol_debug_clock_reset());
     return out32 ? hip_rc(chol_debug_clock(out32)) : SBCE_EINVAL;
+}
+
+// Diagnostic, not part of include/sbce.h: phase-skip mask of the Cholesky kernels (1 panel
+// update, 2 diagonal factor, 8 TRSM tiles, 16 back substitution: results INVALID, every
+// trial flagged SBCE_STATUS_DEBUG; 64: per-phase clocks of the fused kernel, results valid).
+// 0 restores normal operation.
+int sbce_debug_chol_skip(int mask) {
+    if (mask < 0) return SBCE_EINVAL;
+    chol_debug_skip(mask);
+    return SBCE_OK;
 }
 
 // Diagnostic, not part of include/sbce.h: FP64 MFMAs issued by the exact E-step sweep since

@@ -275,7 +275,8 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
     back_substitute(R, y, L, NR, tid, nth, lane, wave, (skip & 16) ? nblk : 0);
     cd* th = a.theta + (size_t)b * L * NR;
     for (int e = tid; e < L * NR; e += nth) th[e] = cconj(y[e]);
-    if (tid == 0 && a.status) a.status[b] |= *flag ? SBCE_STATUS_NONHPD : 0;
+    if (tid == 0 && a.status)
+        a.status[b] |= (*flag ? SBCE_STATUS_NONHPD : 0) | ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
 }
 
 // ---------------------------------------------------------------- MFMA kernel
@@ -456,6 +457,11 @@ __device__ __forceinline__ void back_substitute_pf(const cd* R, cd* y, int L, in
 
 // DIAGNOSTIC (skip & 64): per-phase s_memtime sums of waves 0 and 1 of block 0
 __device__ unsigned long long g_chol_clk[32];
+
+// DIAGNOSTIC phase-skip mask of the Cholesky kernels (timing only, results invalid).  Set
+// only through sbce_debug_chol_skip(); every trial factored while it is nonzero carries
+// SBCE_STATUS_DEBUG, so a result computed with skipped phases can never pass as valid.
+int g_chol_skip = 0;
 
 // Geometry of one chol_mfma_kernel launch: the factored L x L matrix starts at row/col
 // `off` of trial b's matrix (a.R + b*stride), leading dimension ld.  SOLVE = false
@@ -659,7 +665,8 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip, CholGeom g) {
         for (int e = tid; e < L * NR; e += nth) th[e] = cconj(y[e]);
     }
 #undef SBCE_CLK
-    if (tid == 0 && a.status) a.status[b] |= *flag ? SBCE_STATUS_NONHPD : 0;
+    if (tid == 0 && a.status)
+        a.status[b] |= (*flag ? SBCE_STATUS_NONHPD : 0) | ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
 }
 
 // ---------------------------------------------------------------- batched panel kernels
@@ -1000,7 +1007,8 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
             wave_sync();
         }
     }
-    if (tid == 0 && flag && a.status) atomicOr(&a.status[b], SBCE_STATUS_NONHPD);
+    const int st = (flag ? SBCE_STATUS_NONHPD : 0) | ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
+    if (tid == 0 && st && a.status) atomicOr(&a.status[b], st);
 }
 
 // Back substitution L^H x = y (y staged in LDS) and theta = conj(x), one workgroup per trial.
@@ -1099,8 +1107,7 @@ __global__ __launch_bounds__(256) void backsub2_kernel(MstepArgs a, int L, int N
 }
 
 hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_t s) {
-    const char* sk = getenv("SBCE_CHOL_SKIP");      // diagnostic only (see kernels)
-    const int skip = sk ? atoi(sk) : 0;
+    const int skip = g_chol_skip;                   // diagnostic only (see kernels)
     hipError_t e = launch_diag_tol(pb, a, s);
     if (e != hipSuccess) return e;
     const int npan = (pb.L + PW - 1) / PW;
@@ -1132,8 +1139,7 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
 
 template <int RPT, bool YLDS>
 hipError_t launch_rpt(const Problem& pb, const MstepArgs& a, int nth, size_t lds, hipStream_t s) {
-    const char* sk = getenv("SBCE_CHOL_SKIP");      // diagnostic only (see kernel)
-    const int skip = sk ? atoi(sk) : 0;
+    const int skip = g_chol_skip;                   // diagnostic only (see kernel)
     hipLaunchKernelGGL((chol_solve_kernel<RPT, YLDS>), dim3(pb.B), dim3(nth), lds, s, a, pb.L, pb.NR,
                        skip);
     return hipGetLastError();
@@ -1152,8 +1158,7 @@ hipError_t launch_y(const Problem& pb, const MstepArgs& a, int nth, int rpt, siz
 template <bool YLDS, int NWB, int KB>
 hipError_t launch_mfma_cfg(const Problem& pb, const MstepArgs& a, int nw, int maxt, size_t lds,
                            hipStream_t s) {
-    const char* sk = getenv("SBCE_CHOL_SKIP");      // diagnostic only (see kernel)
-    const int skip = sk ? atoi(sk) : 0;
+    const int skip = g_chol_skip;                   // diagnostic only (see kernel)
     const dim3 g(pb.B), blk(64 * nw);
     CholGeom geo;
     geo.ld = pb.L; geo.off = 0; geo.stride = (size_t)pb.L * pb.L; geo.tolp = nullptr;
@@ -1192,12 +1197,17 @@ hipError_t chol_debug_clock(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chol_clk), sizeof(g_chol_clk), 0,
                                hipMemcpyDeviceToHost);
 }
+void chol_debug_skip(int mask) { g_chol_skip = mask; }
 hipError_t chol_debug_clock_reset() {
     static const unsigned long long z[32] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_chol_clk), z, sizeof(z), 0, hipMemcpyHostToDevice);
 }
 
-bool chol_supported(const Problem& pb) { return pb.L >= 1 && (pb.L <= 1024 || pb.NR <= 8); }
+// L <= kLargeL: one workgroup (or batched panel launches) per trial, grid x = batch.
+// kLargeL < L <= kMaxL: the tiled path launches grid (tiles, batch), so batch <= 65535.
+bool chol_supported(const Problem& pb) {
+    return pb.L >= 1 && pb.L <= kMaxL && (pb.L <= kLargeL || pb.B <= 65535);
+}
 
 // Factor the w x w diagonal tile at (k0, k0) of every trial's R in place (large-L path).
 hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w, hipStream_t s) {

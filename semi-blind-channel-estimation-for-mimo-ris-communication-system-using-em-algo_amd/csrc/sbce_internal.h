@@ -157,6 +157,7 @@ hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t
 hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s);
 bool chol_supported(const Problem& pb);
 constexpr int kLargeL = 512;   // L above this: tiled build + blocked right-looking Cholesky
+constexpr int kMaxL = 8192;    // largest supported L (R alone is 1 GiB per trial there)
 bool rbuild_herm_supported(const Problem& pb);   // MFMA build of the Hermitian R: NT in {4, 8}
 hipError_t launch_pilot_factor(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_rbuild_herm(const Problem& pb, const MstepArgs& a, hipStream_t s);
@@ -165,6 +166,7 @@ hipError_t launch_diag_tol(const Problem& pb, const MstepArgs& a, hipStream_t s)
 hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w, hipStream_t s);
 hipError_t chol_debug_clock(unsigned long long* out);   // diagnostic (SBCE_CHOL_SKIP & 64)
 hipError_t chol_debug_clock_reset();
+void chol_debug_skip(int mask);   // diagnostic phase-skip mask (results flagged SBCE_STATUS_DEBUG)
 hipError_t launch_decisions(const Problem& pb, const cd* mom, cd* xdest, hipStream_t s);
 hipError_t launch_sup_shift_y(const Problem& pb, const cd* yd, const cd* psid, const cd* theta,
                               const cd* xsup, cd* yout, const int32_t* done, hipStream_t s);

@@ -22,6 +22,15 @@ def shard(n_trials, world, rank):
     return np.arange(rank, n_trials, world, dtype=np.int64)
 
 
+def collective_device(dist):
+    """Device an all-reduce buffer must live on for the initialised process group:
+    the current HIP device for RCCL ("nccl"), None (host memory) otherwise."""
+    if str(dist.get_backend()).lower() == "nccl":
+        import torch
+        return torch.device("cuda", torch.cuda.current_device())
+    return None
+
+
 class Accumulators:
     """Per-sweep-point sums, packed into one float64 vector for a single all-reduce."""
 
@@ -57,11 +66,16 @@ class Accumulators:
         return self
 
     def allreduce(self, dist=None, device=None):
-        """ONE all-reduce(sum) of every accumulator (no-op when not distributed)."""
+        """ONE all-reduce(sum) of every accumulator (no-op when not distributed).
+
+        RCCL ("nccl" backend) reduces device tensors only, so with that backend and no
+        explicit `device` the vector goes to the current HIP device (gloo: host)."""
         if dist is None or not dist.is_available() or not dist.is_initialized():
             return self
         import torch
         t = torch.from_numpy(self.pack())
+        if device is None:
+            device = collective_device(dist)
         if device is not None:
             t = t.to(device)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)

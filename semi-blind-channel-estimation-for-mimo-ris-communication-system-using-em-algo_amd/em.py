@@ -529,7 +529,7 @@ class EMEngine:
     """
 
     def __init__(self, batch, varn, mode="soft", solve="chol", x_d_true=None, h_true=None,
-                 partition_r=0):
+                 partition_r=0, varx=1.0, x_sup=None):
         torch = _torch()
         self.torch = torch
         self.lib = _lib.load()
@@ -551,7 +551,12 @@ class EMEngine:
         self.n_tx, self.n_rx, self.B, self.T_d, self.T_p, self.P = L // P, n_rx, B, T_d, T_p, P
         self.M = self.cons.shape[0]
         self.varn = float(varn)
-        self.dims = _lib.Dims(B, self.n_tx, n_rx, P, T_p, T_d, self.M, int(partition_r), self.varn)
+        if mode == "gauss" and not varx > 0:
+            raise ValueError("mode 'gauss' needs a prior variance varx > 0")
+        if x_sup is not None and mode not in ("soft", "hard"):
+            raise ValueError("superimposed pilots (x_sup) need the soft or hard E-step")
+        self.dims = _lib.Dims(B, self.n_tx, n_rx, P, T_p, T_d, self.M, int(partition_r), self.varn,
+                              float(varx))
         self.ws = torch.empty(max(_lib.workspace_bytes(self.dims), 16), dtype=torch.uint8,
                               device="cuda")
         self.status = torch.zeros(B, dtype=torch.int32, device="cuda")
@@ -559,10 +564,15 @@ class EMEngine:
         self.x_d = dev(x_d_true)
         self.mom = torch.zeros((B, T_d, self.n_tx + self.n_tx ** 2), dtype=torch.complex128,
                                device="cuda")
-        self.ptrs = _lib.Ptrs(self.y_d.data_ptr(), self.y_p.data_ptr(), self.psi_d.data_ptr(),
-                              self.u_p.data_ptr(), self.cons.data_ptr(), self.theta.data_ptr(),
-                              None, None, None, None, self.status.data_ptr(), self.ws.data_ptr(),
-                              self.ws.numel())
+        self.x_sup = dev(x_sup)
+        # T_p == 0 (superimposed protocol): an empty tensor's data_ptr() is 0, which the ABI
+        # rejects; the pilot buffers are never read then, so pass y_d as a placeholder (em_batch)
+        yp = self.y_p.data_ptr() if T_p else self.y_d.data_ptr()
+        up = self.u_p.data_ptr() if T_p else self.y_d.data_ptr()
+        self.ptrs = _lib.Ptrs(self.y_d.data_ptr(), yp, self.psi_d.data_ptr(), up,
+                              self.cons.data_ptr(), self.theta.data_ptr(), None, None, None, None,
+                              self.status.data_ptr(), self.ws.data_ptr(), self.ws.numel(), None,
+                              self.x_sup.data_ptr() if self.x_sup is not None else None)
 
     def run(self, itera):
         """One full EM (itera iterations) over the whole batch, stream-ordered."""

@@ -85,3 +85,17 @@ def test_product_path_fails_loudly_without_gpu(sbce):
     with pytest.raises(sbce.SbceUnavailable):
         sbce.em_batch(*(None,) * 5, 0.1, 1, None)
     del d
+
+
+def test_oversized_problems_are_unsupported_without_gpu(sbce):
+    """chol_supported: L <= 8192 (the tiled large-L path); larger systems are rejected with
+    SBCE_EUNSUPPORTED before any pointer is dereferenced or HIP call made."""
+    L = sbce._lib
+    lib = L.load()
+    big = L.Dims(2, 8, 4, 1025, 16, 64, 16, 1, 0.1)      # L = 1025 * 8 = 8200 > 8192
+    p = L.Ptrs(*([16] * 12), 1 << 62)
+    assert lib.sbce_em(ctypes.byref(big), ctypes.byref(p), 1, L.SBCE_ESTEP_PM_SOFT,
+                       L.SBCE_SOLVE_CHOL, None) == -2
+    assert lib.sbce_mstep(ctypes.byref(big), ctypes.byref(p), 16, 0, None, None, None) == -2
+    ok = L.Dims(2, 8, 4, 1024, 16, 64, 16, 1, 0.1)       # L = 8192: supported
+    assert L.workspace_bytes(ok) > 2 * 8192 * 8192 * 16

@@ -71,3 +71,53 @@ def test_shard_partition_is_exact(sbce):
             assert np.array_equal(allidx, np.arange(n))
     with pytest.raises(ValueError):
         sbce.distributed.shard(10, 2, 2)
+
+
+class _StubDist:
+    """Initialised process group stand-in: records the device of the all-reduce buffer."""
+
+    class ReduceOp:
+        SUM = "sum"
+
+    def __init__(self, backend):
+        self.backend, self.devices = backend, []
+
+    def is_available(self):
+        return True
+
+    def is_initialized(self):
+        return True
+
+    def get_backend(self):
+        return self.backend
+
+    def all_reduce(self, t, op=None):
+        self.devices.append(t.device)
+
+
+def test_collective_device_follows_backend(sbce, monkeypatch):
+    """RCCL ("nccl") reduces device tensors only: with that backend the accumulator vector
+    must go to the current HIP device; gloo keeps it on the host."""
+    import torch
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 3)
+    assert sbce.distributed.collective_device(_StubDist("nccl")) == torch.device("cuda", 3)
+    assert sbce.distributed.collective_device(_StubDist("gloo")) is None
+
+
+def test_allreduce_uses_collective_device_by_default(sbce, monkeypatch):
+    import torch
+    seen = []
+
+    def fake(dist):
+        seen.append(dist.get_backend())
+        return torch.device("cpu")        # stands in for the HIP device on a CPU-only host
+    monkeypatch.setattr(sbce.distributed, "collective_device", fake)
+    acc = sbce.distributed.Accumulators(2, n_iters=1)
+    acc.add(0, [0.5, 0.25], llf_values=[[1.0], [2.0]])
+    stub = _StubDist("nccl")
+    acc.allreduce(stub)                   # what every sweep does: no explicit device
+    assert seen == ["nccl"] and stub.devices == [torch.device("cpu")]
+    assert acc.count.tolist() == [2.0, 0.0]
+    # an explicit device wins and skips the backend query
+    acc.allreduce(_StubDist("nccl"), device="cpu")
+    assert seen == ["nccl"]

@@ -587,3 +587,81 @@ def test_gaussian_sweep_entry_point(sbce):
     H = d["H0"]
     ref = np.sum(np.abs(d["H_hat0"] - H) ** 2) / np.sum(np.abs(H) ** 2)
     assert np.allclose(nm, [ref], rtol=1e-9, atol=0)
+
+
+# ---------------------------------------------------------------- EMEngine (bench / sweeps)
+def test_engine_matches_em_batch_superimposed_and_gauss(sbce):
+    """EMEngine (resident buffers, one sbce_em per run) equals em_batch for the modes that
+    need more than the default arguments: T_p = 0 with superimposed pilots (placeholder
+    pilot pointers) and the Gaussian prior (varx passed through)."""
+    varn = 0.2
+    b = sbce.signal_model.synthetic_batch(3, 2, 2, 5, 0, 24, 4, varn, seed=9)
+    rng = np.random.default_rng(4)
+    xs = (rng.standard_normal((3, 24, 2)) + 1j * rng.standard_normal((3, 24, 2))) * 0.5
+    th0 = np.zeros_like(b["theta0"])
+    ref = sbce.em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, 3, th0,
+                        x_sup=xs)
+    eng = sbce.EMEngine(dict(b, theta0=th0), varn, x_sup=xs)
+    assert np.array_equal(eng.run(3).cpu().numpy(), ref["theta"])
+
+    bg = sbce.signal_model.synthetic_batch(2, 2, 2, 4, 6, 20, 4, varn, seed=5, direct=False)
+    P = 4                                                 # gauss: no direct-path row
+    ref = sbce.em_batch(bg["y_d"], bg["y_p"], bg["psi_d"], bg["u_p"], bg["cons"], varn, 2,
+                        bg["theta0"], mode="gauss", varx=1.5, solve="drop")
+    eng = sbce.EMEngine(bg, varn, mode="gauss", solve="drop", varx=1.5)
+    assert eng.P == P
+    assert np.array_equal(eng.run(2).cpu().numpy(), ref["theta"])
+
+
+def test_debug_skip_mask_flags_every_trial(sbce):
+    """A diagnostic Cholesky phase-skip mask (results invalid) can only be set through
+    sbce_debug_chol_skip and marks every trial SBCE_STATUS_DEBUG; 0 restores valid runs."""
+    varn = 0.1
+    b = sbce.signal_model.synthetic_batch(4, 4, 4, 8, 16, 40, 4, varn, seed=1)
+    lib = sbce._lib.load()
+    good = sbce.em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, 2,
+                         b["theta0"])
+    assert not (good["status"] & sbce._lib.SBCE_STATUS_DEBUG).any()
+    try:
+        assert lib.sbce_debug_chol_skip(8) == 0
+        bad = sbce.em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, 2,
+                            b["theta0"])
+    finally:
+        lib.sbce_debug_chol_skip(0)
+    assert (bad["status"] & sbce._lib.SBCE_STATUS_DEBUG).all()
+    again = sbce.em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, 2,
+                          b["theta0"])
+    assert np.array_equal(again["theta"], good["theta"]) and not again["status"].any()
+
+
+def test_rccl_accumulator_allreduce_single_rank(sbce, tmp_path):
+    """The sweeps' one collective over a real RCCL ("nccl") group: Accumulators.allreduce
+    without an explicit device must put the vector on the HIP device (RCCL rejects host
+    tensors).  World size 1 in a child process (one GPU on the test box)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    from conftest import ROOT, PKG
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    code = f'''
+import importlib, sys
+sys.path.insert(0, {ROOT!r})
+import numpy as np, torch, torch.distributed as dist
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+sb = importlib.import_module({PKG!r})
+acc = sb.distributed.Accumulators(2, n_iters=2)
+acc.add(1, [0.5, 0.25], llf_values=[[1.0, 2.0], [3.0, 4.0]])
+acc.allreduce(dist)
+assert acc.count.tolist() == [0.0, 2.0] and acc.llf[1].tolist() == [4.0, 6.0], acc.pack()
+dist.destroy_process_group()
+print("RCCL_OK")
+'''
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0 and "RCCL_OK" in r.stdout, r.stderr[-2000:]

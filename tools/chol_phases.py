@@ -1,4 +1,4 @@
-"""Diagnostic: M-step time at cfg1 with Cholesky phases disabled (SBCE_CHOL_SKIP bitmask,
+"""Diagnostic: M-step time at cfg1 with Cholesky phases disabled (sbce_debug_chol_skip bitmask,
 results invalid: 1 panel update, 2 diagonal factor, 8 TRSM tiles, 16 back substitution).
 Not part of the product."""
 import os
@@ -9,6 +9,7 @@ import torch  # noqa: E402
 import __graft_entry__ as ge  # noqa: E402
 
 pkg = ge.package()
+LIB = pkg._lib.load()
 B = int(os.environ.get("B", "1000"))
 varn = float(pkg.signal_model.snr_to_varn(20.0))
 batch = pkg.signal_model.synthetic_batch(B, 4, 4, 64, 16, 256, 16, varn, seed=0)
@@ -33,6 +34,6 @@ def timeit(fn, reps=5):
 for impl in sys.argv[1:] or ["batched"]:
     os.environ["SBCE_CHOL_IMPL"] = impl
     for skip in (0, 1, 2, 8, 16, 2 | 8, 1 | 2 | 8 | 16):
-        os.environ["SBCE_CHOL_SKIP"] = str(skip)
+        LIB.sbce_debug_chol_skip(skip)
         print(f"chol {impl} skip={skip:2d}: mstep {timeit(eng.mstep):.3f} ms", flush=True)
-os.environ["SBCE_CHOL_SKIP"] = "0"
+LIB.sbce_debug_chol_skip(0)

@@ -1,4 +1,4 @@
-"""Diagnostic: time the M-step Cholesky with phases disabled (SBCE_CHOL_SKIP bitmask,
+"""Diagnostic: time the M-step Cholesky with phases disabled (sbce_debug_chol_skip bitmask,
 results invalid) and the E-step per SNR, on cfg1 shapes.  Not part of the product."""
 import os
 import sys
@@ -9,6 +9,7 @@ import torch  # noqa: E402
 import __graft_entry__ as ge  # noqa: E402
 
 pkg = ge.package()
+LIB = pkg._lib.load()
 B = int(os.environ.get("B", "1000"))
 varn = float(pkg.signal_model.snr_to_varn(20.0))
 batch = pkg.signal_model.synthetic_batch(B, 4, 4, 64, 16, 256, 16, varn, seed=0)
@@ -33,9 +34,9 @@ def timeit(fn, reps=5):
 for impl in ("mfma", "valu"):
     os.environ["SBCE_CHOL_IMPL"] = impl
     for skip in (0, 1, 2, 8, 16, 1 | 2 | 8 | 16):
-        os.environ["SBCE_CHOL_SKIP"] = str(skip)
+        LIB.sbce_debug_chol_skip(skip)
         print(f"chol {impl} skip={skip:2d}: mstep {timeit(eng.mstep):.3f} ms", flush=True)
-os.environ["SBCE_CHOL_SKIP"] = "0"
+LIB.sbce_debug_chol_skip(0)
 os.environ["SBCE_CHOL_IMPL"] = "mfma"
 
 # per-phase s_memtime sums (block 0, waves 0/1) of one MFMA Cholesky launch
@@ -43,10 +44,10 @@ import ctypes  # noqa: E402
 lib = pkg._lib.load()
 buf = (ctypes.c_ulonglong * 32)()
 lib.sbce_debug_chol_clock(buf, 1)
-os.environ["SBCE_CHOL_SKIP"] = "64"
+LIB.sbce_debug_chol_skip(64)
 eng.mstep()
 torch.cuda.synchronize()
-os.environ["SBCE_CHOL_SKIP"] = "0"
+LIB.sbce_debug_chol_skip(0)
 lib.sbce_debug_chol_clock(buf, 0)
 names = ["C init+update", "diag factor", "barrier after diag", "trsm tiles", "end barrier",
          "back substitution"]
