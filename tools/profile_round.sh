@@ -25,6 +25,7 @@ for W in cfg1 cfg2; do
     TR=$([ $W = cfg1 ] && echo 1000 || echo 256)
     python3 "$R/tools/pmc_summary.py" --fetch "$O/pmc_fetch_$W" --write "$O/pmc_write_$W" \
         --config $W --trials $TR --out "$O/pmc_$W.json" > /dev/null
+    rm -rf "$O/pmc_fetch_$W" "$O/pmc_write_$W"     # raw databases: gpurun_out/ must stay < 64 MiB
     if [ $W = cfg1 ]; then
         timeout -k 10 400 python3 "$R/bench.py" $C --steps 3 --warmup 1 --pmc "$O/pmc_$W.json" \
             > "$O/bench_$W.log" 2>&1
@@ -38,5 +39,6 @@ for W in cfg1 cfg2; do
             > "$O/trace_$W.log" 2>&1
     fi
     python3 "$R/tools/trace_summary.py" "$O/trace_$W" > "$O/kernel_stats_$W.csv"
+    rm -rf "$O/trace_$W"
 done
 echo done
