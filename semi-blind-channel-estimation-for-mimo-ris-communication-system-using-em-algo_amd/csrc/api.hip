@@ -16,7 +16,7 @@ constexpr size_t kAlign = 256;
 size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 struct Carve {
-    size_t mom, R, rhs, done, ysh, prep, tol, winv, ppsi, pS, pflag, total;
+    size_t mom, R, rhs, done, ysh, prep, list, tree, tol, winv, ppsi, pS, pflag, total;
     bool has_prep;
 };
 
@@ -45,7 +45,10 @@ Carve carve(const Problem& pb) {
     c.prep = align_up(c.ysh + (size_t)pb.B * pb.Td * pb.NR * sizeof(cd));   // MFMA sweep prep
     const int ps = estep_prep_stride(pb);
     c.has_prep = ps > 0;
-    c.tol = align_up(c.prep + (size_t)pb.B * pb.Td * ps * sizeof(double));
+    c.list = align_up(c.prep + (size_t)pb.B * pb.Td * ps * sizeof(double));
+    c.tree = align_up(c.list + (2 * (size_t)pb.B * pb.Td + kEstepListCnt) * sizeof(int32_t));
+    c.tol = c.has_prep ? align_up(c.tree + (size_t)pb.B * pb.Td * kTreeRecDoubles * sizeof(double))
+                       : c.list;
     c.ppsi = c.pS = c.pflag = c.winv = c.tol;
     c.total = c.tol;
     if (rbuild_herm_supported(pb)) {         // MFMA R build: Kronecker-factored pilots
@@ -143,6 +146,8 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     ea.cons = (const cd*)p->cons; ea.mom = (cd*)(ws + c.mom); ea.done = early ? done : nullptr;
     ea.status = p->status;
     ea.prep = c.has_prep ? (double*)(ws + c.prep) : nullptr;
+    ea.list = c.has_prep ? (int32_t*)(ws + c.list) : nullptr;
+    ea.tree = c.has_prep ? (double*)(ws + c.tree) : nullptr;
     MstepArgs ma;
     ma.yd = ea.yd; ma.yp = (const cd*)p->y_p; ma.psid = ea.psid; ma.up = (const cd*)p->u_p;
     ma.mom = ea.mom; ma.R = (cd*)(ws + c.R); ma.rhs = (cd*)(ws + c.rhs); ma.theta = (cd*)p->theta;
@@ -204,9 +209,15 @@ int sbce_estep(const sbce_dims* d, const sbce_ptrs* p, int estep_mode, void* mom
     ea.cons = (const cd*)p->cons; ea.mom = (cd*)moments; ea.done = nullptr;
     ea.status = p->status;
     ea.prep = nullptr;               // workspace optional here: use it when it is large enough
+    ea.list = nullptr;
+    ea.tree = nullptr;
     if (p->workspace && aligned16(p->workspace)) {
         const Carve c = carve(pb);
-        if (c.has_prep && p->workspace_bytes >= c.total) ea.prep = (double*)((char*)p->workspace + c.prep);
+        if (c.has_prep && p->workspace_bytes >= c.total) {
+            ea.prep = (double*)((char*)p->workspace + c.prep);
+            ea.list = (int32_t*)((char*)p->workspace + c.list);
+            ea.tree = (double*)((char*)p->workspace + c.tree);
+        }
     }
     return hip_rc(launch_estep(pb, ea, estep_mode, (hipStream_t)hip_stream));
 }
@@ -265,6 +276,14 @@ int sbce_debug_chol_skip(int mask) {
 int sbce_debug_estep_mfma(unsigned long long* out, int reset) {
     if (!reset && !out) return SBCE_EINVAL;
     return hip_rc(estep_debug_mfma(out, reset));
+}
+
+// Diagnostic, not part of include/sbce.h: symbols the sphere pass resolved by enumeration
+// (out3[0]), left to the MFMA sweep (out3[1]) and resolved by the tree pass's single-path check
+// (out3[2]) since the last reset (counted only with SBCE_ESTEP_COUNT=1).
+int sbce_debug_estep_sphere(unsigned long long* out3, int reset) {
+    if (!reset && !out3) return SBCE_EINVAL;
+    return hip_rc(estep_debug_sphere(out3, reset));
 }
 
 int sbce_ser(const sbce_dims* d, const void* x_dest, const void* x_d_true, double* ser_out,

@@ -669,10 +669,28 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     __syncthreads();
 
     const long nsym = (long)c.B * c.Td;
-    const long g0 = ((long)blockIdx.x * kMfmaWaves + wave) * c.spw;
-    if (g0 >= nsym) return;
-    const long g1 = g0 + c.spw < nsym ? g0 + c.spw : nsym;
+    // With a work list (the prep pass's sphere enumeration resolved the other symbols) the
+    // waves grab chunks of spw list entries from a counter until the list is exhausted;
+    // otherwise each wave takes chunk (block, wave) of all symbols.
+    const bool listed = a.list != nullptr;
+    int32_t* cnt = listed ? a.list + nsym : nullptr;
+    const long nwork = listed ? (long)__builtin_amdgcn_readfirstlane(cnt[0]) : nsym;
     const bool prep = a.prep != nullptr;
+    auto sym_of = [&](long gi) -> long { return listed ? (long)a.list[gi] : gi; };
+    for (;;) {
+    long chunk_id;
+    if (listed) {
+        int v = 0;
+        if (lane == 0) v = atomicAdd(cnt + 1, 1);
+        chunk_id = __builtin_amdgcn_readfirstlane(__shfl(v, 0));
+    } else {
+        chunk_id = (long)blockIdx.x * kMfmaWaves + wave;
+    }
+    // listed symbols are the expensive ones: one per grab (a chunk's symbols run in series)
+    const int spw = listed ? 1 : c.spw;
+    const long g0 = chunk_id * spw;
+    if (g0 >= nwork) return;
+    const long g1 = g0 + spw < nwork ? g0 + spw : nwork;
     // The wave's symbols g0 .. g1-1 in turn.  With a prep record, the next symbol's record,
     // y_t and done flag travel by LDS-DMA (global_load_lds: no VGPRs) into the other half of
     // a double buffer while the current symbol is swept; the sweep reads no global memory,
@@ -693,16 +711,17 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                 (const __attribute__((address_space(1))) void*)(a.done + g / c.Td),
                 (__attribute__((address_space(3))) void*)(dst + 128), 4, 0, 0);
     };
-    if (dma) issue(g0, s_recb);
-    for (long gsym = g0; gsym < g1; ++gsym) {
-    const int cur = (int)((gsym - g0) & 1);
+    if (dma) issue(sym_of(g0), s_recb);
+    for (long gi = g0; gi < g1; ++gi) {
+    const long gsym = sym_of(gi);
+    const int cur = (int)((gi - g0) & 1);
     double* s_rec = s_recb + cur * 160;
     int dn;
     if (dma) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this symbol's record has landed
         wave_sync();
         dn = a.done ? reinterpret_cast<const int*>(s_rec + 128)[0] : 0;
-        if (gsym + 1 < g1) issue(gsym + 1, s_recb + (cur ^ 1) * 160);
+        if (gi + 1 < g1) issue(sym_of(gi + 1), s_recb + (cur ^ 1) * 160);
     } else {
         dn = a.done ? a.done[gsym / c.Td] : 0;
         if (prep && !dn) {
@@ -1204,6 +1223,8 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     }
     }();
     }
+    if (!listed) return;
+    }
 }
 
 // ============================================================================
@@ -1217,19 +1238,22 @@ struct PrepConst {
     int B, Td, P, M, lm, nkt, stride;
     int uni;           // wave-uniform theta loads (SBCE_PREP_UNI=0 disables: A/B runs)
     double reg;
+    // sphere pass (estep_sphere_kernel; EstepArgs::list receives the symbols it leaves)
+    int budget;        // DFS steps per symbol before the symbol is left to the sweep
+    int count;         // SBCE_ESTEP_COUNT=1: tally resolved / listed symbols (g_estep_sphere)
+    int hard;          // hard (argmin) E-step: sphere radius without the soft threshold
+    double inv_s2, thr_d;
 };
 
+// Diagnostic (SBCE_ESTEP_COUNT=1): symbols the sphere pass's enumeration resolved, symbols it
+// left to the MFMA sweep, and symbols the tree pass resolved alone (single surviving path).
+__device__ unsigned long long g_estep_sphere[3];
+
+// ---- H_eff(t) = sum_p psi_p H_p (theta of the symbol's trial, psi of the symbol) ----
 template <int NT, int NR>
-__global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst c) {
-    constexpr int NA = NT / 2, NB = NT - NA, NO = NT * NR;
-    const long nsym = (long)c.B * c.Td;
-    const long gsym = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gsym >= nsym) return;
-    const int b = (int)(gsym / c.Td);
-    if (a.done && a.done[b]) return;
-    const int mask = c.M - 1;
-    // ---- H_eff(t) = sum_p psi_p H_p ----
-    cd H[NT][NR];
+__device__ __forceinline__ void heff_load(const EstepArgs& a, const PrepConst& c, long gsym, int b,
+                                          cd (&H)[NT][NR]) {
+    constexpr int NO = NT * NR;
 #pragma unroll
     for (int q = 0; q < NT; ++q)
 #pragma unroll
@@ -1258,85 +1282,98 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
                 for (int r = 0; r < NR; ++r) H[q][r] = cfma(H[q][r], psi, th[p * NO + q * NR + r]);
         }
     }
-    cd y[NR];
+}
+
+// Ridge Cholesky G + reg I = L L^H of G = H^H H (L strictly lower in Lm, pivots piv,
+// 1/sqrt(pivots) dinv) and zf = L^-1 H^H y.
+template <int NT, int NR>
+__device__ __forceinline__ void ridge_chol(const cd (&H)[NT][NR], const cd (&y)[NR], double reg,
+                                           cd (&Lm)[NT][NT], double (&piv)[NT], double (&dinv)[NT],
+                                           cd (&zf)[NT]) {
 #pragma unroll
-    for (int r = 0; r < NR; ++r) y[r] = a.yd[(size_t)gsym * NR + r];
-    double* out = a.prep + (size_t)gsym * c.stride;
+    for (int j = 0; j < NT; ++j) {
+        cd gjj = czero();
 #pragma unroll
-    for (int q = 0; q < NT; ++q)
+        for (int r = 0; r < NR; ++r) gjj = cfmac(gjj, H[j][r], H[j][r]);
+        double d = gjj.x + reg;
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            out[4 + 2 * (q * NR + r)] = H[q][r].x;
-            out[5 + 2 * (q * NR + r)] = H[q][r].y;
-        }
-    // ---- candidate: quantised ridge LS (candidate_distance, same arithmetic order) ----
-    {
-        cd Lm[NT][NT];
-        double dinv[NT];
-        cd z[NT];
+        for (int k = 0; k < j; ++k) d -= cabs2(Lm[j][k]);
+        piv[j] = fmax(d, 1e-300);
+        const double inv = fast_rsqrt(piv[j]);
+        dinv[j] = inv;
 #pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            cd gjj = czero();
-#pragma unroll
-            for (int r = 0; r < NR; ++r) gjj = cfmac(gjj, H[j][r], H[j][r]);
-            double d = gjj.x + c.reg;
-#pragma unroll
-            for (int k = 0; k < j; ++k) d -= cabs2(Lm[j][k]);
-            const double inv = fast_rsqrt(fmax(d, 1e-300));
-            dinv[j] = inv;
-#pragma unroll
-            for (int i = j + 1; i < NT; ++i) {
-                cd s = czero();
-#pragma unroll
-                for (int r = 0; r < NR; ++r) s = cfmac(s, H[j][r], H[i][r]);   // G[i][j]
-#pragma unroll
-                for (int k = 0; k < j; ++k) s = csub(s, cmulc(Lm[i][k], Lm[j][k]));
-                Lm[i][j] = cscale(s, inv);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < NT; ++i) {
+        for (int i = j + 1; i < NT; ++i) {
             cd s = czero();
 #pragma unroll
-            for (int r = 0; r < NR; ++r) s = cfmac(s, y[r], H[i][r]);          // (H^H y)_i
+            for (int r = 0; r < NR; ++r) s = cfmac(s, H[j][r], H[i][r]);   // G[i][j]
 #pragma unroll
-            for (int k = 0; k < i; ++k) s = csub(s, cmul(Lm[i][k], z[k]));
-            z[i] = cscale(s, dinv[i]);
+            for (int k = 0; k < j; ++k) s = csub(s, cmulc(Lm[i][k], Lm[j][k]));
+            Lm[i][j] = cscale(s, inv);
         }
+    }
 #pragma unroll
-        for (int i = NT - 1; i >= 0; --i) {
-            cd s = z[i];
+    for (int i = 0; i < NT; ++i) {
+        cd s = czero();
 #pragma unroll
-            for (int k = i + 1; k < NT; ++k) s = csub(s, cmul(cconj(Lm[k][i]), z[k]));
-            z[i] = cscale(s, dinv[i]);
+        for (int r = 0; r < NR; ++r) s = cfmac(s, y[r], H[i][r]);          // (H^H y)_i
+#pragma unroll
+        for (int k = 0; k < i; ++k) s = csub(s, cmul(Lm[i][k], zf[k]));
+        zf[i] = cscale(s, dinv[i]);
+    }
+}
+
+// Candidate of candidate_distance (same arithmetic order): quantised ridge LS estimate from
+// the factorisation above; returns its distance d0 and the magnitude scale sc.
+template <int NT, int NR>
+__device__ __forceinline__ double prep_candidate(const cd (&H)[NT][NR], const cd (&y)[NR],
+                                                 const cd (&Lm)[NT][NT], const double (&dinv)[NT],
+                                                 const cd (&zf)[NT], const cd* cons, int M,
+                                                 double& sc) {
+    cd z[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) z[i] = zf[i];
+#pragma unroll
+    for (int i = NT - 1; i >= 0; --i) {
+        cd s = z[i];
+#pragma unroll
+        for (int k = i + 1; k < NT; ++k) s = csub(s, cmul(cconj(Lm[k][i]), z[k]));
+        z[i] = cscale(s, dinv[i]);
+    }
+    cd x[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+        double bd = INFINITY;
+        int bs = 0;
+        for (int s = 0; s < M; ++s) {
+            const double dd = cabs2(csub(z[q], cons[s]));
+            if (dd < bd) { bd = dd; bs = s; }
         }
-        cd x[NT];
+        x[q] = cons[bs];
+    }
+    double d0 = 0.0;
+    sc = 0.0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        cd res = y[r];
+        sc += cabs2(res);
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
-            double bd = INFINITY;
-            int bs = 0;
-            for (int s = 0; s < c.M; ++s) {
-                const double dd = cabs2(csub(z[q], a.cons[s]));
-                if (dd < bd) { bd = dd; bs = s; }
-            }
-            x[q] = a.cons[bs];
+            const cd hx = cmul(H[q][r], x[q]);
+            res = csub(res, hx);
+            sc += NT * cabs2(hx);
         }
-        double d0 = 0.0, sc = 0.0;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            cd res = y[r];
-            sc += cabs2(res);
-#pragma unroll
-            for (int q = 0; q < NT; ++q) {
-                const cd hx = cmul(H[q][r], x[q]);
-                res = csub(res, hx);
-                sc += NT * cabs2(hx);
-            }
-            d0 += cabs2(res);
-        }
-        out[0] = d0;
-        out[1] = sc;
+        d0 += cabs2(res);
     }
+    return d0;
+}
+
+// Column-tile bounds (column_tile_bounds) and, for NT = 4, the row-tile bound vectors of
+// one symbol into its prep record `out`.
+template <int NT, int NR>
+__device__ __forceinline__ void prep_bounds(const cd (&H)[NT][NR], const cd (&y)[NR], double* out,
+                                            const cd* cons, const PrepConst& c) {
+    constexpr int NA = NT / 2, NB = NT - NA, NO = NT * NR;
+    const int mask = c.M - 1;
     // ---- column-tile bounds (column_tile_bounds) ----
     {
         cd u[NA][NR];
@@ -1392,7 +1429,7 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
             }
         }
         double cmax2 = 0.0;
-        for (int s = 0; s < c.M; ++s) cmax2 = fmax(cmax2, cabs2(a.cons[s]));
+        for (int s = 0; s < c.M; ++s) cmax2 = fmax(cmax2, cabs2(cons[s]));
         out[2] = sc + NB * cmax2 * g2;
         double* lbo = out + 4 + 2 * NO;
         if (NB == 2 && c.M == 16) {
@@ -1403,7 +1440,7 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
 #pragma unroll
             for (int r = 0; r < NR; ++r) ng += cabs2(g[NB - 1][r]);
             for (int kt = 0; kt < c.nkt; ++kt) {
-                const cd xb0 = a.cons[kt];
+                const cd xb0 = cons[kt];
                 double n0 = 0.0;
                 cd aa = czero();
 #pragma unroll
@@ -1414,7 +1451,7 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
                 }
                 double lbm = INFINITY;
                 for (int s1 = 0; s1 < 16; ++s1) {
-                    const cd x = a.cons[s1];
+                    const cd x = cons[s1];
                     const double lb = fma(cabs2(x), ng, n0 - 2.0 * (x.x * aa.x + x.y * aa.y));
                     lbm = fmin(lbm, lb);
                 }
@@ -1431,7 +1468,7 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
                     cd res = w[r];
 #pragma unroll
                     for (int bb = 0; bb < NB; ++bb)
-                        res = csub(res, cmul(g[bb][r], a.cons[(k >> (c.lm * (NB - 1 - bb))) & mask]));
+                        res = csub(res, cmul(g[bb][r], cons[(k >> (c.lm * (NB - 1 - bb))) & mask]));
                     lb += cabs2(res);
                 }
                 lbm = fmin(lbm, lb);
@@ -1490,6 +1527,450 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
                 rbo[2 * (m * NR + r)] = ok ? w[m][r].x : 0.0;
                 rbo[2 * (m * NR + r) + 1] = ok ? w[m][r].y : 0.0;
             }
+    }
+}
+
+template <int NT, int NR>
+__global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst c) {
+    const long nsym = (long)c.B * c.Td;
+    const long gsym = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gsym >= nsym) return;
+    const int b = (int)(gsym / c.Td);
+    if (a.done && a.done[b]) return;
+    cd H[NT][NR];
+    heff_load<NT, NR>(a, c, gsym, b, H);
+    cd y[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) y[r] = a.yd[(size_t)gsym * NR + r];
+    double* out = a.prep + (size_t)gsym * c.stride;
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            out[4 + 2 * (q * NR + r)] = H[q][r].x;
+            out[5 + 2 * (q * NR + r)] = H[q][r].y;
+        }
+    cd Lm[NT][NT], zf[NT];
+    double piv[NT], dinv[NT], sc;
+    ridge_chol<NT, NR>(H, y, c.reg, Lm, piv, dinv, zf);
+    out[0] = prep_candidate<NT, NR>(H, y, Lm, dinv, zf, a.cons, c.M, sc);
+    out[1] = sc;
+    prep_bounds<NT, NR>(H, y, out, a.cons, c);
+}
+
+// The tile bounds of the symbols the sphere pass left to the sweep (H_eff, d0 and the scale
+// are in their prep records already).  Grid over all symbols; threads past the list exit.
+template <int NT, int NR>
+__global__ __launch_bounds__(256) void estep_bounds_kernel(EstepArgs a, PrepConst c) {
+    const long nsym = (long)c.B * c.Td;
+    const long n = a.list[nsym];
+    const long gi = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gi >= n) return;
+    const long gsym = a.list[gi];
+    double* out = a.prep + (size_t)gsym * c.stride;
+    cd H[NT][NR], y[NR];
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) H[q][r] = cmk(out[4 + 2 * (q * NR + r)], out[5 + 2 * (q * NR + r)]);
+#pragma unroll
+    for (int r = 0; r < NR; ++r) y[r] = a.yd[(size_t)gsym * NR + r];
+    prep_bounds<NT, NR>(H, y, out, a.cons, c);
+}
+
+// ============================================================================
+// Sphere pass (SPH = 1 soft, 2 hard), replacing the preparation pass when n_rx >= n_tx:
+// every symbol's hypotheses inside
+//   d(x) <= R,   R = R0 + 50 varn^2 (soft) / R0 (hard),   R0 = the distance of a real hypothesis,
+// are enumerated exactly -- the hypotheses whose weights are not below e^-50 of the posterior
+// maximum (or that can be the argmin): the set the sweep's tile bounds keep.
+//   Streams are ordered by reliability (diag of (H^H H + reg I)^-1: the least reliable at
+// level 0, the most reliable at the top level NT-1, as in V-BLAST).  With G' = Hp^H Hp + reg I
+// = L L^H for the permuted H and zf = L^-1 Hp^H y:
+//   ||y - Hp x||^2 = c0 + sum_i T_i,   c0 = ||y||^2 - ||zf||^2,
+//   T_i = |L_ii x_i - e_i|^2 - reg |x_i|^2,   e_i = zf_i - sum_{j>i} conj(L_ji) x_j,
+// and T_j >= -reg max|c|^2, so every hypothesis below a level-i node has
+//   d - c0 >= sum_{j>=i} T_j - i reg max|c|^2.
+// Distances are kept relative to c0 (common to all hypotheses of the symbol: it cancels from
+// the weights and the argmin).  R0 = min(candidate, Babai point of the sorted tree).
+// Part 1 (estep_tree_kernel, one THREAD per symbol): H_eff, the sweep's prep record, the
+// ordering, the factorisation, the Babai point -> the symbol's tree record.
+// Part 2 (estep_bfs_kernel, one WAVE per symbol): level by level, every (surviving path,
+// child) pair in its own lane, survivors compacted by ballot into an LDS path list; leaves
+// weighted in the lanes.  Control flow is wave-uniform: a symbol costs what its tree holds.
+// A symbol whose path list outgrows `budget`, or whose G' is ill-conditioned, is listed for
+// the tile bounds and the MFMA sweep.
+// ============================================================================
+constexpr int kTrec = kTreeRecDoubles;   // doubles per symbol of the tree record (NT <= 4)
+constexpr int kBfsWaves = 4;       // waves per block of the enumeration
+constexpr int kBfsSpw = 8;         // consecutive symbols per wave
+constexpr int kBfsPmax = 256;      // path list capacity per level
+
+template <int NT, int NR>
+__global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst c) {
+    const long nsym = (long)c.B * c.Td;
+    const long gsym = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    bool live = gsym < nsym;
+    const int b = live ? (int)(gsym / c.Td) : 0;
+    if (live && a.done && a.done[b]) live = false;
+    bool single = false;
+    if (live) {
+    cd Lm[NT][NT], zf[NT];
+    double piv[NT], dinv[NT], d0, sc;
+    int lev[NT];
+    double c0 = 0.0;
+    {
+        cd H[NT][NR], y[NR];
+        heff_load<NT, NR>(a, c, gsym, b, H);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) y[r] = a.yd[(size_t)gsym * NR + r];
+        double* out = a.prep + (size_t)gsym * c.stride;
+#pragma unroll
+        for (int q = 0; q < NT; ++q)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                out[4 + 2 * (q * NR + r)] = H[q][r].x;
+                out[5 + 2 * (q * NR + r)] = H[q][r].y;
+            }
+        ridge_chol<NT, NR>(H, y, c.reg, Lm, piv, dinv, zf);
+        d0 = prep_candidate<NT, NR>(H, y, Lm, dinv, zf, a.cons, c.M, sc);
+        out[0] = d0;
+        out[1] = sc;
+        // reliability of stream q: g_q = [(G + reg I)^-1]_qq = sum_k |(L^-1)_kq|^2
+        cd W[NT][NT];
+        double g[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            W[j][j] = cmk(dinv[j], 0.0);
+#pragma unroll
+            for (int i = j + 1; i < NT; ++i) {
+                cd s = czero();
+#pragma unroll
+                for (int k = j; k < i; ++k) s = cfma(s, Lm[i][k], W[k][j]);
+                W[i][j] = cscale(s, -dinv[i]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            double s = 0.0;
+#pragma unroll
+            for (int k = q; k < NT; ++k) s += cabs2(W[k][q]);
+            g[q] = s;
+        }
+        // level of stream q = its rank in descending g (ties by index)
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            int rk = 0;
+#pragma unroll
+            for (int p = 0; p < NT; ++p) rk += (g[p] > g[q] || (g[p] == g[q] && p < q)) ? 1 : 0;
+            lev[q] = rk;
+        }
+        cd Hp[NT][NR];
+#pragma unroll
+        for (int l = 0; l < NT; ++l)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                cd v = H[0][r];
+#pragma unroll
+                for (int q = 1; q < NT; ++q) v = csel(lev[q] == l, H[q][r], v);
+                Hp[l][r] = v;
+            }
+        ridge_chol<NT, NR>(Hp, y, c.reg, Lm, piv, dinv, zf);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) c0 += cabs2(y[r]);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) c0 -= cabs2(zf[j]);
+    }
+    double ui[NT];
+    double pmin = piv[0], pmax = piv[0];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        ui[j] = piv[j] * dinv[j];                          // L_jj = sqrt(pivot)
+        pmin = fmin(pmin, piv[j]);
+        pmax = fmax(pmax, piv[j]);
+    }
+    // Babai point of the sorted tree: the nearest child level by level
+    double db = 0.0, cmax2 = 0.0;
+    cd xb[NT], eb[NT];
+    int sb[NT];
+#pragma unroll
+    for (int l = NT - 1; l >= 0; --l) {
+        cd e = zf[l];
+#pragma unroll
+        for (int j = l + 1; j < NT; ++j) e = csub(e, cmul(cconj(Lm[j][l]), xb[j]));
+        const double aa = fma(ui[l], ui[l], -c.reg), m2u = -2.0 * ui[l];
+        double tb = INFINITY;
+        int si = 0;
+        for (int s = 0; s < c.M; ++s) {
+            const cd x = a.cons[s];
+            const double x2 = cabs2(x);
+            cmax2 = fmax(cmax2, x2);
+            const double t = fma(aa, x2, m2u * fma(x.x, e.x, x.y * e.y));
+            if (t < tb) { tb = t; si = s; }
+        }
+        xb[l] = a.cons[si];
+        sb[l] = si;
+        eb[l] = e;
+        db += tb + cabs2(e);
+    }
+    const bool ok = pmax <= 1e10 * pmin;                 // ill-conditioned G': to the sweep
+    const double R0 = fmin(d0 - c0, db);
+    // single-path check: if along the Babai path every level has exactly one child whose
+    // subtree bound is inside R (the Babai child), the Babai point is the only hypothesis
+    // inside the sphere -- the posterior is x_B (weights of all others < e^-50) / the argmin
+    if (ok && db <= R0) {
+        const double R = R0 + (c.hard ? 0.0 : c.thr_d) + 1e-9 * sc;
+        const double slack = c.reg * cmax2;
+        double base = 0.0;
+        bool one = true;
+#pragma unroll
+        for (int l = NT - 1; l >= 0; --l) {
+            const cd e = eb[l];
+            const double aa = fma(ui[l], ui[l], -c.reg), m2u = -2.0 * ui[l];
+            const double thr = R + l * slack - base - cabs2(e);
+            int n = 0;
+            for (int s = 0; s < c.M; ++s) {
+                const cd x = a.cons[s];
+                n += fma(aa, cabs2(x), m2u * fma(x.x, e.x, x.y * e.y)) <= thr ? 1 : 0;
+            }
+            one = one && n == 1;
+            const cd x = xb[l];
+            base += fma(aa, cabs2(x), m2u * fma(x.x, e.x, x.y * e.y)) + cabs2(e);
+        }
+        if (one) {
+            single = true;
+            constexpr int MS = NT + NT * NT;
+            cd xo[NT];                                   // stream order
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
+                cd v = xb[0];
+#pragma unroll
+                for (int l = 1; l < NT; ++l) v = csel(lev[q] == l, xb[l], v);
+                xo[q] = v;
+            }
+            cd* mo = a.mom + (size_t)gsym * MS;
+#pragma unroll
+            for (int p2 = 0; p2 < NT; ++p2) {
+                mo[p2] = xo[p2];
+#pragma unroll
+                for (int q = 0; q < NT; ++q) mo[NT + p2 * NT + q] = cmulc(xo[p2], xo[q]);
+            }
+        }
+    }
+    int packed = ok ? (1 << 16) : 0;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) packed |= q << (4 * lev[q]);   // level l holds stream perm[l]
+    double* rec = a.tree + (size_t)gsym * kTrec;
+    rec[0] = c0;
+    rec[1] = R0;
+    rec[2] = sc;
+    rec[3] = (double)packed;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        rec[4 + j] = ui[j];
+        rec[4 + NT + 2 * j] = zf[j].x;
+        rec[5 + NT + 2 * j] = zf[j].y;
+    }
+    int k = 0;
+#pragma unroll
+    for (int i = 1; i < NT; ++i)
+#pragma unroll
+        for (int j = 0; j < i; ++j) {
+            rec[4 + 3 * NT + 2 * k] = Lm[i][j].x;
+            rec[5 + 3 * NT + 2 * k] = Lm[i][j].y;
+            ++k;
+        }
+    }   // live
+    // the other live symbols go to the enumeration's list: one atomic per wave
+    const bool enumer = live && !single;
+    const int lane = threadIdx.x & 63;
+    const unsigned long long bal = __ballot(enumer);
+    int32_t* cnt = a.list + nsym;
+    if (bal) {
+        const int first = __builtin_ctzll(bal);
+        int base = 0;
+        if (lane == first) base = atomicAdd(cnt + 2, __builtin_popcountll(bal));
+        base = __shfl(base, first);
+        if (enumer)
+            cnt[kEstepListCnt + base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = (int32_t)gsym;
+    }
+    if (c.count) {
+        const unsigned long long one = __ballot(single);
+        if (lane == 0) atomicAdd(&g_estep_sphere[2], (unsigned long long)__builtin_popcountll(one));
+    }
+}
+
+template <int NT, int SPH>
+__global__ __launch_bounds__(64 * kBfsWaves) void estep_bfs_kernel(EstepArgs a, PrepConst c) {
+    typedef unsigned long long u64;
+    constexpr int NP = NT * (NT - 1) / 2;
+    constexpr int MS = NT + NT * NT;
+    __shared__ cd s_cons[64];
+    __shared__ double s_c2[64];
+    __shared__ double s_pb[kBfsWaves][2][kBfsPmax];     // path bound (relative distance so far)
+    __shared__ int s_pi[kBfsWaves][2][kBfsPmax];        // path symbols, level l at bits lm*l
+    if ((int)threadIdx.x < c.M) {
+        const cd x = a.cons[threadIdx.x];
+        s_cons[threadIdx.x] = x;
+        s_c2[threadIdx.x] = cabs2(x);
+    }
+    __syncthreads();
+    double cmax2 = 0.0;
+    for (int s = 0; s < c.M; ++s) cmax2 = fmax(cmax2, s_c2[s]);
+    const double slack = c.reg * cmax2;                  // per level below: T_j >= -slack
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const long nsym = (long)c.B * c.Td;
+    // the tree pass's enumeration list: wave w takes entries w*spw .. (w+1)*spw - 1
+    const int32_t* elist = a.list + nsym + kEstepListCnt;
+    const long nwork = __builtin_amdgcn_readfirstlane(a.list[nsym + 2]);
+    const long g0 = ((long)blockIdx.x * kBfsWaves + wave) * kBfsSpw;
+    if (g0 >= nwork) return;
+    const long g1 = g0 + kBfsSpw < nwork ? g0 + kBfsSpw : nwork;
+    const int mask = c.M - 1, lm = c.lm;
+    const int pmax = c.budget < kBfsPmax ? c.budget : kBfsPmax;
+    const u64 lt = (1ull << lane) - 1ull;
+    unsigned listed_mask = 0, resolved_n = 0;
+    for (long gi = g0; gi < g1; ++gi) {
+        const long gsym = elist[gi];
+        const double* rec = a.tree + (size_t)gsym * kTrec;
+        const int packed = (int)rec[3];
+        bool listed = !((packed >> 16) & 1);
+        const double R0 = rec[1];
+        const double margin = 1e-9 * rec[2];
+        const double R = R0 + (SPH == 2 ? 0.0 : c.thr_d) + margin;
+        double ui[NT];
+        cd zf[NT], Lc[NP + 1];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            ui[j] = rec[4 + j];
+            zf[j] = cmk(rec[4 + NT + 2 * j], rec[5 + NT + 2 * j]);
+        }
+#pragma unroll
+        for (int k = 0; k < NP; ++k) Lc[k] = cmk(rec[4 + 3 * NT + 2 * k], -rec[5 + 3 * NT + 2 * k]);  // conj
+        double bd = INFINITY;            // hard: this lane's best (distance, hypothesis index)
+        int bj = 0x7fffffff;
+        if (lane == 0) { s_pb[wave][0][0] = 0.0; s_pi[wave][0][0] = 0; }
+        wave_sync();
+        int n_in = 1;                    // paths entering the level; after level 0: leaves
+#pragma unroll
+        for (int l = NT - 1; l >= 0; --l) {
+            if (listed) break;
+            const int ib = (NT - 1 - l) & 1;
+            const double* pbi = s_pb[wave][ib];
+            const int* pii = s_pi[wave][ib];
+            double* pbo = s_pb[wave][ib ^ 1];
+            int* pio = s_pi[wave][ib ^ 1];
+            const double u = ui[l];
+            const double aa = fma(u, u, -c.reg), m2u = -2.0 * u;
+            const double lim = R + l * slack;
+            const int total = n_in << lm;
+            int n_out = 0;
+            for (int base = 0; base < total; base += 64) {
+                const int i = base + lane;
+                const bool valid = i < total;
+                const int p = valid ? i >> lm : 0;
+                const int s = i & mask;
+                const double bp = pbi[p];
+                const int ip = pii[p];
+                cd e = zf[l];
+#pragma unroll
+                for (int j = l + 1; j < NT; ++j)      // L_jl at row-major strict index j(j-1)/2 + l
+                    e = csub(e, cmul(Lc[j * (j - 1) / 2 + l], s_cons[(ip >> (lm * j)) & mask]));
+                const cd x = s_cons[s];
+                const double bb = bp + fma(aa, s_c2[s], m2u * fma(x.x, e.x, x.y * e.y)) + cabs2(e);
+                const bool keep = valid && bb <= lim;
+                const int idx = ip | (s << (lm * l));
+                if (SPH == 2 && l == 0) {
+                    if (keep) {
+                        int jr = 0;                   // hypothesis index, original stream order
+#pragma unroll
+                        for (int q = 0; q < NT; ++q)
+                            jr |= ((idx >> (lm * q)) & mask) << (lm * (NT - 1 - ((packed >> (4 * q)) & 15)));
+                        if (bb < bd || (bb == bd && jr < bj)) { bd = bb; bj = jr; }
+                    }
+                } else {
+                    // surviving paths (l > 0) / leaves inside the sphere (l == 0, soft)
+                    const u64 bal = __ballot(keep);
+                    const int slot = n_out + __builtin_popcountll(bal & lt);
+                    if (keep && slot < pmax) { pbo[slot] = bb; pio[slot] = idx; }
+                    n_out += __builtin_popcountll(bal);
+                }
+            }
+            if (SPH == 2 && l == 0) break;
+            if (n_out > pmax || n_out == 0) listed = true;    // too wide (or rounding lost all)
+            n_in = n_out;
+            wave_sync();
+        }
+        cd* mo = a.mom + (size_t)gsym * MS;
+        if (!listed) {
+            if constexpr (SPH == 2) {
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    const double od = shfl_xor_d(bd, off);
+                    const int oj = __shfl_xor(bj, off);
+                    if (od < bd || (od == bd && oj < bj)) { bd = od; bj = oj; }
+                }
+                if (bj == 0x7fffffff) listed = true;
+                else if (lane < MS) {
+                    const int p2 = lane < NT ? lane : (lane - NT) / NT;
+                    const int q = lane < NT ? 0 : (lane - NT) % NT;
+                    const cd xp = s_cons[(bj >> (lm * (NT - 1 - p2))) & mask];
+                    const cd xq = s_cons[(bj >> (lm * (NT - 1 - q))) & mask];
+                    mo[lane] = lane < NT ? xp : cmulc(xp, xq);
+                }
+            } else {
+                // the n_in leaves inside the sphere (LDS list, level order): lane o < MS forms
+                // output o (m_t, then S_t row-major, stream order) over the list, weights
+                // exp(-(d - d_min)/varn^2) for the leaves within 50 varn^2 of the minimum
+                const int ib = NT & 1;
+                const double* lb = s_pb[wave][ib];
+                const int* li = s_pi[wave][ib];
+                double dmin = INFINITY;
+                for (int k = 0; k < n_in; ++k) dmin = fmin(dmin, lb[k]);
+                if (lane < MS) {
+                    const int sp_ = lane < NT ? lane : (lane - NT) / NT;   // output stream pair
+                    const int sq_ = lane < NT ? 0 : (lane - NT) % NT;
+                    int lp = 0, lq = 0;                                    // their levels
+#pragma unroll
+                    for (int l = 0; l < NT; ++l) {
+                        const int st = (packed >> (4 * l)) & 15;
+                        lp = st == sp_ ? l : lp;
+                        lq = st == sq_ ? l : lq;
+                    }
+                    double z = 0.0;
+                    cd v = czero();
+                    for (int k = 0; k < n_in; ++k) {
+                        const double d = lb[k];
+                        if (d <= dmin + c.thr_d) {
+                            const double w = fexp_neg((dmin - d) * c.inv_s2);
+                            const int id = li[k];
+                            const cd xp = s_cons[(id >> (lm * lp)) & mask];
+                            const cd xq = s_cons[(id >> (lm * lq)) & mask];
+                            z += w;
+                            v = caxpy(v, w, lane < NT ? xp : cmulc(xp, xq));
+                        }
+                    }
+                    mo[lane] = cscale(v, 1.0 / z);
+                }
+            }
+        }
+        wave_sync();
+        if (listed) listed_mask |= 1u << (gi - g0);
+        else ++resolved_n;
+    }
+    // the wave's listed symbols join the sweep's work list: one atomic per wave
+    const int nl = __builtin_popcount(listed_mask);
+    if (nl) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(a.list + nsym, nl);
+        base = __shfl(base, 0);
+        if (lane < kBfsSpw && ((listed_mask >> lane) & 1))
+            a.list[base + __builtin_popcount(listed_mask & ((1u << lane) - 1u))] = elist[g0 + lane];
+    }
+    if (c.count && lane == 0) {
+        atomicAdd(&g_estep_sphere[0], (unsigned long long)resolved_n);
+        atomicAdd(&g_estep_sphere[1], (unsigned long long)nl);
     }
 }
 
@@ -1684,6 +2165,15 @@ hipError_t dispatch_nr(int NR, const Geometry& g, const EstepArgs& a, int mode, 
 
 }  // namespace
 
+hipError_t estep_debug_sphere(unsigned long long* out3, int reset) {
+    if (reset) {
+        const unsigned long long z[3] = {0, 0, 0};
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_estep_sphere), z, sizeof(z), 0, hipMemcpyHostToDevice);
+    }
+    return hipMemcpyFromSymbol(out3, HIP_SYMBOL(g_estep_sphere), 3 * sizeof(*out3), 0,
+                               hipMemcpyDeviceToHost);
+}
+
 hipError_t estep_debug_mfma(unsigned long long* out, int reset) {
     if (reset) {
         const unsigned long long z = 0;
@@ -1715,31 +2205,73 @@ hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStre
     long mblocks;
     if (!force_valu && make_mfma(pb, mc, mlds, mblocks)) {
         if (mblocks == 0) return hipSuccess;
+        EstepArgs as = a;            // the sweep's view: list only when the sphere pass ran
         if (a.prep) {
             PrepConst pc;
             pc.B = pb.B; pc.Td = pb.Td; pc.P = pb.P; pc.M = pb.M; pc.lm = mc.lm;
             pc.nkt = mc.JB >> 4; pc.stride = mc.prep_stride; pc.reg = mc.reg;
             const char* un = getenv("SBCE_PREP_UNI");
             pc.uni = !(un && un[0] == '0');
+            // sphere pass instead of the preparation pass (SBCE_ESTEP_SPHERE=0 disables: A/B);
+            // n_rx < n_tx (singular H^H H) always leaves the symbol to the sweep: not compiled
+            const char* sp = getenv("SBCE_ESTEP_SPHERE");
+            const bool sphere = a.list && a.tree && pb.NR >= pb.NT && !(sp && sp[0] == '0');
+            const char* bu = getenv("SBCE_SPHERE_BUDGET");      // path list cap per level
+            pc.budget = bu ? atoi(bu) : 128;
+            pc.count = mc.count;
+            pc.inv_s2 = mc.inv_s2;
+            pc.thr_d = mc.thr_d;
+            pc.hard = mode == SBCE_ESTEP_HARD;
+            if (!sphere) as.list = nullptr;
             const long nsym = (long)pb.B * pb.Td;
             const dim3 pg((unsigned)((nsym + 255) / 256)), pblk(256);
             hipError_t e = hipErrorInvalidValue;
-            switch (pb.NT * 16 + pb.NR) {
-#define SBCE_PREP(nt, nr) case nt * 16 + nr: hipLaunchKernelGGL((estep_prep_kernel<nt, nr>), pg, pblk, 0, s, a, pc); e = hipGetLastError(); break;
-                SBCE_PREP(2, 1) SBCE_PREP(2, 2) SBCE_PREP(2, 3) SBCE_PREP(2, 4)
-                SBCE_PREP(2, 5) SBCE_PREP(2, 6) SBCE_PREP(2, 7) SBCE_PREP(2, 8)
-                SBCE_PREP(3, 1) SBCE_PREP(3, 2) SBCE_PREP(3, 3) SBCE_PREP(3, 4)
-                SBCE_PREP(3, 5) SBCE_PREP(3, 6) SBCE_PREP(3, 7) SBCE_PREP(3, 8)
-                SBCE_PREP(4, 1) SBCE_PREP(4, 2) SBCE_PREP(4, 3) SBCE_PREP(4, 4)
-                SBCE_PREP(4, 5) SBCE_PREP(4, 6) SBCE_PREP(4, 7) SBCE_PREP(4, 8)
+            if (sphere) {
+                // sphere pass (tree records, enumeration), then the tile bounds of the listed
+                if (hipMemsetAsync(a.list + nsym, 0, 3 * sizeof(int32_t), s) != hipSuccess)
+                    return hipGetLastError();
+                const long nbfs = (nsym + kBfsSpw * kBfsWaves - 1) / (kBfsSpw * kBfsWaves);
+                const dim3 bg((unsigned)nbfs), bblk(64 * kBfsWaves);
+                const bool hard = mode == SBCE_ESTEP_HARD;
+                switch (pb.NT * 16 + pb.NR) {
+#define SBCE_SPH(nt, nr) case nt * 16 + nr: \
+    hipLaunchKernelGGL((estep_tree_kernel<nt, nr>), pg, pblk, 0, s, as, pc); \
+    if (hard) hipLaunchKernelGGL((estep_bfs_kernel<nt, 2>), bg, bblk, 0, s, as, pc); \
+    else hipLaunchKernelGGL((estep_bfs_kernel<nt, 1>), bg, bblk, 0, s, as, pc); \
+    e = hipGetLastError(); \
+    if (e == hipSuccess) { hipLaunchKernelGGL((estep_bounds_kernel<nt, nr>), pg, pblk, 0, s, as, pc); \
+                           e = hipGetLastError(); } \
+    break;
+                    SBCE_SPH(2, 2) SBCE_SPH(2, 3) SBCE_SPH(2, 4) SBCE_SPH(2, 5)
+                    SBCE_SPH(2, 6) SBCE_SPH(2, 7) SBCE_SPH(2, 8)
+                    SBCE_SPH(3, 3) SBCE_SPH(3, 4) SBCE_SPH(3, 5) SBCE_SPH(3, 6) SBCE_SPH(3, 7)
+                    SBCE_SPH(3, 8)
+                    SBCE_SPH(4, 4) SBCE_SPH(4, 5) SBCE_SPH(4, 6) SBCE_SPH(4, 7) SBCE_SPH(4, 8)
+#undef SBCE_SPH
+                }
+            } else {
+                switch (pb.NT * 16 + pb.NR) {
+#define SBCE_PREP(nt, nr) case nt * 16 + nr: hipLaunchKernelGGL((estep_prep_kernel<nt, nr>), pg, pblk, 0, s, as, pc); e = hipGetLastError(); break;
+                    SBCE_PREP(2, 1) SBCE_PREP(2, 2) SBCE_PREP(2, 3) SBCE_PREP(2, 4)
+                    SBCE_PREP(2, 5) SBCE_PREP(2, 6) SBCE_PREP(2, 7) SBCE_PREP(2, 8)
+                    SBCE_PREP(3, 1) SBCE_PREP(3, 2) SBCE_PREP(3, 3) SBCE_PREP(3, 4)
+                    SBCE_PREP(3, 5) SBCE_PREP(3, 6) SBCE_PREP(3, 7) SBCE_PREP(3, 8)
+                    SBCE_PREP(4, 1) SBCE_PREP(4, 2) SBCE_PREP(4, 3) SBCE_PREP(4, 4)
+                    SBCE_PREP(4, 5) SBCE_PREP(4, 6) SBCE_PREP(4, 7) SBCE_PREP(4, 8)
 #undef SBCE_PREP
+                }
             }
             if (e != hipSuccess) return e;
+            // listed sweep: waves grab work until the list is exhausted, so a grid that
+            // fills the chip (8 two-wave blocks per CU) is enough
+            if (sphere && mblocks > 2048) mblocks = 2048;
+        } else {
+            as.list = nullptr;
         }
         switch (pb.NT) {
-            case 2: return dispatch_mfma_nr<2>(pb.NR, mc, mlds, mblocks, a, mode, s);
-            case 3: return dispatch_mfma_nr<3>(pb.NR, mc, mlds, mblocks, a, mode, s);
-            case 4: return dispatch_mfma_nr<4>(pb.NR, mc, mlds, mblocks, a, mode, s);
+            case 2: return dispatch_mfma_nr<2>(pb.NR, mc, mlds, mblocks, as, mode, s);
+            case 3: return dispatch_mfma_nr<3>(pb.NR, mc, mlds, mblocks, as, mode, s);
+            case 4: return dispatch_mfma_nr<4>(pb.NR, mc, mlds, mblocks, as, mode, s);
         }
     }
     Geometry g;

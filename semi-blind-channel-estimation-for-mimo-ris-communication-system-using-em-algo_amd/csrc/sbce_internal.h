@@ -120,7 +120,13 @@ struct EstepArgs {
     int32_t* status;   // [B] or null (detector index flag)
     double* prep;      // [B*Td][estep_prep_stride] workspace of the MFMA sweep, or null
                        // (then the sweep kernel prepares each symbol itself)
+    int32_t* list;     // [B*Td] symbols the sphere pass left to the sweep, 16 counters
+                       // (0 listed, 1 grabbed by the sweep, 2 listed for the enumeration),
+                       // [B*Td] symbols the tree pass left to the enumeration; null: no sphere
+    double* tree;      // [B*Td][32] the sphere pass's per-symbol search-tree records
 };
+constexpr int kTreeRecDoubles = 32;
+constexpr int kEstepListCnt = 16;      // int32 counters after the sweep's list
 
 struct MstepArgs {
     const cd* yd;
@@ -175,6 +181,7 @@ hipError_t launch_sup_shift_mom(const Problem& pb, cd* mom, const cd* xsup, cons
 hipError_t launch_ser(const Problem& pb, const cd* xdest, const cd* xtrue, double* out,
                       hipStream_t s);
 hipError_t estep_debug_mfma(unsigned long long* out, int reset);   // SBCE_ESTEP_COUNT=1
+hipError_t estep_debug_sphere(unsigned long long* out3, int reset);   // [enumerated, listed, single path]
 hipError_t launch_gauss_rank1(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_gauss_expand(const Problem& pb, const cd* theta, cd* out, hipStream_t s);
 hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* out,

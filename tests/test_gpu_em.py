@@ -209,28 +209,70 @@ def test_singular_system_flags_and_drop_mode(sbce):
                                    # and 2 (span(h1, h3) is all of C^2: the bounds are 0)
                                    (4, 8, 6, 16, 8, 16, 25), (4, 2, 6, 16, 8, 16, 30)])
 def test_mfma_and_valu_estep_agree(sbce, shape, monkeypatch):
-    """The FP64-MFMA E-step (with its preparation pass, with in-kernel preparation, and
-    with the exact tile bounds disabled) and the VALU E-step compute the same posterior
+    """The FP64-MFMA E-step (with its preparation pass, with in-kernel preparation, with
+    the exact tile bounds disabled, with and without the preparation pass's sphere
+    enumeration at several step budgets) and the VALU E-step compute the same posterior
     moments; hard decisions are identical."""
     n_tx, n_rx, N, T_p, T_d, M, snr = shape
     varn = float(sbce.signal_model.snr_to_varn(snr))
     b = sbce.signal_model.synthetic_batch(3, n_tx, n_rx, N, T_p, T_d, M, varn, seed=21)
     out = {}
-    for impl, ws, prune in (("mfma", True, "1"), ("mfma", False, "1"), ("mfma", True, "0"),
-                            ("valu", True, "1")):
+    # (impl, workspace, tile bounds, sphere pass, sphere budget): the sphere pass resolves
+    # symbols in the preparation kernel; budget 1 lists every symbol for the sweep, 6 a mix
+    for impl, ws, prune, sph, bud in (("mfma", True, "1", "1", "48"), ("mfma", False, "1", "1", "48"),
+                                      ("mfma", True, "0", "0", "48"), ("mfma", True, "1", "0", "48"),
+                                      ("mfma", True, "1", "1", "1"), ("mfma", True, "1", "1", "6"),
+                                      ("valu", True, "1", "1", "48")):
         monkeypatch.setenv("SBCE_ESTEP_IMPL", impl)
         monkeypatch.setenv("SBCE_ESTEP_PRUNE", prune)
-        out[(impl, ws, prune)] = [sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"],
-                                                   varn, n_tx, m, workspace=ws)
-                                  for m in ("soft", "hard")]
+        monkeypatch.setenv("SBCE_ESTEP_SPHERE", sph)
+        monkeypatch.setenv("SBCE_SPHERE_BUDGET", bud)
+        out[(impl, ws, prune, sph, bud)] = [
+            sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx, m,
+                             workspace=ws)
+            for m in ("soft", "hard")]
     scale = np.abs(b["cons"]).max() ** 2
-    ref = out[("valu", True, "1")]
+    ref = out[("valu", True, "1", "1", "48")]
     for key, res in out.items():
         (m1, S1), (mh1, _) = res
         (m2, S2), (mh2, _) = ref
         assert np.abs(m1 - m2).max() < 1e-11 * scale, key
         assert np.abs(S1 - S2).max() < 1e-11 * scale, key
         assert np.array_equal(mh1, mh2), key
+
+
+@pytest.mark.parametrize("snr", [25, 20, 10, 0])
+def test_sphere_estep_cfg1_geometry(sbce, snr, monkeypatch):
+    """BASELINE cfg-1 geometry (n_tx = n_rx = 4, N_RIS = 64, 16-QAM): the preparation pass's
+    sphere enumeration (default) against the tile sweep alone (SBCE_ESTEP_SPHERE=0), soft
+    moments and hard decisions, at theta_0 and near the true channel; at 20 dB and above the
+    sphere pass resolves most symbols itself (device counters, SBCE_ESTEP_COUNT=1)."""
+    import ctypes
+    varn = float(sbce.signal_model.snr_to_varn(snr))
+    b = sbce.signal_model.synthetic_batch(4, 4, 4, 64, 16, 64, 16, varn, seed=5 + snr)
+    lib = sbce._lib.load()
+    scale = np.abs(b["cons"]).max() ** 2
+    for th in (b["theta0"], b["h"] + 0.05 * b["theta0"] / np.abs(b["theta0"]).max()):
+        res = {}
+        for sph in ("1", "0"):
+            monkeypatch.setenv("SBCE_ESTEP_SPHERE", sph)
+            monkeypatch.setenv("SBCE_ESTEP_COUNT", "1")
+            lib.sbce_debug_estep_sphere(None, 1)
+            res[sph] = [sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], th, varn, 4, m)
+                        for m in ("soft", "hard")]
+            cnt = (ctypes.c_ulonglong * 3)()
+            lib.sbce_debug_estep_sphere(cnt, 0)
+            if sph == "1":
+                # [enumerated, left to the sweep, single surviving path]
+                resolved, listed = cnt[0] + cnt[2], cnt[1]
+                assert resolved + listed == 2 * 4 * 64
+                if snr >= 20 and th is not b["theta0"]:
+                    assert resolved > listed, (resolved, listed)
+        (m1, S1), (mh1, _) = res["1"]
+        (m0, S0), (mh0, _) = res["0"]
+        assert np.abs(m1 - m0).max() < 1e-11 * scale
+        assert np.abs(S1 - S0).max() < 1e-11 * scale
+        assert np.array_equal(mh1, mh0)
 
 
 def test_snr_sweep_entry_point_reproduces_reference_curve(sbce):

@@ -11,8 +11,8 @@ B = int(os.environ.get("B", "1000"))
 varn = float(pkg.signal_model.snr_to_varn(float(os.environ.get("SNR", "20"))))
 batch = pkg.signal_model.synthetic_batch(B, 4, 4, 64, 16, 256, 16, varn, seed=0)
 eng = pkg.EMEngine(batch, varn)
-eng.run(2)
-for _ in range(3):
+eng.run(int(os.environ.get("ITERS", "2")))
+for _ in range(int(os.environ.get("REPS", "3"))):
     eng.estep()
 torch.cuda.synchronize()
 print("ok")
