@@ -1344,6 +1344,7 @@ __device__ __forceinline__ double prep_candidate(const cd (&H)[NT][NR], const cd
     for (int q = 0; q < NT; ++q) {
         double bd = INFINITY;
         int bs = 0;
+        #pragma unroll 4
         for (int s = 0; s < M; ++s) {
             const double dd = cabs2(csub(z[q], cons[s]));
             if (dd < bd) { bd = dd; bs = s; }
@@ -1530,8 +1531,18 @@ __device__ __forceinline__ void prep_bounds(const cd (&H)[NT][NR], const cd (&y)
     }
 }
 
+// The constellation in LDS (wave-uniform loops over it read broadcasts instead of issuing a
+// dependent global load per point); every thread of the block must call it.
+__device__ __forceinline__ const cd* stage_cons(const cd* cons, int M) {
+    __shared__ cd s_cons[64];
+    if ((int)threadIdx.x < M) s_cons[threadIdx.x] = cons[threadIdx.x];
+    __syncthreads();
+    return s_cons;
+}
+
 template <int NT, int NR>
 __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst c) {
+    const cd* cons = stage_cons(a.cons, c.M);
     const long nsym = (long)c.B * c.Td;
     const long gsym = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gsym >= nsym) return;
@@ -1553,15 +1564,16 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
     cd Lm[NT][NT], zf[NT];
     double piv[NT], dinv[NT], sc;
     ridge_chol<NT, NR>(H, y, c.reg, Lm, piv, dinv, zf);
-    out[0] = prep_candidate<NT, NR>(H, y, Lm, dinv, zf, a.cons, c.M, sc);
+    out[0] = prep_candidate<NT, NR>(H, y, Lm, dinv, zf, cons, c.M, sc);
     out[1] = sc;
-    prep_bounds<NT, NR>(H, y, out, a.cons, c);
+    prep_bounds<NT, NR>(H, y, out, cons, c);
 }
 
 // The tile bounds of the symbols the sphere pass left to the sweep (H_eff, d0 and the scale
 // are in their prep records already).  Grid over all symbols; threads past the list exit.
 template <int NT, int NR>
 __global__ __launch_bounds__(256) void estep_bounds_kernel(EstepArgs a, PrepConst c) {
+    const cd* cons = stage_cons(a.cons, c.M);
     const long nsym = (long)c.B * c.Td;
     const long n = a.list[nsym];
     const long gi = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1575,7 +1587,7 @@ __global__ __launch_bounds__(256) void estep_bounds_kernel(EstepArgs a, PrepCons
         for (int r = 0; r < NR; ++r) H[q][r] = cmk(out[4 + 2 * (q * NR + r)], out[5 + 2 * (q * NR + r)]);
 #pragma unroll
     for (int r = 0; r < NR; ++r) y[r] = a.yd[(size_t)gsym * NR + r];
-    prep_bounds<NT, NR>(H, y, out, a.cons, c);
+    prep_bounds<NT, NR>(H, y, out, cons, c);
 }
 
 // ============================================================================
@@ -1608,6 +1620,7 @@ constexpr int kBfsPmax = 256;      // path list capacity per level
 
 template <int NT, int NR>
 __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst c) {
+    const cd* cons = stage_cons(a.cons, c.M);
     const long nsym = (long)c.B * c.Td;
     const long gsym = (long)blockIdx.x * blockDim.x + threadIdx.x;
     bool live = gsym < nsym;
@@ -1633,7 +1646,7 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
                 out[5 + 2 * (q * NR + r)] = H[q][r].y;
             }
         ridge_chol<NT, NR>(H, y, c.reg, Lm, piv, dinv, zf);
-        d0 = prep_candidate<NT, NR>(H, y, Lm, dinv, zf, a.cons, c.M, sc);
+        d0 = prep_candidate<NT, NR>(H, y, Lm, dinv, zf, cons, c.M, sc);
         out[0] = d0;
         out[1] = sc;
         // reliability of stream q: g_q = [(G + reg I)^-1]_qq = sum_k |(L^-1)_kq|^2
@@ -1701,14 +1714,15 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
         const double aa = fma(ui[l], ui[l], -c.reg), m2u = -2.0 * ui[l];
         double tb = INFINITY;
         int si = 0;
+        #pragma unroll 4
         for (int s = 0; s < c.M; ++s) {
-            const cd x = a.cons[s];
+            const cd x = cons[s];
             const double x2 = cabs2(x);
             cmax2 = fmax(cmax2, x2);
             const double t = fma(aa, x2, m2u * fma(x.x, e.x, x.y * e.y));
             if (t < tb) { tb = t; si = s; }
         }
-        xb[l] = a.cons[si];
+        xb[l] = cons[si];
         sb[l] = si;
         eb[l] = e;
         db += tb + cabs2(e);
@@ -1729,8 +1743,9 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
             const double aa = fma(ui[l], ui[l], -c.reg), m2u = -2.0 * ui[l];
             const double thr = R + l * slack - base - cabs2(e);
             int n = 0;
+            #pragma unroll 4
             for (int s = 0; s < c.M; ++s) {
-                const cd x = a.cons[s];
+                const cd x = cons[s];
                 n += fma(aa, cabs2(x), m2u * fma(x.x, e.x, x.y * e.y)) <= thr ? 1 : 0;
             }
             one = one && n == 1;
