@@ -678,15 +678,16 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip, CholGeom g) {
 // needs the register budget of a whole trial's tiles.  y lives in the rhs buffer.
 //
 // panel_update_kernel (jb > 0): C_tau = A[rows tau, jb:jb+32] - L[rows tau, 0:jb] L[jb:jb+32, 0:jb]^H
-// for the 16-row tiles tau = 0.. of panel jb; block = 4 waves = 4 row tiles of ONE trial,
+// for the 16-row tiles tau = 0.. of panel jb; block = NWU waves = NWU row tiles of ONE trial,
 // the panel's top rows staged per KBU-column chunk in LDS by LDS-DMA (shared B operand),
 // each wave's rows streamed from R with the next 16 columns in flight; every A value
 // feeds both 16-column halves (the left-looking re-reads of a 16-column panel halved).
 // Blocks of one trial sit on one XCD.
 constexpr int KBU = 64;
 constexpr int PW = 32;    // panel width: two 16-column sub-panels
-__global__ __launch_bounds__(256) void panel_update_kernel(MstepArgs a, int L, int jb, int ntile,
-                                                           int gpt, int skip) {
+template <int NWU>        // waves (= row tiles) per block: the staged panel rows serve NWU tiles
+__global__ __launch_bounds__(64 * NWU) void panel_update_kernel(MstepArgs a, int L, int jb, int ntile,
+                                                                int gpt, int skip) {
     // skip: DIAGNOSTIC (timing only, results invalid): 1 no update
     __shared__ __attribute__((aligned(16))) cd Bp[PW * (KBU + 1)];
     const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
@@ -696,7 +697,7 @@ __global__ __launch_bounds__(256) void panel_update_kernel(MstepArgs a, int L, i
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
-    const int tau = grp * 4 + wave;
+    const int tau = grp * NWU + wave;
     const bool active = tau < ntile;                         // wave-uniform
     const int w2 = (L - jb) < PW ? (L - jb) : PW;
     cd* R = a.R + (size_t)b * L * L;
@@ -734,8 +735,8 @@ __global__ __launch_bounds__(256) void panel_update_kernel(MstepArgs a, int L, i
         // panel top rows by LDS-DMA: one wave-instruction per row (64 lanes = the row's KBU
         // slots, never crossing into the pad); lanes past kbs / rows past w2 read row jb
 #pragma unroll
-        for (int c8 = 0; c8 < PW / 4; ++c8) {
-            const int c = wave * (PW / 4) + c8;
+        for (int c8 = 0; c8 < PW / NWU; ++c8) {
+            const int c = wave * (PW / NWU) + c8;
             const cd* src = R + (size_t)jb * L + kb0;
             if (c < w2 && lane < kbs) src = R + (size_t)(jb + c) * L + kb0 + lane;
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -883,6 +884,13 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
     if (tid == 0) flag = 0;
     __syncthreads();
     cd xv[4];
+    // waves 1-3: their first row tile (A part) and y rows are in flight while wave 0 factors
+    cd cur[4], ycur[2];
+    if (wave != 0) {
+        const int tau = 1 + wave;
+        load_tile16(R, L, jb + tau * NB, jb, wA, lane, trsm && tau < ntile, cur);
+        load_yrows(y, L, NR, jb + tau * NB, li, lk, trsm && tau < ntile, ycur);
+    }
     if (wave == 0) {
         cd t1[4], y1[2];
         load_tile16(R, L, jbB, jb, wA, lane, ntile > 1, t1);        // row tile 1, A part
@@ -944,10 +952,7 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
         }
     } else if (trsm) {
         // row tiles tau >= 2: TRSM against D_A, in-panel update of their B part
-        cd cur[4], ycur[2];
         int tau = 1 + wave;
-        load_tile16(R, L, jb + tau * NB, jb, wA, lane, tau < ntile, cur);
-        load_yrows(y, L, NR, jb + tau * NB, li, lk, tau < ntile, ycur);
         for (; tau < ntile; tau += 3) {
             const int row0 = jb + tau * NB;
 #pragma unroll
@@ -991,7 +996,6 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
     __syncthreads();
     if (wB > 0 && trsm) {
         // row tiles tau >= 2: TRSM of the updated B part against D_B
-        cd cur[4], ycur[2];
         int tau = 2 + wave;
         load_tile16(R, L, jb + tau * NB, jbB, wB, lane, tau < ntile, cur);
         load_yrows(y, L, NR, jb + tau * NB, li, lk, tau < ntile, ycur);
@@ -1111,14 +1115,25 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
     hipError_t e = launch_diag_tol(pb, a, s);
     if (e != hipSuccess) return e;
     const int npan = (pb.L + PW - 1) / PW;
+    const char* uw = getenv("SBCE_UPD_WAVES");
+    const int upd_waves = (uw && uw[0] == '8') ? 8 : 4;
     for (int j = 0; j < npan; ++j) {
         const int jb = j * PW;
         const int rem = (pb.L - jb + NB - 1) / NB;               // 16-row tiles from jb
         if (j > 0) {
-            const int gpt = (rem + 3) / 4;
-            const long nblk = 8L * ((pb.B + 7) / 8) * gpt;
-            hipLaunchKernelGGL(panel_update_kernel, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L,
-                               jb, rem, gpt, skip);
+            // four-tile blocks; SBCE_UPD_WAVES=8: eight-tile blocks (A/B runs: 4 % slower at
+            // cfg1 -- the panel rows' re-reads by the blocks of a trial are L2 hits)
+            if (upd_waves == 4) {
+                const int gpt = (rem + 3) / 4;
+                const long nblk = 8L * ((pb.B + 7) / 8) * gpt;
+                hipLaunchKernelGGL(panel_update_kernel<4>, dim3((unsigned)nblk), dim3(256), 0, s, a,
+                                   pb.L, jb, rem, gpt, skip);
+            } else {
+                const int gpt = (rem + 7) / 8;
+                const long nblk = 8L * ((pb.B + 7) / 8) * gpt;
+                hipLaunchKernelGGL(panel_update_kernel<8>, dim3((unsigned)nblk), dim3(512), 0, s, a,
+                                   pb.L, jb, rem, gpt, skip);
+            }
         }
         hipLaunchKernelGGL(panel_factor_kernel, dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR, jb, rem,
                            skip);
