@@ -1110,6 +1110,94 @@ __global__ __launch_bounds__(256) void backsub2_kernel(MstepArgs a, int L, int N
     for (int e = tid; e < L * NR; e += 256) th[e] = cconj(y[e]);
 }
 
+// Back substitution for L <= 272, NR <= 4 with ONE barrier per 16-column block step (the
+// two-ahead kernel above pays three).  Thread tid owns row k = tid < 256 of y in registers
+// (rows of the last block past 255 are only ever read, from the input).  Every
+// wave solves the block x = D^{-H} z itself (lane c*NR + r: output (c, r)) into a
+// wave-private LDS copy, so the update of the wave's own rows needs no workgroup barrier; the
+// owners of the next block's rows then publish them, every thread publishes its entry of the
+// next diagonal block (L_cc, conj(Di[c2][c]) above the diagonal; loaded two steps ahead with
+// its update column), both double-buffered in LDS, and the workgroup synchronises once.
+struct Bs3Buf {
+    cd lv[NB];         // L[k0 + cc][tid], this thread's update column
+    cd dd;             // entry (tid >> 4, tid & 15) of the diagonal block
+};
+__device__ __forceinline__ void bs3_load(const cd* R, int L, int kb, int tid, Bs3Buf& bf) {
+    const int k0 = kb * NB, w = (L - k0) < NB ? (L - k0) : NB;
+    const int c = tid >> 4, c2 = tid & 15;
+    bf.dd = (kb >= 0 && c < w && c2 >= c && c2 < w) ? R[(size_t)(k0 + c) * L + k0 + c2] : czero();
+#pragma unroll
+    for (int cc = 0; cc < NB; ++cc)
+        bf.lv[cc] = (kb >= 0 && tid < k0 && cc < w) ? R[(size_t)(k0 + cc) * L + tid] : czero();
+}
+template <int NR>
+__device__ __forceinline__ void bs3_step(int kb, int L, int tid, int lane, int wave, int c, int r,
+                                         const Bs3Buf& bf, const cd& dnext, cd (&yr)[NR],
+                                         cd (*zb)[NB * NR], cd (*db)[NB * NB], cd (*xw)[NB * NR],
+                                         cd* th) {
+    const int k0 = kb * NB, w = (L - k0) < NB ? (L - k0) : NB;
+    const cd* z = zb[kb & 1];
+    const cd* d = db[kb & 1] + c * NB;         // row c: L_cc, then conj(Di[c2][c]) for c2 > c
+    cd x = czero();
+    if (c < w) {
+        const double lcc = d[c].x;
+        x = lcc > 0.0 ? cscale(z[c * NR + r], 1.0 / lcc) : czero();
+        for (int c2 = c + 1; c2 < w; ++c2) x = cfma(x, d[c2], z[c2 * NR + r]);
+    }
+    if (lane < NB * NR) xw[wave][lane] = x;
+    if (wave == 0 && c < w) th[(size_t)(k0 + c) * NR + r] = cconj(x);
+    wave_sync();
+    if (tid < k0) {
+#pragma unroll
+        for (int cc = 0; cc < NB; ++cc)
+#pragma unroll
+            for (int q = 0; q < NR; ++q) yr[q] = csub(yr[q], cmulc(xw[wave][cc * NR + q], bf.lv[cc]));
+    }
+    if (kb > 0) {                              // publish the next block's rows and diagonal block
+        if (tid >= k0 - NB && tid < k0) {
+#pragma unroll
+            for (int q = 0; q < NR; ++q) zb[(kb - 1) & 1][(tid - (k0 - NB)) * NR + q] = yr[q];
+        }
+        db[(kb - 1) & 1][tid] = dnext;
+    }
+    __syncthreads();
+}
+template <int NR>
+__global__ __launch_bounds__(256) void backsub3_kernel(MstepArgs a, int L) {
+    __shared__ cd zb[2][NB * NR];              // the current / next block's z rows
+    __shared__ cd db[2][NB * NB];              // the current / next diagonal block
+    __shared__ cd xw[4][NB * NR];              // per-wave block solution
+    const int b = blockIdx.x;
+    if (a.done && a.done[b]) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const cd* R = a.R + (size_t)b * L * L;
+    const cd* yg = a.rhs + (size_t)b * L * NR;
+    cd* th = a.theta + (size_t)b * L * NR;
+    const int nblk = (L + NB - 1) / NB;
+    const int c = lane / NR, r = lane - (lane / NR) * NR;     // block-solve output of this lane
+    cd yr[NR];                                                 // row k = tid of y
+#pragma unroll
+    for (int q = 0; q < NR; ++q) yr[q] = tid < L ? yg[(size_t)tid * NR + q] : czero();
+    Bs3Buf bA, bB;
+    bs3_load(R, L, nblk - 1, tid, bA);
+    bs3_load(R, L, nblk - 2, tid, bB);
+    {
+        // the last block's rows (k0 may be 256: no owner thread) straight from the input
+        const int k0 = (nblk - 1) * NB, w = L - k0;
+        if (tid < w * NR) zb[(nblk - 1) & 1][tid] = yg[(size_t)k0 * NR + tid];
+        db[(nblk - 1) & 1][tid] = bA.dd;
+    }
+    __syncthreads();
+    for (int kb = nblk - 1; kb >= 0; kb -= 2) {
+        bs3_step<NR>(kb, L, tid, lane, wave, c, r, bA, bB.dd, yr, zb, db, xw, th);
+        bs3_load(R, L, kb - 2, tid, bA);
+        if (kb - 1 < 0) break;
+        bs3_step<NR>(kb - 1, L, tid, lane, wave, c, r, bB, bA.dd, yr, zb, db, xw, th);
+        bs3_load(R, L, kb - 3, tid, bB);
+    }
+}
+
 hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_t s) {
     const int skip = g_chol_skip;                   // diagnostic only (see kernels)
     hipError_t e = launch_diag_tol(pb, a, s);
@@ -1139,8 +1227,18 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
                            skip);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    // SBCE_BACKSUB=1 keeps the one-step-prefetch kernel (A/B runs)
+    // SBCE_BACKSUB=1 keeps the one-step-prefetch kernel, =2 the two-ahead three-barrier
+    // kernel (A/B runs); default: one barrier per block step
     const char* bsv = getenv("SBCE_BACKSUB");
+    if (pb.L <= 272 && pb.NR <= 4 && !(bsv && (bsv[0] == '1' || bsv[0] == '2')) && !(skip & 16)) {
+        switch (pb.NR) {
+            case 1: hipLaunchKernelGGL(backsub3_kernel<1>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+            case 2: hipLaunchKernelGGL(backsub3_kernel<2>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+            case 3: hipLaunchKernelGGL(backsub3_kernel<3>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+            default: hipLaunchKernelGGL(backsub3_kernel<4>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+        }
+        return hipGetLastError();
+    }
     if (pb.L <= 272 && pb.NR <= 4 && !(bsv && bsv[0] == '1') && !(skip & 16)) {
         hipLaunchKernelGGL(backsub2_kernel, dim3(pb.B), dim3(256),
                            ((size_t)pb.L * pb.NR + NB * NB) * sizeof(cd), s, a, pb.L, pb.NR);

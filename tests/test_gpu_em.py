@@ -406,10 +406,10 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape, monkeypatch):
     out = {}
     # default = batched panel launches; "fused" = one workgroup per trial; "valu"
     # "batched_bs1": batched, with the one-step-prefetch back substitution instead of the
-    # two-ahead kernel (default for L <= 272, n_rx <= 4)
-    for impl in ("batched", "fused", "valu", "batched_bs1"):
+    # one-barrier kernel (default for L <= 272, n_rx <= 4), two-ahead three-barrier kernel
+    for impl in ("batched", "fused", "valu", "batched_bs1", "batched_bs2"):
         monkeypatch.setenv("SBCE_CHOL_IMPL", impl.split("_")[0])
-        monkeypatch.setenv("SBCE_BACKSUB", "1" if impl.endswith("bs1") else "0")
+        monkeypatch.setenv("SBCE_BACKSUB", impl[-1] if "_bs" in impl else "0")
         out[impl] = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], m, S, 0.05)
     th_m, R, rhs, st = out["batched"]
     assert not st.any()
@@ -421,6 +421,7 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape, monkeypatch):
     assert rel(th_m, out["fused"][0]) < 1e-9
     assert rel(th_m, out["valu"][0]) < 1e-9
     assert rel(th_m, out["batched_bs1"][0]) < 1e-12
+    assert rel(th_m, out["batched_bs2"][0]) < 1e-12
 
 
 # ---------------------------------------------------------------- large-L M-step (L > 512)
