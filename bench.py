@@ -16,14 +16,13 @@ after the timed region, as in the reference's Monte-Carlo average
 (Proposed_method_NMSEvsTp.py:176).
 
 Also reported (one JSON line on rank 0):
-  roofline      the dominant phase (E-step or M-step, whichever is longer per
-                EM iteration; "kernels" lists the launches it consists of) timed live
-                with HIP events on the launch stream;
-                M-step: algorithmic flops per launch; E-step: the
-                FP64 MFMAs it issued (device counter; its exact bounds skip
-                provably negligible hypothesis tiles), with the full-enumeration
-                flops next to it; peak = FP64 rate of MI355X; traffic from the
-                committed rocprofv3 PMC summary when present.
+  roofline      the M-step (the dominant phase per EM iteration; "kernels" lists the
+                launches it consists of) timed live with HIP events on the launch
+                stream: algorithmic flops per launch / time, peak = FP64
+                rate of MI355X; traffic from the committed rocprofv3 PMC summary.
+                The E-step (a tree search + MFMA sweep of the listed remainder) is
+                reported next to it (estep_roofline: time, where the symbols were
+                resolved, hypotheses covered per second).
   cpu_baseline  the build's vectorised float64 NumPy port of the same
                 algorithm (oracle/em_reduced.py) on a bounded sample of the
                 same workload, on this host's cores (rank 0, N=1 only).
@@ -59,10 +58,11 @@ ESTEP = {"cfg1": ("soft", 0, "chol"), "plumbing": ("soft", 0, "chol"),
 
 
 # kernels of one E-step / M-step launch sequence (rocprofv3 names, tools/pmc_summary.py keys)
-ESTEP_KERNELS = ["estep_prep_kernel", "estep_mfma_kernel_occ3", "estep_mfma_kernel"]
+ESTEP_KERNELS = ["estep_tree_kernel", "estep_bfs_kernel", "estep_bounds_kernel", "estep_prep_kernel",
+                 "estep_mfma_kernel_occ3", "estep_mfma_kernel"]
 MSTEP_KERNELS = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_kernel", "rhs_lds_kernel",
                  "rhs_kernel", "diag_tol_kernel", "panel_update_kernel", "panel_factor_kernel",
-                 "backsub_kernel", "chol_mfma_kernel"]
+                 "backsub_kernel", "backsub2_kernel", "backsub3_kernel", "chol_mfma_kernel"]
 MSTEP_KERNELS_LARGE = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_wide_kernel",
                        "rhs_kernel", "diag_tol_kernel", "chol_mfma_kernel", "tile_inverse_kernel",
                        "tile_gemm_kernel", "backdiag_kernel", "backupd_kernel"]
@@ -238,17 +238,25 @@ def main():
     # FP64 MFMAs the exact E-step actually issued at this theta (its exact column-tile
     # bounds skip provably negligible tiles): one counted launch outside the timed loops
     mfma_issued = None
+    sphere = None
     lib = pkg._lib.load()
     if mode in ("soft", "hard") and hasattr(lib, "sbce_debug_estep_mfma"):
         import ctypes
         cnt = ctypes.c_ulonglong(0)
+        sph = (ctypes.c_ulonglong * 3)()
         os.environ["SBCE_ESTEP_COUNT"] = "1"
         lib.sbce_debug_estep_mfma(None, 1)
+        lib.sbce_debug_estep_sphere(None, 1)
         eng.estep()
         torch.cuda.synchronize()
         lib.sbce_debug_estep_mfma(ctypes.byref(cnt), 0)
+        lib.sbce_debug_estep_sphere(sph, 0)
         del os.environ["SBCE_ESTEP_COUNT"]
         mfma_issued = int(cnt.value)
+        nsym = float(B * T_d)
+        # where the symbols' posteriors were computed: single surviving path
+        # in the tree pass, breadth-first enumeration, or the MFMA tile sweep
+        sphere = {"single_path": sph[2] / nsym, "enumerated": sph[0] / nsym, "swept": sph[1] / nsym}
     e0.record(stream)
     for _ in range(args.kernel_reps):
         eng.mstep()
@@ -290,19 +298,20 @@ def main():
         # executed work: the MFMAs issued (16x16x4 f64 = 2048 flop each); the full
         # enumeration's flops are reported next to it ("enumeration_*")
         executed = mfma_issued * 2048 if mfma_issued is not None else flops
-        achieved_tf = executed / (estep_ms * 1e-3) / 1e12
-        estep_roof = {"bound": "mfma", "pipe": "FP64 MFMA v_mfma_f64_16x16x4f64 (+ FP64 VALU)",
+        # the E-step is a search (tree pass, enumeration, sweep of the listed remainder): its
+        # time is set by per-symbol latency, not a pipe's peak; reported for reference, the
+        # M-step carries the roofline object
+        estep_roof = {"bound": "latency", "pipe": "FP64 VALU tree search + FP64 MFMA sweep",
                       "phase": "E-step", "kernels": ESTEP_KERNELS, "ms": estep_ms,
-                      "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic_of(ESTEP_KERNELS, ESTEP_KERNELS),
-                      "flops_per_launch": executed,
+                      "sphere_pass": sphere,
+                      "traffic": traffic_of(ESTEP_KERNELS, ESTEP_KERNELS),
+                      "sweep_mfma_flops_per_launch": executed,
                       "enumeration_flops_per_launch": flops,
-                      "enumeration_fraction_issued": executed / flops,
+                      "hypotheses_per_s": B * T_d * float(M) ** n_tx / (estep_ms * 1e-3),
                       "algorithmic_bytes": algo_bytes,
                       "hbm_GBps_algorithmic": algo_bytes / (estep_ms * 1e-3) / 1e9,
                       "hbm_frac_algorithmic": algo_bytes / (estep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
-        # the dominant phase (longest per EM iteration) carries the roofline object
-        roofline = estep_roof if estep_ms >= mstep_ms else mstep_roof
+        roofline = mstep_roof
     else:
         estep_roof = None
         # list-detector workloads: the M-step (MFMA tile build + blocked Cholesky) dominates

@@ -23,6 +23,8 @@
 //   subtracts L_ik y_k from its rows; back L^H x = y by column blocks from the last:
 //   backdiag_kernel (diagonal tile, 16-blocks through the inverses kept in R's strict upper
 //   16 x 16 blocks) then backupd_kernel (all earlier row blocks in parallel).
+#include <stdlib.h>
+
 #include "sbce_internal.h"
 
 namespace sbce {
@@ -633,6 +635,11 @@ hipError_t launch_rbuild_herm(const Problem& pb, const MstepArgs& a, hipStream_t
     // staged phases per block <= min(P, pairs per block + 1) (two p-major index segments)
     if (pb.NT == 4) {
         const int smax = pb.P < 257 ? pb.P : 257;
+        // 16-symbol chunks (19 KB of LDS per block: more resident blocks per CU); measured
+        // at cfg1 against 8 / 32 / 64 and 2 / 6 / 8 tiles per wave: 16 x 4 and 16 x 6 lead by
+        // ~2 % of the M-step.  SBCE_RB_TC=32: the previous 32-symbol chunks (A/B runs)
+        const char* tc = getenv("SBCE_RB_TC");
+        if (smax <= 68 && !(tc && tc[0] == '3')) return launch_herm<4, 4, 16, 68>(pb, a, smax, s);
         if (smax <= 68) return launch_herm<4, 4, 32, 68>(pb, a, smax, s);
         return smax <= 130 ? launch_herm<4, 4, 32, 0>(pb, a, smax, s)
                            : launch_herm<4, 4, 8, 0>(pb, a, smax, s);
