@@ -1846,9 +1846,22 @@ __global__ __launch_bounds__(64 * kBfsWaves) void estep_bfs_kernel(EstepArgs a, 
     const int pmax = c.budget < kBfsPmax ? c.budget : kBfsPmax;
     const u64 lt = (1ull << lane) - 1ull;
     unsigned listed_mask = 0, resolved_n = 0;
+    // tree records by LDS-DMA, the next symbol's in flight while the current one is enumerated
+    // (lanes 0-15 carry the record's 256 bytes; the others re-read its first 16 bytes)
+    __shared__ __attribute__((aligned(16))) double s_rec[kBfsWaves][2][128];
+    auto issue = [&](long gi, int buf) {
+        const double* src = a.tree + (size_t)elist[gi] * kTrec + (lane < kTrec / 2 ? 2 * lane : 0);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)s_rec[wave][buf],
+                                         16, 0, 0);
+    };
+    issue(g0, 0);
     for (long gi = g0; gi < g1; ++gi) {
         const long gsym = elist[gi];
-        const double* rec = a.tree + (size_t)gsym * kTrec;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this symbol's record landed
+        wave_sync();
+        const double* rec = s_rec[wave][(gi - g0) & 1];
+        if (gi + 1 < g1) issue(gi + 1, (gi + 1 - g0) & 1);
         const int packed = (int)rec[3];
         bool listed = !((packed >> 16) & 1);
         const double R0 = rec[1];
