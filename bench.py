@@ -39,6 +39,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector (= FP64 matrix); half the guide's 157.3 TF FP32
+# FP64 MFMA rate measured on the box with operands that change every iteration (DESIGN.md §8
+# item 6, tools/ubench/): reported beside the datasheet peak, never used as "peak"
+FP64_MFMA_MEASURED_TFLOPS = 46.0
 HBM_PEAK_GBS = 8000.0
 
 CONFIGS = {
@@ -291,7 +294,10 @@ def main():
                   "unit": "TFLOP/s", "frac": mflops / (mstep_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
                   "traffic": traffic_of(m_kern, MSTEP_ANCHORS), "algorithmic_bytes": mbytes,
                   "hbm_frac_algorithmic": mbytes / (mstep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                  "flops_per_launch": mflops}
+                  "flops_per_launch": mflops,
+                  "measured_pipe_tflops": FP64_MFMA_MEASURED_TFLOPS,
+                  "frac_of_measured_pipe": mflops / (mstep_ms * 1e-3) / 1e12
+                  / FP64_MFMA_MEASURED_TFLOPS}
     if mode in ("soft", "hard"):
         flops = estep_flops_per_trial_iter(n_tx, n_rx, T_d, M) * B
         algo_bytes = estep_bytes_per_trial_iter(n_tx, n_rx, P, T_d) * B
