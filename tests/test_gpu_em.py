@@ -461,7 +461,8 @@ def test_large_l_pilot_not_kronecker_is_flagged(sbce):
     assert st[0] & sbce._lib.SBCE_STATUS_PILOT
 
 
-@pytest.mark.parametrize("shape", [(4, 2, 20, 8, 60), (8, 3, 9, 6, 40)])
+@pytest.mark.parametrize("shape", [(4, 2, 20, 8, 60), (8, 3, 9, 6, 40),
+                                   (4, 8, 20, 8, 60)])   # B^H not fused into the build (n_rx 8)
 def test_mstep_pilot_not_kronecker_falls_back_exactly(sbce, shape):
     """n_tx in {4, 8} builds R by MFMA from Kronecker-factored pilots; a trial whose u_p
     is not psi (x) x is flagged and rebuilt by the VALU path, so R stays exact."""
