@@ -107,6 +107,29 @@ __device__ __forceinline__ void forward_y_block(const cd* Di, cd* yblk, int w, i
     if (e1 < w * NR) yblk[e1] = t1;
 }
 
+// The same with the block staged in LDS (yb: NB*NR entries, raw on entry): the result goes
+// to yb (zero past w rows) and to y in global memory, so the next reader of the block
+// waits on LDS, not on a global store-then-load round trip.  NR <= 8.
+__device__ __forceinline__ void forward_y_lds(const cd* Di, cd* yb, cd* yglob, int w, int NR,
+                                              int lane) {
+    const int e0 = lane, e1 = lane + 64;
+    cd t0 = czero(), t1 = czero();
+    if (e0 < w * NR) {
+        const int c = e0 / NR, r = e0 - c * NR;
+        for (int c2 = 0; c2 <= c; ++c2) t0 = cfma(t0, Di[c * NB + c2], yb[c2 * NR + r]);
+    }
+    if (e1 < w * NR) {
+        const int c = e1 / NR, r = e1 - c * NR;
+        for (int c2 = 0; c2 <= c; ++c2) t1 = cfma(t1, Di[c * NB + c2], yb[c2 * NR + r]);
+    }
+    wave_sync();
+    if (e0 < NB * NR) yb[e0] = t0;
+    if (e1 < NB * NR) yb[e1] = t1;
+    if (e0 < w * NR) yglob[e0] = t0;
+    if (e1 < w * NR) yglob[e1] = t1;
+    wave_sync();
+}
+
 // Blocked back substitution L^H x = y (whole workgroup), then theta = conj(x).
 __device__ __forceinline__ void back_substitute(const cd* R, cd* y, int L, int NR, int tid, int nth, int lane,
                                 int wave, int kb_stop) {
@@ -797,9 +820,14 @@ __device__ __forceinline__ void load_tile16(const cd* R, int L, int row0, int c0
 // TRSM of one 16-row tile (values in X, LDS) against the factored diagonal block of the
 // sub-panel at column c0 (inverse Di): L = C D^{-H}, written to R; y rows updated with the
 // sub-panel's y block yb.  Returns X[li][lk + 4q] in xv (the A-operand layout of k-step q).
+// The y update Y_tile -= X Y_blk is two real MFMA GEMMs over the 16 columns of X with the
+// right-hand sides embedded as 2*NR real columns (re | im): A = Re X, Im X (= xv as it
+// comes out of the TRSM), B1 = [Re Y | Im Y], B2 = [-Im Y | Re Y]; lane (li, lk) ends with
+// component (li < NR: re, else im) of right-hand side li mod NR for rows lk + 4q, and
+// yd[q] holds the same component of those rows before the update (load_ycomp).  NR <= 8.
 __device__ __forceinline__ void trsm_tile16(cd* R, cd* y, const cd* Di, const cd* X, const cd* yb,
                                             int L, int NR, int row0, int c0, int w, int li,
-                                            int lk, cd* xv, const cd* yv) {
+                                            int lk, cd* xv, const double* yd, cd* ylds = nullptr) {
     d4v xre = {0.0, 0.0, 0.0, 0.0}, xim = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int s2 = 0; s2 < NB / 4; ++s2) {
@@ -819,36 +847,39 @@ __device__ __forceinline__ void trsm_tile16(cd* R, cd* y, const cd* Di, const cd
         xv[q] = cmk(xre[q], xim[q]);
         if (live && j < w) crow[j] = xv[q];
     }
-    // y[row0+li] -= sum_j X[li][j] y_blk[j]: 4 columns per lane, reduced over lk; lane
-    // (li, lk) then owns right-hand sides r = lk + 4m of row li, prefetched in yv[m]
-    for (int r0 = 0; r0 < NR; r0 += 4) {                     // 4 right-hand sides per pass
-        cd p[4];
+    const bool isre = li < NR, on = li < 2 * NR;
+    const int r = isre ? li : li - NR;
+    d4v u = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int r = r0 + rr;
-            p[rr] = czero();
-            if (r < NR) {
+    for (int s2 = 0; s2 < NB / 4; ++s2) {
+        const cd v = on ? yb[(4 * s2 + lk) * NR + r] : czero();     // Y_blk[4s+lk][r]
+        const double b1 = isre ? v.x : v.y, b2 = isre ? -v.y : v.x;
+        u = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[s2].x, b1, u, 0, 0, 0);
+        u = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[s2].y, b2, u, 0, 0, 0);
+    }
+    if (on) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) p[rr] = cfma(p[rr], xv[q], yb[(lk + 4 * q) * NR + r]);
-                p[rr].x += shfl_xor_d(p[rr].x, 16); p[rr].y += shfl_xor_d(p[rr].y, 16);
-                p[rr].x += shfl_xor_d(p[rr].x, 32); p[rr].y += shfl_xor_d(p[rr].y, 32);
-            }
-        }
-        const int r = r0 + lk;
-        if (live && r < NR) {
-            const cd pm = csel(lk == 0, p[0], csel(lk == 1, p[1], csel(lk == 2, p[2], p[3])));
-            y[(size_t)(row0 + li) * NR + r] = csub(yv[r0 >> 2], pm);
+        for (int q = 0; q < 4; ++q) {
+            const int rr = lk + 4 * q;
+            const double yn = yd[q] - u[q];
+            if (row0 + rr < L) ((double*)(y + (size_t)(row0 + rr) * NR + r))[isre ? 0 : 1] = yn;
+            // the updated rows also to LDS (zero past L) when the caller solves them next
+            if (ylds) ((double*)(ylds + rr * NR + r))[isre ? 0 : 1] = row0 + rr < L ? yn : 0.0;
         }
     }
 }
 
-// the y rows of a 16-row tile for trsm_tile16: lane (li, lk) holds r = lk + 4m of row li
-__device__ __forceinline__ void load_yrows(const cd* y, int L, int NR, int row0, int li, int lk,
-                                           bool on, cd* yv) {
+// the y rows of a 16-row tile for trsm_tile16: lane (li, lk) holds component li < NR (re) /
+// NR <= li < 2 NR (im) of right-hand side li mod NR, rows lk + 4q
+__device__ __forceinline__ void load_ycomp(const cd* y, int L, int NR, int row0, int li, int lk,
+                                           bool on, double* yd) {
+    const bool isre = li < NR;
+    const int r = isre ? li : li - NR;
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-        const int r = lk + 4 * m;
-        yv[m] = (on && row0 + li < L && r < NR) ? y[(size_t)(row0 + li) * NR + r] : czero();
+    for (int q = 0; q < 4; ++q) {
+        const int rr = row0 + lk + 4 * q;
+        yd[q] = (on && li < 2 * NR && rr < L) ? ((const double*)(y + (size_t)rr * NR + r))[isre ? 0 : 1]
+                                              : 0.0;
     }
 }
 
@@ -885,16 +916,31 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
     __syncthreads();
     cd xv[4];
     // waves 1-3: their first row tile (A part) and y rows are in flight while wave 0 factors
-    cd cur[4], ycur[2];
+    cd cur[4];
+    double ycur[4];
     if (wave != 0) {
         const int tau = 1 + wave;
         load_tile16(R, L, jb + tau * NB, jb, wA, lane, trsm && tau < ntile, cur);
-        load_yrows(y, L, NR, jb + tau * NB, li, lk, trsm && tau < ntile, ycur);
+        load_ycomp(y, L, NR, jb + tau * NB, li, lk, trsm && tau < ntile, ycur);
     }
+    // wave 0's serial chain reads every global operand up front: B's diagonal tile (written
+    // by no one in this launch) and y block A go to registers / LDS before factor A starts
+    d4v cbre = {0.0, 0.0, 0.0, 0.0}, cbim = {0.0, 0.0, 0.0, 0.0};
     if (wave == 0) {
-        cd t1[4], y1[2];
+        cd t1[4];
+        double y1[4];
         load_tile16(R, L, jbB, jb, wA, lane, ntile > 1, t1);        // row tile 1, A part
-        load_yrows(y, L, NR, jbB, li, lk, ntile > 1, y1);
+        load_ycomp(y, L, NR, jbB, li, lk, ntile > 1, y1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int rr = lk + 4 * q;
+            if (rr < wB && li < wB) {
+                const cd x = R[(size_t)(jbB + rr) * L + jbB + li];
+                cbre[q] = x.x;
+                cbim[q] = x.y;
+            }
+        }
+        for (int e = lane; e < NB * NR; e += 64) ybA[e] = (e < wA * NR) ? y[jb * NR + e] : czero();
         for (int e = lane; e < NB * NB; e += 64) {
             const int rr = e >> 4, c = e & 15;
             X[e] = (rr < wA && c <= rr) ? R[(size_t)(jb + rr) * L + jb + c] : czero();
@@ -903,16 +949,15 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
         if (!(skip & 2)) {
             factor_diag_lds(X, wA, lane, tol, a.solve_mode, DiA, dinv, &flag,
                             R + (size_t)jb * L + jb, L);
-            forward_y_block(DiA, y + jb * NR, wA, NR, lane);
+            forward_y_lds(DiA, ybA, y + jb * NR, wA, NR, lane);
         }
-        wave_sync();
-        for (int e = lane; e < NB * NR; e += 64) ybA[e] = (e < wA * NR) ? y[jb * NR + e] : czero();
         wave_sync();
         if (ntile > 1 && trsm) {
 #pragma unroll
             for (int h = 0; h < 4; ++h) X[lane + 64 * h] = t1[h];
             wave_sync();
-            trsm_tile16(R, y, DiA, X, ybA, L, NR, jbB, jb, wA, li, lk, xv, y1);
+            // row tile 1 = sub-panel B's rows: its updated y rows are staged raw in ybB
+            trsm_tile16(R, y, DiA, X, ybA, L, NR, jbB, jb, wA, li, lk, xv, y1, ybB);
 #pragma unroll
             for (int q = 0; q < 4; ++q) XA1[li * NB + lk + 4 * q] = xv[q];
         }
@@ -921,16 +966,7 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
     if (wave == 0) {
         if (wB > 0) {
             // B's diagonal tile: C_B1 -= X_A1 X_A1^H, then factor
-            d4v cre = {0.0, 0.0, 0.0, 0.0}, cim = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int rr = lk + 4 * q;
-                if (rr < wB && li < wB) {
-                    const cd x = R[(size_t)(jbB + rr) * L + jbB + li];
-                    cre[q] = x.x;
-                    cim[q] = x.y;
-                }
-            }
+            d4v cre = cbre, cim = cbim;
 #pragma unroll
             for (int s2 = 0; s2 < 4; ++s2) {
                 const cd v = xv[s2], t = XA1[li * NB + 4 * s2 + lk];
@@ -945,10 +981,8 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
             if (!(skip & 2)) {
                 factor_diag_lds(X, wB, lane, tol, a.solve_mode, DiB, dinv, &flag,
                                 R + (size_t)jbB * L + jbB, L);
-                forward_y_block(DiB, y + jbB * NR, wB, NR, lane);
+                forward_y_lds(DiB, ybB, y + jbB * NR, wB, NR, lane);
             }
-            wave_sync();
-            for (int e = lane; e < NB * NR; e += 64) ybB[e] = (e < wB * NR) ? y[jbB * NR + e] : czero();
         }
     } else if (trsm) {
         // row tiles tau >= 2: TRSM against D_A, in-panel update of their B part
@@ -969,11 +1003,10 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
                     }
                 }
             }
-            const cd yv0 = ycur[0], yv1 = ycur[1];
+            const double yv[4] = {ycur[0], ycur[1], ycur[2], ycur[3]};
             load_tile16(R, L, row0 + 3 * NB, jb, wA, lane, tau + 3 < ntile, cur);   // next
-            load_yrows(y, L, NR, row0 + 3 * NB, li, lk, tau + 3 < ntile, ycur);
+            load_ycomp(y, L, NR, row0 + 3 * NB, li, lk, tau + 3 < ntile, ycur);
             wave_sync();
-            const cd yv[2] = {yv0, yv1};
             trsm_tile16(R, y, DiA, X, ybA, L, NR, row0, jb, wA, li, lk, xv, yv);
             if (wB > 0) {
 #pragma unroll
@@ -998,14 +1031,14 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
         // row tiles tau >= 2: TRSM of the updated B part against D_B
         int tau = 2 + wave;
         load_tile16(R, L, jb + tau * NB, jbB, wB, lane, tau < ntile, cur);
-        load_yrows(y, L, NR, jb + tau * NB, li, lk, tau < ntile, ycur);
+        load_ycomp(y, L, NR, jb + tau * NB, li, lk, tau < ntile, ycur);
         for (; tau < ntile; tau += 4) {
             const int row0 = jb + tau * NB;
 #pragma unroll
             for (int h = 0; h < 4; ++h) X[lane + 64 * h] = cur[h];
-            const cd yv[2] = {ycur[0], ycur[1]};
+            const double yv[4] = {ycur[0], ycur[1], ycur[2], ycur[3]};
             load_tile16(R, L, row0 + 4 * NB, jbB, wB, lane, tau + 4 < ntile, cur);
-            load_yrows(y, L, NR, row0 + 4 * NB, li, lk, tau + 4 < ntile, ycur);
+            load_ycomp(y, L, NR, row0 + 4 * NB, li, lk, tau + 4 < ntile, ycur);
             wave_sync();
             trsm_tile16(R, y, DiB, X, ybB, L, NR, row0, jbB, wB, li, lk, xv, yv);
             wave_sync();
