@@ -924,20 +924,21 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
         load_ycomp(y, L, NR, jb + tau * NB, li, lk, trsm && tau < ntile, ycur);
     }
     // wave 0's serial chain reads every global operand up front: B's diagonal tile (written
-    // by no one in this launch) and y block A go to registers / LDS before factor A starts
-    d4v cbre = {0.0, 0.0, 0.0, 0.0}, cbim = {0.0, 0.0, 0.0, 0.0};
+    // by no one in this launch) arrives by LDS-DMA in DiB (unused until factor B; no
+    // registers held across factor A), y block A in ybA, before factor A starts
     if (wave == 0) {
         cd t1[4];
         double y1[4];
         load_tile16(R, L, jbB, jb, wA, lane, ntile > 1, t1);        // row tile 1, A part
         load_ycomp(y, L, NR, jbB, li, lk, ntile > 1, y1);
+        if (wB > 0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int rr = lk + 4 * q;
-            if (rr < wB && li < wB) {
-                const cd x = R[(size_t)(jbB + rr) * L + jbB + li];
-                cbre[q] = x.x;
-                cbim[q] = x.y;
+            for (int h = 0; h < 4; ++h) {          // DiB[e] = R[jbB + e/16][jbB + e%16]
+                const int e = lane + 64 * h, rr = e >> 4, c = e & 15;
+                const cd* src = R + (size_t)(jbB + (rr < wB ? rr : 0)) * L + jbB + (c < wB ? c : 0);
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                 (__attribute__((address_space(3))) void*)(DiB + 64 * h),
+                                                 16, 0, 0);
             }
         }
         for (int e = lane; e < NB * NR; e += 64) ybA[e] = (e < wA * NR) ? y[jb * NR + e] : czero();
@@ -961,12 +962,23 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
 #pragma unroll
             for (int q = 0; q < 4; ++q) XA1[li * NB + lk + 4 * q] = xv[q];
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // B's diagonal tile is in DiB
     }
     __syncthreads();
     if (wave == 0) {
         if (wB > 0) {
             // B's diagonal tile: C_B1 -= X_A1 X_A1^H, then factor
-            d4v cre = cbre, cim = cbim;
+            d4v cre = {0.0, 0.0, 0.0, 0.0}, cim = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rr = lk + 4 * q;
+                if (rr < wB && li < wB) {
+                    const cd x = DiB[rr * NB + li];
+                    cre[q] = x.x;
+                    cim[q] = x.y;
+                }
+            }
+            wave_sync();                                         // DiB is overwritten next
 #pragma unroll
             for (int s2 = 0; s2 < 4; ++s2) {
                 const cd v = xv[s2], t = XA1[li * NB + 4 * s2 + lk];
