@@ -1196,7 +1196,10 @@ __device__ __forceinline__ void bs3_step(int kb, int L, int tid, int lane, int w
 #pragma unroll
         for (int cc = 0; cc < NB; ++cc)
 #pragma unroll
-            for (int q = 0; q < NR; ++q) yr[q] = csub(yr[q], cmulc(xw[wave][cc * NR + q], bf.lv[cc]));
+            for (int q = 0; q < NR; ++q) {           // y -= x conj(l): four FMAs
+                const cd xv = xw[wave][cc * NR + q];
+                yr[q] = cfmac(yr[q], cmk(-xv.x, -xv.y), bf.lv[cc]);
+            }
     }
     if (kb > 0) {                              // publish the next block's rows and diagonal block
         if (tid >= k0 - NB && tid < k0) {
@@ -1243,6 +1246,78 @@ __global__ __launch_bounds__(256) void backsub3_kernel(MstepArgs a, int L) {
     }
 }
 
+// The same one-barrier block step with the factor entries loaded ONE step ahead into a single
+// buffer (issued as soon as the update has consumed the current one, the next diagonal-block
+// entry at the start of the step): ~100 VGPRs instead of backsub3's 192, so four trials'
+// workgroups are resident per CU (one round over ~1000 trials instead of two).
+template <int NR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+void backsub4_kernel(MstepArgs a, int L) {
+    __shared__ cd zb[2][NB * NR];              // the current / next block's z rows
+    __shared__ cd db[2][NB * NB];              // the current / next diagonal block
+    __shared__ cd xw[4][NB * NR];              // per-wave block solution
+    const int b = blockIdx.x;
+    if (a.done && a.done[b]) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const cd* R = a.R + (size_t)b * L * L;
+    const cd* yg = a.rhs + (size_t)b * L * NR;
+    cd* th = a.theta + (size_t)b * L * NR;
+    const int nblk = (L + NB - 1) / NB;
+    const int c = lane / NR, r = lane - (lane / NR) * NR;     // block-solve output of this lane
+    const int dc = tid >> 4, dc2 = tid & 15;                  // this thread's diagonal-block entry
+    cd yr[NR];                                                 // row k = tid of y
+#pragma unroll
+    for (int q = 0; q < NR; ++q) yr[q] = tid < L ? yg[(size_t)tid * NR + q] : czero();
+    Bs3Buf bf;
+    bs3_load(R, L, nblk - 1, tid, bf);
+    {
+        // the last block's rows (k0 may be 256: no owner thread) straight from the input
+        const int k0 = (nblk - 1) * NB, w = L - k0;
+        if (tid < w * NR) zb[(nblk - 1) & 1][tid] = yg[(size_t)k0 * NR + tid];
+        db[(nblk - 1) & 1][tid] = bf.dd;
+    }
+    __syncthreads();
+    for (int kb = nblk - 1; kb >= 0; --kb) {
+        const int k0 = kb * NB, w = (L - k0) < NB ? (L - k0) : NB;
+        cd dnext = czero();                    // entry of the next diagonal block (k0 - 16 ..)
+        if (kb > 0 && dc2 >= dc) dnext = R[(size_t)(k0 - NB + dc) * L + k0 - NB + dc2];
+        const cd* z = zb[kb & 1];
+        const cd* d = db[kb & 1] + c * NB;     // row c: L_cc, then conj(Di[c2][c]) for c2 > c
+        cd x = czero();
+        if (c < w) {
+            const double lcc = d[c].x;
+            x = lcc > 0.0 ? cscale(z[c * NR + r], 1.0 / lcc) : czero();
+            for (int c2 = c + 1; c2 < w; ++c2) x = cfma(x, d[c2], z[c2 * NR + r]);
+        }
+        if (lane < NB * NR) xw[wave][lane] = x;
+        if (wave == 0 && c < w) th[(size_t)(k0 + c) * NR + r] = cconj(x);
+        wave_sync();
+        if (tid < k0) {
+#pragma unroll
+            for (int cc = 0; cc < NB; ++cc)
+#pragma unroll
+                for (int q = 0; q < NR; ++q) {       // y -= x conj(l): four FMAs
+                    const cd xv = xw[wave][cc * NR + q];
+                    yr[q] = cfmac(yr[q], cmk(-xv.x, -xv.y), bf.lv[cc]);
+                }
+        }
+        if (kb > 0) {
+            // next block's update columns into the same registers (rows tid < k0 - 16 only)
+#pragma unroll
+            for (int cc = 0; cc < NB; ++cc)
+                bf.lv[cc] = (tid < k0 - NB) ? R[(size_t)(k0 - NB + cc) * L + tid] : czero();
+            // publish the next block's rows and diagonal block
+            if (tid >= k0 - NB && tid < k0) {
+#pragma unroll
+                for (int q = 0; q < NR; ++q) zb[(kb - 1) & 1][(tid - (k0 - NB)) * NR + q] = yr[q];
+            }
+            db[(kb - 1) & 1][tid] = dnext;
+        }
+        __syncthreads();
+    }
+}
+
 hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_t s) {
     const int skip = g_chol_skip;                   // diagnostic only (see kernels)
     hipError_t e = launch_diag_tol(pb, a, s);
@@ -1272,10 +1347,20 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
                            skip);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    // SBCE_BACKSUB=1 keeps the one-step-prefetch kernel, =2 the two-ahead three-barrier
-    // kernel (A/B runs); default: one barrier per block step
+    // default: one-buffer one-barrier kernel (backsub4); SBCE_BACKSUB=3 the two-buffer one-barrier
+    // kernel, =2 the two-ahead three-barrier kernel, =1 the one-step-prefetch kernel (A/B runs)
     const char* bsv = getenv("SBCE_BACKSUB");
-    if (pb.L <= 272 && pb.NR <= 4 && !(bsv && (bsv[0] == '1' || bsv[0] == '2')) && !(skip & 16)) {
+    if (pb.L <= 272 && pb.NR <= 4 && !(bsv && (bsv[0] == '1' || bsv[0] == '2' || bsv[0] == '3')) &&
+        !(skip & 16)) {
+        switch (pb.NR) {
+            case 1: hipLaunchKernelGGL(backsub4_kernel<1>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+            case 2: hipLaunchKernelGGL(backsub4_kernel<2>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+            case 3: hipLaunchKernelGGL(backsub4_kernel<3>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+            default: hipLaunchKernelGGL(backsub4_kernel<4>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+        }
+        return hipGetLastError();
+    }
+    if (pb.L <= 272 && pb.NR <= 4 && bsv && bsv[0] == '3' && !(skip & 16)) {
         switch (pb.NR) {
             case 1: hipLaunchKernelGGL(backsub3_kernel<1>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
             case 2: hipLaunchKernelGGL(backsub3_kernel<2>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
