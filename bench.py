@@ -64,7 +64,7 @@ ESTEP = {"cfg1": ("soft", 0, "chol"), "plumbing": ("soft", 0, "chol"),
 ESTEP_KERNELS = ["estep_tree_kernel", "estep_bfs_kernel", "estep_bounds_kernel", "estep_prep_kernel",
                  "estep_mfma_kernel_occ3", "estep_mfma_kernel"]
 MSTEP_KERNELS = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_kernel", "rhs_lds_kernel",
-                 "rhs_kernel", "diag_tol_kernel", "panel_update_kernel", "panel_factor_kernel",
+                 "rhs_dma_kernel", "rhs_kernel", "diag_tol_kernel", "panel_update_kernel", "panel_factor_kernel",
                  "backsub_kernel", "backsub2_kernel", "backsub3_kernel",
                  "backsub4_kernel", "chol_mfma_kernel"]
 MSTEP_KERNELS_LARGE = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_wide_kernel",

@@ -199,6 +199,83 @@ __global__ __launch_bounds__(512) void rhs_lds_kernel(MstepArgs a, int P, int NT
     }
 }
 
+// The same with the symbol chunks double-buffered by LDS-DMA (global_load_lds, no staging
+// registers): chunk c + 1's phases, moments and observations are in flight while chunk c is
+// accumulated, one workgroup barrier per chunk (rhs_lds_kernel waits on each chunk's global
+// loads with the whole block idle).  Lanes past a partial last chunk re-read its last element.
+template <int NR>
+__global__ __launch_bounds__(512) void rhs_dma_kernel(MstepArgs a, int P, int NT, int Tp, int Td,
+                                                      int L, int TCR) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int CH = TCR * (P + NT + NR);              // cd per chunk buffer: [TCR][P] [TCR][NT] [TCR][NR]
+    const int b = blockIdx.x;
+    if (a.done && a.done[b]) return;
+    const int tid = threadIdx.x, nth = blockDim.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nth >> 6;
+    const bool live = tid < L;
+    const int l = live ? tid : L - 1;
+    const int p = l / NT, ai = l - p * NT;
+    const int MS = NT + NT * NT;
+    const cd* ps = a.psid + (size_t)b * Td * P;
+    const cd* mom = a.mom + (size_t)b * Td * MS;
+    const cd* yd = a.yd + (size_t)b * Td * NR;
+    auto stage = [&](int t0, cd* dst) {
+        const int tc = (Td - t0) < TCR ? (Td - t0) : TCR;
+        cd* d_m = dst + TCR * P;
+        cd* d_y = d_m + TCR * NT;
+        for (int e0 = wave * 64; e0 < TCR * P; e0 += nw * 64) {
+            const int e = e0 + lane, ec = e < tc * P ? e : tc * P - 1;
+            if (e < TCR * P)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ps + (size_t)t0 * P + ec),
+                                                 (__attribute__((address_space(3))) void*)(dst + e0), 16, 0, 0);
+        }
+        for (int e0 = wave * 64; e0 < TCR * NT; e0 += nw * 64) {
+            const int e = e0 + lane, tt = e / NT, tcl = tt < tc ? tt : tc - 1;
+            if (e < TCR * NT)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(mom + (size_t)(t0 + tcl) * MS + (e - tt * NT)),
+                                                 (__attribute__((address_space(3))) void*)(d_m + e0), 16, 0, 0);
+        }
+        for (int e0 = wave * 64; e0 < TCR * NR; e0 += nw * 64) {
+            const int e = e0 + lane, ec = e < tc * NR ? e : tc * NR - 1;
+            if (e < TCR * NR)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(yd + (size_t)t0 * NR + ec),
+                                                 (__attribute__((address_space(3))) void*)(d_y + e0), 16, 0, 0);
+        }
+    };
+    cd* buf = reinterpret_cast<cd*>(smem);
+    if (Td > 0) stage(0, buf);                       // first chunk in flight during the pilot sums
+    cd acc[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc[r] = czero();
+    const cd* up = a.up + (size_t)b * Tp * L;
+    const cd* yp = a.yp + (size_t)b * Tp * NR;
+    for (int tp = 0; tp < Tp; ++tp) {
+        const cd u = up[tp * L + l];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) acc[r] = cfmac(acc[r], u, yp[tp * NR + r]);
+    }
+    int c = 0;
+    for (int t0 = 0; t0 < Td; t0 += TCR, ++c) {
+        const int tc = (Td - t0) < TCR ? (Td - t0) : TCR;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's DMAs of chunk c
+        __syncthreads();                                     // everyone's; chunk c - 1 consumed
+        if (t0 + TCR < Td) stage(t0 + TCR, buf + ((c + 1) & 1) * CH);
+        const cd* s_ps = buf + (c & 1) * CH;
+        const cd* s_m = s_ps + TCR * P;
+        const cd* s_y = s_m + TCR * NT;
+        for (int tt = 0; tt < tc; ++tt) {
+            const cd w = cmul(s_ps[tt * P + p], s_m[tt * NT + ai]);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) acc[r] = cfmac(acc[r], w, s_y[tt * NR + r]);
+        }
+    }
+    if (live) {
+        cd* rhs = a.rhs + ((size_t)b * L + l) * NR;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) rhs[r] = acc[r];
+    }
+}
+
 // ------------------------------------------------------------------ small per-trial kernels
 __device__ double block_sum(double v, double* sh) {
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
@@ -453,6 +530,17 @@ hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a0, hipStream_
         const int nth = (pb.L + 63) / 64 * 64;
         const int tcr = pb.P <= 128 ? 16 : 4;             // <= 33 KB of phases per chunk
         const size_t lds = (size_t)tcr * (pb.P + pb.NT + pb.NR) * sizeof(cd);
+        // default: LDS-DMA double-buffered chunks when two buffers fit 64 KB (cfg1: 37 KB);
+        // SBCE_RHS_IMPL=lds keeps the single-buffer kernel (A/B runs)
+        if (2 * lds <= 64 * 1024 && !(rimpl && rimpl[0] == 'l')) {
+            switch (pb.NR) {
+#define SBCE_RHSD(n) case n: hipLaunchKernelGGL(rhs_dma_kernel<n>, dim3(pb.B), dim3(nth), 2 * lds, s, a, pb.P, pb.NT, pb.Tp, pb.Td, pb.L, tcr); break;
+                SBCE_RHSD(1) SBCE_RHSD(2) SBCE_RHSD(3) SBCE_RHSD(4) SBCE_RHSD(5) SBCE_RHSD(6) SBCE_RHSD(7) SBCE_RHSD(8)
+#undef SBCE_RHSD
+                default: return hipErrorInvalidValue;
+            }
+            return hipGetLastError();
+        }
         switch (pb.NR) {
 #define SBCE_RHSL(n) case n: hipLaunchKernelGGL(rhs_lds_kernel<n>, dim3(pb.B), dim3(nth), lds, s, a, pb.P, pb.NT, pb.Tp, pb.Td, pb.L, tcr); break;
             SBCE_RHSL(1) SBCE_RHSL(2) SBCE_RHSL(3) SBCE_RHSL(4) SBCE_RHSL(5) SBCE_RHSL(6) SBCE_RHSL(7) SBCE_RHSL(8)
