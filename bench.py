@@ -72,7 +72,7 @@ MSTEP_KERNELS_LARGE = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_wide
                        "tile_gemm_kernel", "backdiag_kernel", "backupd_kernel"]
 # launched exactly once per M-step (the divisor of the phase's PMC totals; the pilot
 # factorisation runs once per EM run, so its bytes are spread over the run's M-steps)
-MSTEP_ANCHORS = ["rhs_lds_kernel", "rhs_kernel"]
+MSTEP_ANCHORS = ["rhs_dma_kernel", "rhs_lds_kernel", "rhs_kernel"]
 
 
 def mstep_flops_per_trial_iter(n_tx, n_rx, N, T_p, T_d):
