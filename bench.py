@@ -115,6 +115,19 @@ def load_pmc_traffic(path):
         return None
 
 
+def phase_traffic(pmc, kernels, anchor):
+    """HBM bytes of ONE phase execution from a PMC summary (tools/pmc_summary.py): total
+    FETCH / WRITE bytes of the phase's kernels divided by the launches of its once-per-phase
+    anchor kernel (the first name in `anchor` the summary holds); None without an anchor."""
+    ks = (pmc or {}).get("kernels", {})
+    anc = next((ks[a] for a in anchor if a in ks), None)
+    if not anc or not anc["launches_fetch"] or not anc["launches_write"]:
+        return None
+    ents = [v for k, v in ks.items() if k in kernels]
+    return (sum(e["fetch_bytes_total"] for e in ents) / anc["launches_fetch"] +
+            sum(e["write_bytes_total"] for e in ents) / anc["launches_write"])
+
+
 def cpu_baseline(cfg, varn, seed, iters=2, mode="soft", part_r=0):
     """Oracle port (vectorised float64 NumPy reduced form, or the PM list oracle) on
     1 trial x `iters` EM iterations of the same configuration: ~10-30 s of CPU work."""
@@ -273,18 +286,7 @@ def main():
     pmc_ok = bool(pmc and pmc.get("config") == args.config and pmc.get("trials") == B)
 
     def traffic_of(kernels, anchor):
-        """HBM bytes of ONE phase execution from the committed PMC summary of the same config
-        and trial count (tools/pmc_summary.py): total FETCH / WRITE bytes of the phase's
-        kernels divided by the launches of its once-per-phase anchor kernel; else None."""
-        if not pmc_ok:
-            return None
-        ks = pmc.get("kernels", {})
-        anc = next((ks[a] for a in anchor if a in ks), None)
-        if not anc or not anc["launches_fetch"] or not anc["launches_write"]:
-            return None
-        ents = [v for k, v in ks.items() if k in kernels]
-        return (sum(e["fetch_bytes_total"] for e in ents) / anc["launches_fetch"] +
-                sum(e["write_bytes_total"] for e in ents) / anc["launches_write"])
+        return phase_traffic(pmc, kernels, anchor) if pmc_ok else None
 
     mflops = mstep_flops_per_trial_iter(n_tx, n_rx, N, T_p, T_d) * B
     mbytes = mstep_bytes_per_trial_iter(n_tx, n_rx, N, T_p, T_d) * B

@@ -102,3 +102,26 @@ def test_oversized_problems_are_unsupported_without_gpu(sbce):
     assert lib.sbce_mstep(ctypes.byref(big), ctypes.byref(p), 16, 0, None, None, None) == -2
     ok = L.Dims(2, 8, 4, 1024, 16, 64, 16, 1, 0.1)       # L = 8192: supported
     assert L.workspace_bytes(ok) > 2 * 8192 * 8192 * 16
+
+
+def test_bench_roofline_traffic_uses_committed_pmc():
+    """bench.py's roofline.traffic comes from the committed PMC summaries: every phase's
+    anchor kernel must be present in them, or the bench line silently reports null
+    (the B^H kernel's rename once did exactly that)."""
+    import importlib.util
+    import json
+    spec = importlib.util.spec_from_file_location("sbce_bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    with open(os.path.join(ROOT, "profiles", "pmc_cfg1_latest.json")) as f:
+        pmc1 = json.load(f)
+    assert pmc1["config"] == "cfg1" and pmc1["trials"] == 1000
+    m = bench.phase_traffic(pmc1, bench.MSTEP_KERNELS, bench.MSTEP_ANCHORS)
+    e = bench.phase_traffic(pmc1, bench.ESTEP_KERNELS, bench.ESTEP_KERNELS)
+    assert m is not None and e is not None
+    # above the algorithmic floor of one 1000-trial M-step
+    assert m > bench.mstep_bytes_per_trial_iter(4, 4, 64, 16, 256) * 1000
+    with open(os.path.join(ROOT, "profiles", "pmc_cfg2_latest.json")) as f:
+        pmc2 = json.load(f)
+    assert bench.phase_traffic(pmc2, bench.MSTEP_KERNELS_LARGE, bench.MSTEP_ANCHORS) is not None
+    assert bench.phase_traffic({}, bench.MSTEP_KERNELS, bench.MSTEP_ANCHORS) is None
