@@ -16,8 +16,8 @@ constexpr size_t kAlign = 256;
 size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 struct Carve {
-    size_t mom, R, rhs, done, ysh, prep, list, tree, tol, winv, ppsi, pS, pflag, total;
-    bool has_prep;
+    size_t mom, R, rhs, done, ysh, prep, list, tree, tol, winv, ppsi, pS, pflag, prhs, total;
+    bool has_prep, has_prhs;
 };
 
 bool make_problem(const sbce_dims* d, Problem& pb) {
@@ -57,6 +57,11 @@ Carve carve(const Problem& pb) {
         c.pflag = align_up(c.pS + (size_t)pb.B * pb.Tp * pb.NT * pb.NT * sizeof(cd));
         c.total = align_up(c.pflag + (size_t)pb.B * sizeof(int32_t));
     }
+    // the pilot part of B^H is fixed across iterations: kept once per run for the L <= 512
+    // B^H kernel (mstep.hip rhs_dma_kernel), which then reads L*NR values instead of u_p, y_p
+    c.has_prhs = rbuild_herm_supported(pb) && pb.L <= kLargeL;
+    c.prhs = c.total;
+    if (c.has_prhs) c.total = align_up(c.prhs + (size_t)pb.B * pb.L * pb.NR * sizeof(cd));
     c.tol = c.total;                         // per-trial pivot threshold
     c.winv = c.total = align_up(c.tol + (size_t)pb.B * sizeof(double));
     if (pb.L > kLargeL)                      // tiled large-L M-step (mstep_large.hip)
@@ -72,6 +77,7 @@ void set_large(MstepArgs& ma, char* ws, const Carve& c) {
     ma.ppsi = (cd*)(ws + c.ppsi);
     ma.pS = (cd*)(ws + c.pS);
     ma.pflag = (int32_t*)(ws + c.pflag);
+    ma.prhs = c.has_prhs ? (cd*)(ws + c.prhs) : nullptr;
     ma.gate = nullptr;
 }
 

@@ -247,12 +247,18 @@ __global__ __launch_bounds__(512) void rhs_dma_kernel(MstepArgs a, int P, int NT
     cd acc[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) acc[r] = czero();
-    const cd* up = a.up + (size_t)b * Tp * L;
-    const cd* yp = a.yp + (size_t)b * Tp * NR;
-    for (int tp = 0; tp < Tp; ++tp) {
-        const cd u = up[tp * L + l];
+    if (a.prhs && Tp > 0) {                          // pilot part kept once per run
+        const cd* pr = a.prhs + ((size_t)b * L + l) * NR;
 #pragma unroll
-        for (int r = 0; r < NR; ++r) acc[r] = cfmac(acc[r], u, yp[tp * NR + r]);
+        for (int r = 0; r < NR; ++r) acc[r] = pr[r];
+    } else {
+        const cd* up = a.up + (size_t)b * Tp * L;
+        const cd* yp = a.yp + (size_t)b * Tp * NR;
+        for (int tp = 0; tp < Tp; ++tp) {
+            const cd u = up[tp * L + l];
+#pragma unroll
+            for (int r = 0; r < NR; ++r) acc[r] = cfmac(acc[r], u, yp[tp * NR + r]);
+        }
     }
     int c = 0;
     for (int t0 = 0; t0 < Td; t0 += TCR, ++c) {

@@ -83,6 +83,20 @@ __global__ __launch_bounds__(64) void pilot_factor_kernel(MstepArgs a, int P, in
     }
 }
 
+// Pilot part of B^H, once per run: prhs[b][l][r] = sum_tp u_p[tp][l] y_p[tp][r], one thread per
+// (l, r), summed in tp order exactly as rhs_dma_kernel's own pilot loop (same bits).
+__global__ __launch_bounds__(256) void pilot_rhs_kernel(MstepArgs a, int Tp, int L, int NR) {
+    const int b = blockIdx.y;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= L * NR) return;
+    const int l = e / NR, r = e - l * NR;
+    const cd* up = a.up + (size_t)b * Tp * L;
+    const cd* yp = a.yp + (size_t)b * Tp * NR;
+    cd acc = czero();
+    for (int tp = 0; tp < Tp; ++tp) acc = cfmac(acc, up[tp * L + l], yp[tp * NR + r]);
+    a.prhs[((size_t)b * L + l) * NR + r] = acc;
+}
+
 // ---------------------------------------------------------------- R build (MFMA)
 // R[(p,i),(q,j)] = sum_t psi_t[p] conj(psi_t[q]) S_t[i][j] over the pairs p >= q, with
 // S_t Hermitian.  Writing w = psi_p conj(psi_q) = wr + i wi and S_ij = Sr + i Si (i < j):
@@ -613,6 +627,9 @@ hipError_t launch_pilot_factor(const Problem& pb, const MstepArgs& a, hipStream_
     if (pb.Tp == 0 || pb.B == 0) return hipSuccess;
     hipLaunchKernelGGL(pilot_factor_kernel, dim3(pb.Tp, pb.B), dim3(64), 0, s, a, pb.P, pb.NT,
                        pb.Tp, pb.L);
+    if (a.prhs)
+        hipLaunchKernelGGL(pilot_rhs_kernel, dim3((pb.L * pb.NR + 255) / 256, pb.B), dim3(256), 0,
+                           s, a, pb.Tp, pb.L, pb.NR);
     return hipGetLastError();
 }
 

@@ -145,6 +145,8 @@ struct MstepArgs {
     cd* ppsi;          // [B][Tp][P]  pilot phases psi' (Kronecker factor of u_p)
     cd* pS;            // [B][Tp][NT*NT] pilot x' x'^H
     int32_t* pflag;    // [B] u_p of the trial is not a Kronecker product (set by pilot_factor)
+    cd* prhs;          // [B][L][NR] pilot part of B^H, sum_p u_p y_p (set by pilot_factor; null:
+                       // not kept, the B^H kernel sums the pilots itself)
     const int32_t* gate;  // VALU build: only trials with gate[b] != 0 (null: all trials)
     // large-L path (L > 512) workspace
     double* tol;       // [B]     pivot threshold
