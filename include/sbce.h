@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define SBCE_ABI_VERSION 3
+#define SBCE_ABI_VERSION 4
 
 /* return codes */
 #define SBCE_OK 0
@@ -87,8 +87,18 @@ extern "C" {
 #define SBCE_SOLVE_CHOL 0       /* Hermitian Cholesky of the reduced L x L system
                                    (== LU of the K x K reference system,
                                    Proposed_method_NMSEvsTp.py:80, on HPD R) */
-#define SBCE_SOLVE_CHOL_DROP 1  /* non-HPD pivots dropped (solution restricted to
-                                   the well-posed subspace; lstsq-like, PM.py:108) */
+#define SBCE_SOLVE_CHOL_DROP 1  /* non-HPD pivots (<= 1e-14 max diag R) dropped: a basic
+                                   solution on the kept coordinates, NOT minimum-norm */
+#define SBCE_SOLVE_MINNORM 2    /* minimum-norm least squares, np.linalg.lstsq of PM.py:108
+                                   (the intended fallback of all_detectorsvsTd.py:238-241):
+                                   R's rank is cut at eps*K*lambda_max(R) (lstsq's default
+                                   rcond = eps*max(K,K) on the K x K system, whose singular
+                                   values are R's eigenvalues), lambda_max by 6 Lanczos steps;
+                                   R = G G^H by a Cholesky that drops the pivots below 32x the
+                                   cut (above its rounding noise), theta = conj(G (G^H G)^-2
+                                   G^H B^H).  Equal to lstsq when no pivot lies between 4x the
+                                   cut and 2048x it (else SBCE_STATUS_RANK) and no eigenvalue
+                                   of R lies just below the cut */
 
 /* per-trial status bits */
 #define SBCE_STATUS_NONHPD 1
@@ -100,7 +110,11 @@ extern "C" {
                                    all_possibleSymbols (IndexError at
                                    all_detectorsvsTd.py:52); row flat mod M^n_tx used */
 #define SBCE_STATUS_DEBUG 8     /* a diagnostic phase-skip mask (sbce_debug_chol_skip, not
-                                   part of this header's API) was active: theta is invalid */
+                                   part of this header's API) or a non-default kernel selected
+                                   by an SBCE_* debug environment variable was active */
+#define SBCE_STATUS_RANK 16     /* SBCE_SOLVE_MINNORM: a Cholesky pivot lay between 4x lstsq's
+                                   rank cut and 2048x it, where the pivot-based rank may differ
+                                   from the singular-value rank np.linalg.lstsq uses */
 
 typedef struct sbce_dims {
     int32_t batch;      /* B: independent Monte-Carlo trials */
@@ -145,7 +159,8 @@ int sbce_abi_version(void);
 /* Static description of an error code. */
 const char* sbce_strerror(int code);
 
-/* Device workspace needed by sbce_em / sbce_estep / sbce_mstep for `d`. */
+/* Device workspace needed by sbce_em / sbce_estep / sbce_mstep for `d` (every solve mode).
+ * The size depends on the library version: re-query it after upgrading the library. */
 int sbce_workspace_bytes(const sbce_dims* d, size_t* bytes);
 
 /* Full EM: `iters` iterations of E-step + M-step on every trial of the batch.

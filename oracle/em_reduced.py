@@ -103,6 +103,32 @@ def mstep_build(U_p, Y_p, Psi, Y_d, m, S):
     return R, rhs
 
 
+def mstep_build_gemm(U_p, Y_p, Psi, Y_d, m, S):
+    """mstep_build as two GEMMs (same sums, any order): R[(p,a),(q,b)] = sum_t Psi[p,t]
+    S_t[a,b] conj(Psi[q,t]) -- for the full-size (L = 2056 / 4100) checks, where the einsum
+    would take minutes."""
+    P, T = Psi.shape
+    n_tx = m.shape[1]
+    L = P * n_tx
+    A = (Psi[:, None, None, :] * np.transpose(S, (1, 2, 0))[None]).reshape(P * n_tx * n_tx, T)
+    R4 = (A @ np.conj(Psi).T).reshape(P, n_tx, n_tx, P)            # [p, a, b, q]
+    R = np.transpose(R4, (0, 1, 3, 2)).reshape(L, L) + U_p.T @ np.conj(U_p)
+    rhs = U_p.T @ np.conj(Y_p)
+    rhs = rhs + ((Psi[:, None, :] * m.T[None]).reshape(L, T) @ np.conj(Y_d))
+    return R, rhs
+
+
+def mstep_lstsq(R, rhs):
+    """np.linalg.lstsq of PMd/PM.py:108 on the reduced system.  The reference's K x K
+    matrix A = sum Z^H Z = conj(R) (x) I_{n_rx} (up to the vec permutation) has R's
+    eigenvalues as singular values, each n_rx times, and lstsq's default rcond is
+    eps * max(K, K): the same cut applied to R's spectrum (K = L n_rx).  Returns
+    (theta, rank of R)."""
+    L, n_rx = rhs.shape
+    X, _, rank, _ = np.linalg.lstsq(R, rhs, rcond=np.finfo(float).eps * L * n_rx)
+    return np.conj(X).reshape(-1), int(rank)
+
+
 def mstep_solve(R, rhs):
     """H_c R = B  <=>  R H_c^H = B^H; theta[l*n_rx + r] = conj(X[l, r])
     (PMd/Proposed_method_NMSEvsTp.py:80 np.linalg.solve on the K x K form)."""

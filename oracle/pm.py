@@ -88,17 +88,19 @@ def pm_moments(theta, Y_d, Psi, qamCons, n_tx, n_rx, partition_r, varn, soft):
 
 
 def em_pm(Y_d, Y_p, U_p, Psi, varn, itera, theta0, n_tx, n_rx, partition_r, qamCons,
-          soft=False, h=None, return_trace=False):
+          soft=False, h=None, return_trace=False, solve=None):
     """PM EM over one trial, array inputs (Y_d (T_d,n_rx), Psi (N+1,T_d), U_p (T_p,L)).
-    Reduced-form M-step; list weights uniform (soft=False, PM.py) or posterior
-    (soft=True, PM_beta.py)."""
-    from .em_reduced import mstep_build, mstep_solve
+    Reduced-form M-step; list weights uniform (soft=False, PM.py, np.linalg.lstsq at
+    PM.py:108) or posterior (soft=True, PM_beta.py, np.linalg.solve at PM_beta.py:104);
+    ``solve`` ('lstsq' / 'solve') overrides the reference's choice."""
+    from .em_reduced import mstep_build, mstep_solve, mstep_lstsq
+    solve = solve or ("solve" if soft else "lstsq")
     theta = np.asarray(theta0, dtype=complex).reshape(-1)
     trace = []
     for l in range(itera):
         m, S = pm_moments(theta, Y_d, Psi, qamCons, n_tx, n_rx, partition_r, varn, soft)
         R, rhs = mstep_build(U_p, Y_p, Psi, Y_d, m, S)
-        theta = mstep_solve(R, rhs)
+        theta = mstep_lstsq(R, rhs)[0] if solve == "lstsq" else mstep_solve(R, rhs)
         trace.append(theta.copy())
         if h is not None and np.abs(norm(theta) - norm(h)) < 1 and l != 0:
             break

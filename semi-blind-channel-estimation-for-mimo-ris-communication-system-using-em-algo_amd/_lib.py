@@ -4,13 +4,14 @@ This is the ONLY way the package reaches its compute path.  There is no CPU
 fallback: if the shared library is missing, or no HIP device is visible, the
 calls raise ``SbceUnavailable``.
 """
+import contextlib
 import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsbce.so")
 
-SBCE_ABI_VERSION = 3
+SBCE_ABI_VERSION = 4
 SBCE_ESTEP_SOFT = 0
 SBCE_ESTEP_HARD = 1
 SBCE_ESTEP_PM = 2
@@ -20,10 +21,12 @@ SBCE_ESTEP_MMSE = 5
 SBCE_ESTEP_GAUSS = 6
 SBCE_SOLVE_CHOL = 0
 SBCE_SOLVE_CHOL_DROP = 1
+SBCE_SOLVE_MINNORM = 2
 SBCE_STATUS_NONHPD = 1
 SBCE_STATUS_PILOT = 2
 SBCE_STATUS_DETECTOR = 4
 SBCE_STATUS_DEBUG = 8
+SBCE_STATUS_RANK = 16
 
 EXPORTED = ("sbce_abi_version", "sbce_strerror", "sbce_workspace_bytes", "sbce_em",
             "sbce_estep", "sbce_mstep", "sbce_ser", "sbce_gauss_expand", "sbce_nmse")
@@ -95,6 +98,34 @@ def load(path=None):
     if path is None:
         _lib = lib
     return lib
+
+
+def reload_debug_env():
+    """Re-read the SBCE_* A/B switches (include/sbce.h SBCE_STATUS_DEBUG) into the loaded
+    library; they are otherwise read once, when libsbce.so is loaded.  Returns True when a
+    result-affecting switch is active."""
+    lib = load()
+    lib.sbce_debug_reload_env.restype = ctypes.c_int
+    return bool(lib.sbce_debug_reload_env())
+
+
+@contextlib.contextmanager
+def debug_env(**env):
+    """Run a block with SBCE_* debug switches set (diagnostics and A/B tests only):
+    ``with debug_env(SBCE_ESTEP_IMPL="valu"): ...``; restores the environment after."""
+    old = {k: os.environ.get(k) for k in env}
+    try:
+        for k, v in env.items():
+            os.environ[k] = str(v)
+        reload_debug_env()
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        reload_debug_env()
 
 
 def check(rc, what):

@@ -4,11 +4,60 @@
 // for a whole batch of Monte-Carlo trials: per iteration one E-step launch over
 // every (trial, symbol), one normal-equation build and one batched Cholesky
 // solve, all stream-ordered, with no host synchronisation and no allocation.
+#include <stdlib.h>
 #include <string.h>
 
 #include "sbce_internal.h"
 
 using namespace sbce;
+
+namespace sbce {
+
+DebugConfig g_debug;
+
+namespace {
+constexpr DebugConfig kDebugDefault = {false, false, false, 4, false, false, false, false, 128,
+                                       0, false, false, 0, 0};
+constexpr int kSphereBudgetMax = 256;      // estep.hip kBfsPmax
+
+void read_debug_env(DebugConfig& c) {
+    c = kDebugDefault;
+    auto env = [](const char* n) { const char* v = getenv(n); return (v && v[0]) ? v : nullptr; };
+    const char* v;
+    if ((v = env("SBCE_ESTEP_IMPL"))) c.estep_valu = v[0] == 'v';
+    if ((v = env("SBCE_ESTEP_PRUNE"))) c.estep_noprune = v[0] == '0';
+    if ((v = env("SBCE_ESTEP_COUNT"))) c.estep_count = v[0] == '1';
+    if ((v = env("SBCE_ESTEP_SPW"))) c.estep_spw = atoi(v) < 1 ? 1 : atoi(v);
+    if ((v = env("SBCE_ESTEP_ROWB"))) c.estep_norowb = v[0] == '0';
+    if ((v = env("SBCE_ESTEP_OCC"))) c.estep_occ2 = v[0] == '2';
+    if ((v = env("SBCE_PREP_UNI"))) c.prep_nouni = v[0] == '0';
+    if ((v = env("SBCE_ESTEP_SPHERE"))) c.estep_nosphere = v[0] == '0';
+    if ((v = env("SBCE_SPHERE_BUDGET"))) {
+        const int bu = atoi(v);
+        c.sphere_budget = bu < 1 ? 1 : (bu > kSphereBudgetMax ? kSphereBudgetMax : bu);
+    }
+    if ((v = env("SBCE_RHS_IMPL"))) c.rhs_impl = (v[0] == 'r' || v[0] == 'l') ? v[0] : 0;
+    if ((v = env("SBCE_RB_TC"))) c.rb_tc32 = v[0] == '3';
+    if ((v = env("SBCE_UPD_WAVES"))) c.upd_waves8 = v[0] == '8';
+    if ((v = env("SBCE_BACKSUB"))) c.backsub = (v[0] >= '1' && v[0] <= '3') ? v[0] - '0' : 0;
+    if ((v = env("SBCE_CHOL_IMPL"))) c.chol_impl = (v[0] == 'v' || v[0] == 'f') ? v[0] : 0;
+}
+
+__attribute__((constructor)) void load_debug_env() { read_debug_env(g_debug); }
+}  // namespace
+
+bool debug_nondefault() {
+    const DebugConfig& c = g_debug;
+    const DebugConfig& d = kDebugDefault;
+    return c.estep_valu != d.estep_valu || c.estep_noprune != d.estep_noprune ||
+           c.estep_spw != d.estep_spw || c.estep_norowb != d.estep_norowb ||
+           c.estep_occ2 != d.estep_occ2 || c.prep_nouni != d.prep_nouni ||
+           c.estep_nosphere != d.estep_nosphere || c.sphere_budget != d.sphere_budget ||
+           c.rhs_impl != d.rhs_impl || c.rb_tc32 != d.rb_tc32 || c.upd_waves8 != d.upd_waves8 ||
+           c.backsub != d.backsub || c.chol_impl != d.chol_impl || (chol_debug_skip_mask() & 31);
+}
+
+}  // namespace sbce
 
 namespace {
 
@@ -16,7 +65,8 @@ constexpr size_t kAlign = 256;
 size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 struct Carve {
-    size_t mom, R, rhs, done, ysh, prep, list, tree, tol, winv, ppsi, pS, pflag, prhs, total;
+    size_t mom, R, rhs, done, ysh, prep, list, tree, tol, winv, ppsi, pS, pflag, prhs, gram, grhs,
+        act, tol2, total;
     bool has_prep, has_prhs;
 };
 
@@ -63,9 +113,14 @@ Carve carve(const Problem& pb) {
     c.prhs = c.total;
     if (c.has_prhs) c.total = align_up(c.prhs + (size_t)pb.B * pb.L * pb.NR * sizeof(cd));
     c.tol = c.total;                         // per-trial pivot threshold
-    c.winv = c.total = align_up(c.tol + (size_t)pb.B * sizeof(double));
-    if (pb.L > kLargeL)                      // tiled large-L M-step (mstep_large.hip)
-        c.total = align_up(c.winv + (size_t)pb.B * 64 * 64 * sizeof(cd));
+    c.winv = align_up(c.tol + (size_t)pb.B * sizeof(double));
+    // tiled factorisation (L > 512, and the min-norm solve at every L): diagonal-tile inverse
+    c.gram = align_up(c.winv + (size_t)pb.B * 64 * 64 * sizeof(cd));
+    // min-norm solve (minnorm.hip): Gram matrix C = G^H G, its right-hand sides, extents
+    c.grhs = align_up(c.gram + (size_t)pb.B * pb.L * pb.L * sizeof(cd));
+    c.act = align_up(c.grhs + (size_t)pb.B * pb.L * pb.NR * sizeof(cd));
+    c.tol2 = align_up(c.act + (size_t)pb.B * sizeof(int32_t));
+    c.total = align_up(c.tol2 + (size_t)pb.B * sizeof(double));
     return c;
 }
 
@@ -79,9 +134,22 @@ void set_large(MstepArgs& ma, char* ws, const Carve& c) {
     ma.pflag = (int32_t*)(ws + c.pflag);
     ma.prhs = c.has_prhs ? (cd*)(ws + c.prhs) : nullptr;
     ma.gate = nullptr;
+    ma.gram = (cd*)(ws + c.gram);
+    ma.grhs = (cd*)(ws + c.grhs);
+    ma.act = (int32_t*)(ws + c.act);
+    ma.tol2 = (double*)(ws + c.tol2);
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// per-trial status starts at 0, or at SBCE_STATUS_DEBUG while a result-affecting debug switch
+// (DebugConfig) is active
+int status_init(int32_t* status, int B, hipStream_t s) {
+    if (!status) return SBCE_OK;
+    const unsigned v = debug_nondefault() ? SBCE_STATUS_DEBUG : 0u;
+    return hipMemsetD32Async((hipDeviceptr_t)status, v, (size_t)B, s) == hipSuccess ? SBCE_OK
+                                                                                    : SBCE_EHIP;
+}
 
 int check_ptrs(const sbce_ptrs* p, const Problem& pb, bool need_ws) {
     if (!p) return SBCE_EINVAL;
@@ -127,7 +195,9 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     if (!estep_supported(pb, estep_mode) || !chol_supported(pb)) return SBCE_EUNSUPPORTED;
     int rc = check_ptrs(p, pb, true);
     if (rc) return rc;
-    if (solve_mode != SBCE_SOLVE_CHOL && solve_mode != SBCE_SOLVE_CHOL_DROP) return SBCE_EINVAL;
+    if (solve_mode != SBCE_SOLVE_CHOL && solve_mode != SBCE_SOLVE_CHOL_DROP &&
+        solve_mode != SBCE_SOLVE_MINNORM)
+        return SBCE_EINVAL;
     if (p->llf && !p->x_d_true) return SBCE_EINVAL;
     const bool gauss = estep_mode == SBCE_ESTEP_GAUSS;
     if (gauss && !(pb.varx > 0.0)) return SBCE_EINVAL;
@@ -143,8 +213,7 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     char* ws = (char*)p->workspace;
     int32_t* done = (int32_t*)(ws + c.done);
     if (hipMemsetAsync(done, 0, (size_t)pb.B * sizeof(int32_t), s) != hipSuccess) return SBCE_EHIP;
-    if (p->status && hipMemsetAsync(p->status, 0, (size_t)pb.B * sizeof(int32_t), s) != hipSuccess)
-        return SBCE_EHIP;
+    if ((rc = status_init(p->status, pb.B, s))) return rc;
     const bool early = p->h_true != nullptr;
 
     EstepArgs ea;
@@ -210,6 +279,7 @@ int sbce_estep(const sbce_dims* d, const sbce_ptrs* p, int estep_mode, void* mom
     if (estep_mode == SBCE_ESTEP_GAUSS && !(pb.varx > 0.0)) return SBCE_EINVAL;
     if (!estep_supported(pb, estep_mode)) return SBCE_EUNSUPPORTED;
     if (pb.B == 0) return SBCE_OK;
+    if ((rc = status_init(p->status, pb.B, (hipStream_t)hip_stream))) return rc;
     EstepArgs ea;
     ea.yd = (const cd*)p->y_d; ea.psid = (const cd*)p->psi_d; ea.theta = (const cd*)p->theta;
     ea.cons = (const cd*)p->cons; ea.mom = (cd*)moments; ea.done = nullptr;
@@ -236,12 +306,14 @@ int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int 
     int rc = check_ptrs(p, pb, true);
     if (rc) return rc;
     if (!moments) return SBCE_EINVAL;
+    if (solve_mode != SBCE_SOLVE_CHOL && solve_mode != SBCE_SOLVE_CHOL_DROP &&
+        solve_mode != SBCE_SOLVE_MINNORM)
+        return SBCE_EINVAL;
     if (pb.B == 0) return SBCE_OK;
     hipStream_t s = (hipStream_t)hip_stream;
     const Carve c = carve(pb);
     char* ws = (char*)p->workspace;
-    if (p->status && hipMemsetAsync(p->status, 0, (size_t)pb.B * sizeof(int32_t), s) != hipSuccess)
-        return SBCE_EHIP;
+    if ((rc = status_init(p->status, pb.B, s))) return rc;
     MstepArgs ma;
     ma.yd = (const cd*)p->y_d; ma.yp = (const cd*)p->y_p; ma.psid = (const cd*)p->psi_d;
     ma.up = (const cd*)p->u_p; ma.mom = (const cd*)moments; ma.R = (cd*)(ws + c.R);
@@ -267,14 +339,50 @@ int sbce_debug_chol_clock(unsigned long long* out32, int reset) {
     return out32 ? hip_rc(chol_debug_clock(out32)) : SBCE_EINVAL;
 }
 
-// Diagnostic, not part of include/sbce.h: phase-skip mask of the Cholesky kernels (1 panel
-// update, 2 diagonal factor, 8 TRSM tiles, 16 back substitution: results INVALID, every
-// trial flagged SBCE_STATUS_DEBUG; 64: per-phase clocks of the fused kernel, results valid).
+// Diagnostic, not part of include/sbce.h: phase-skip mask of the L <= 512 Cholesky kernels (1
+// panel update, 2 diagonal factor, 8 TRSM tiles, 16 back substitution: results INVALID; 64:
+// per-phase clocks of the fused kernel, results valid).  Process-wide (every thread and
+// stream); while bits 0-4 are set every trial of every path is flagged SBCE_STATUS_DEBUG.
 // 0 restores normal operation.
 int sbce_debug_chol_skip(int mask) {
     if (mask < 0) return SBCE_EINVAL;
     chol_debug_skip(mask);
     return SBCE_OK;
+}
+
+// Diagnostic, not part of include/sbce.h: one piece of the M-step for kernel timing (bench.py's
+// dominant-kernel roofline), from the given moments: phase 0 = the pilot factorisation (once per
+// EM run), 1 = the R build alone (the MFMA Hermitian build rbuild_herm_kernel when n_tx is 4 or
+// 8 -- phase 0 must have run -- else the VALU build with B^H), 2 = the whole build (R and B^H).
+int sbce_debug_mstep_phase(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int phase,
+                           void* hip_stream) {
+    Problem pb;
+    if (!make_problem(d, pb)) return SBCE_EINVAL;
+    if (!chol_supported(pb)) return SBCE_EUNSUPPORTED;
+    int rc = check_ptrs(p, pb, true);
+    if (rc) return rc;
+    if (!moments || phase < 0 || phase > 2) return SBCE_EINVAL;
+    if (pb.B == 0) return SBCE_OK;
+    hipStream_t s = (hipStream_t)hip_stream;
+    const Carve c = carve(pb);
+    char* ws = (char*)p->workspace;
+    MstepArgs ma;
+    ma.yd = (const cd*)p->y_d; ma.yp = (const cd*)p->y_p; ma.psid = (const cd*)p->psi_d;
+    ma.up = (const cd*)p->u_p; ma.mom = (const cd*)moments; ma.R = (cd*)(ws + c.R);
+    ma.rhs = (cd*)(ws + c.rhs); ma.theta = (cd*)p->theta; ma.status = nullptr; ma.done = nullptr;
+    ma.solve_mode = SBCE_SOLVE_CHOL; ma.nbatch = pb.B;
+    set_large(ma, ws, c);
+    if (phase == 0) return rbuild_herm_supported(pb) ? hip_rc(launch_pilot_factor(pb, ma, s)) : SBCE_OK;
+    if (phase == 1 && rbuild_herm_supported(pb)) return hip_rc(launch_rbuild_herm(pb, ma, s));
+    return hip_rc(launch_mstep_build(pb, ma, s, rbuild_herm_supported(pb)));
+}
+
+// Diagnostic, not part of include/sbce.h: re-read the SBCE_* debug switches from the
+// environment (they are otherwise read once, when the library is loaded).  Returns 1 when a
+// result-affecting switch is now non-default (every trial is then flagged SBCE_STATUS_DEBUG).
+int sbce_debug_reload_env(void) {
+    read_debug_env(g_debug);
+    return debug_nondefault() ? 1 : 0;
 }
 
 // Diagnostic, not part of include/sbce.h: FP64 MFMAs issued by the exact E-step sweep since

@@ -52,10 +52,10 @@ __device__ __forceinline__ void factor_diag(cd* dr, int w, int lane, double tol,
             wave_sync();
             const double dia = colbuf[NB].x;
             const bool bad = !(dia > tol);
-            const bool drop = bad && solve_mode == SBCE_SOLVE_CHOL_DROP;
+            const bool drop = bad && solve_mode != SBCE_SOLVE_CHOL;
             const double piv = sqrt(bad ? tol : dia);
             const double inv = drop ? 0.0 : 1.0 / piv;
-            if (lane == 0) { dinv[c] = inv; if (bad) *flag = 1; }
+            if (lane == 0) { dinv[c] = inv; if (bad) *flag |= 1; }
             if (lane == c) dr[c] = cmk(drop ? 0.0 : piv, 0.0);
             else if (mine && lane > c) dr[c] = cscale(dr[c], inv);
             if (mine && lane > c) colbuf[lane] = dr[c];
@@ -299,7 +299,8 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
     cd* th = a.theta + (size_t)b * L * NR;
     for (int e = tid; e < L * NR; e += nth) th[e] = cconj(y[e]);
     if (tid == 0 && a.status)
-        a.status[b] |= (*flag ? SBCE_STATUS_NONHPD : 0) | ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
+        a.status[b] |= ((*flag & 1) ? SBCE_STATUS_NONHPD : 0) | ((*flag & 2) ? SBCE_STATUS_RANK : 0) |
+                       ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
 }
 
 // ---------------------------------------------------------------- MFMA kernel
@@ -323,7 +324,7 @@ __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double t
                                                 unsigned long long* clk = nullptr) {
     const int col = lane & 15, r0 = lane >> 4;
     unsigned long long tc = clk ? __builtin_amdgcn_s_memtime() : 0;
-    bool bad_any = false;
+    bool bad_any = false, near_any = false;
     // Branch-free: every entry (r, col) has exactly one owner lane, which rewrites it each
     // column (unchanged entries get their old value back); divergent branches in this
     // single-wave dependent chain cost more than the arithmetic.
@@ -340,7 +341,10 @@ __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double t
         }
         const bool bad = !(dia > tol);
         bad_any |= bad;
-        const bool drop = bad && solve_mode == SBCE_SOLVE_CHOL_DROP;
+        // min-norm solve (tol = 32 x lstsq's cut, minnorm.hip): a pivot between 4 cut and
+        // 64 tol may be decided differently from the singular values lstsq thresholds
+        near_any |= solve_mode == SBCE_SOLVE_MINNORM && dia > tol * (1.0 / 8) && dia < tol * 64;
+        const bool drop = bad && solve_mode != SBCE_SOLVE_CHOL;
         const double pv = bad ? tol : dia;
         const double rs = fast_rsqrt(pv);
         const double piv = drop ? 0.0 : pv * rs;
@@ -365,7 +369,8 @@ __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double t
         wave_sync();
         if (clk && lane == 0) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); clk[10] += t2 - tc; tc = t2; }
     }
-    if (bad_any) *flag = 1;
+    if (bad_any) *flag |= 1;
+    if (near_any) *flag |= 2;
     if (clk && lane == 0) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); clk[0] += t2 - tc; tc = t2; }
     // Di[k][j] = (delta_kj - sum_{j<=m<k} L[k][m] Di[m][j]) / L[k][k]; lane = (j, part)
     {
@@ -493,6 +498,8 @@ struct CholGeom {
     int ld, off;
     size_t stride;
     const double* tolp;
+    const int32_t* ext;    // SOLVE = false: per-trial active columns (null: all); tiles at or
+                           // past ext[b] are left untouched (min-norm path, minnorm.hip)
 };
 
 template <int MAXT, bool YLDS, int NWB, int KB, bool SOLVE = true>
@@ -504,6 +511,7 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip, CholGeom g) {
     // 8 trsm tiles, 16 back substitution
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
+    if (!SOLVE && g.ext && g.off >= g.ext[b]) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, nth = blockDim.x;
     const int lane = tid & 63, nw = nth >> 6;
@@ -689,7 +697,8 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip, CholGeom g) {
     }
 #undef SBCE_CLK
     if (tid == 0 && a.status)
-        a.status[b] |= (*flag ? SBCE_STATUS_NONHPD : 0) | ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
+        a.status[b] |= ((*flag & 1) ? SBCE_STATUS_NONHPD : 0) | ((*flag & 2) ? SBCE_STATUS_RANK : 0) |
+                       ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
 }
 
 // ---------------------------------------------------------------- batched panel kernels
@@ -1056,7 +1065,8 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
             wave_sync();
         }
     }
-    const int st = (flag ? SBCE_STATUS_NONHPD : 0) | ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
+    const int st = ((flag & 1) ? SBCE_STATUS_NONHPD : 0) | ((flag & 2) ? SBCE_STATUS_RANK : 0) |
+                   ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
     if (tid == 0 && st && a.status) atomicOr(&a.status[b], st);
 }
 
@@ -1323,8 +1333,7 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
     hipError_t e = launch_diag_tol(pb, a, s);
     if (e != hipSuccess) return e;
     const int npan = (pb.L + PW - 1) / PW;
-    const char* uw = getenv("SBCE_UPD_WAVES");
-    const int upd_waves = (uw && uw[0] == '8') ? 8 : 4;
+    const int upd_waves = g_debug.upd_waves8 ? 8 : 4;
     for (int j = 0; j < npan; ++j) {
         const int jb = j * PW;
         const int rem = (pb.L - jb + NB - 1) / NB;               // 16-row tiles from jb
@@ -1349,9 +1358,8 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
     }
     // default: one-buffer one-barrier kernel (backsub4); SBCE_BACKSUB=3 the two-buffer one-barrier
     // kernel, =2 the two-ahead three-barrier kernel, =1 the one-step-prefetch kernel (A/B runs)
-    const char* bsv = getenv("SBCE_BACKSUB");
-    if (pb.L <= 272 && pb.NR <= 4 && !(bsv && (bsv[0] == '1' || bsv[0] == '2' || bsv[0] == '3')) &&
-        !(skip & 16)) {
+    const int bsv = g_debug.backsub;
+    if (pb.L <= 272 && pb.NR <= 4 && bsv == 0 && !(skip & 16)) {
         switch (pb.NR) {
             case 1: hipLaunchKernelGGL(backsub4_kernel<1>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
             case 2: hipLaunchKernelGGL(backsub4_kernel<2>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
@@ -1360,7 +1368,7 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
         }
         return hipGetLastError();
     }
-    if (pb.L <= 272 && pb.NR <= 4 && bsv && bsv[0] == '3' && !(skip & 16)) {
+    if (pb.L <= 272 && pb.NR <= 4 && bsv == 3 && !(skip & 16)) {
         switch (pb.NR) {
             case 1: hipLaunchKernelGGL(backsub3_kernel<1>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
             case 2: hipLaunchKernelGGL(backsub3_kernel<2>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
@@ -1369,7 +1377,7 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
         }
         return hipGetLastError();
     }
-    if (pb.L <= 272 && pb.NR <= 4 && !(bsv && bsv[0] == '1') && !(skip & 16)) {
+    if (pb.L <= 272 && pb.NR <= 4 && bsv != 1 && !(skip & 16)) {
         hipLaunchKernelGGL(backsub2_kernel, dim3(pb.B), dim3(256),
                            ((size_t)pb.L * pb.NR + NB * NB) * sizeof(cd), s, a, pb.L, pb.NR);
         return hipGetLastError();
@@ -1404,7 +1412,7 @@ hipError_t launch_mfma_cfg(const Problem& pb, const MstepArgs& a, int nw, int ma
     const int skip = g_chol_skip;                   // diagnostic only (see kernel)
     const dim3 g(pb.B), blk(64 * nw);
     CholGeom geo;
-    geo.ld = pb.L; geo.off = 0; geo.stride = (size_t)pb.L * pb.L; geo.tolp = nullptr;
+    geo.ld = pb.L; geo.off = 0; geo.stride = (size_t)pb.L * pb.L; geo.tolp = nullptr; geo.ext = nullptr;
 #define SBCE_CM(t)                                                                                \
     case t:                                                                                       \
         hipLaunchKernelGGL((chol_mfma_kernel<t, YLDS, NWB, KB>), g, blk, lds, s, a, pb.L, pb.NR,  \
@@ -1441,22 +1449,24 @@ hipError_t chol_debug_clock(unsigned long long* out) {
                                hipMemcpyDeviceToHost);
 }
 void chol_debug_skip(int mask) { g_chol_skip = mask; }
+int chol_debug_skip_mask() { return g_chol_skip; }
 hipError_t chol_debug_clock_reset() {
     static const unsigned long long z[32] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_chol_clk), z, sizeof(z), 0, hipMemcpyHostToDevice);
 }
 
-// L <= kLargeL: one workgroup (or batched panel launches) per trial, grid x = batch.
-// kLargeL < L <= kMaxL: the tiled path launches grid (tiles, batch), so batch <= 65535.
+// Every path launches some grid with the batch in grid y (the tiled large-L and min-norm
+// factorisations, pilot_rhs_kernel, the small-L R build), so batch <= 65535 for every shape.
 bool chol_supported(const Problem& pb) {
-    return pb.L >= 1 && pb.L <= kMaxL && (pb.L <= kLargeL || pb.B <= 65535);
+    return pb.L >= 1 && pb.L <= kMaxL && pb.B <= 65535;
 }
 
 // Factor the w x w diagonal tile at (k0, k0) of every trial's R in place (large-L path).
-hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w, hipStream_t s) {
+hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w, const int32_t* ext,
+                            hipStream_t s) {
     const int ntile = (w + NB - 1) / NB;             // <= 4 -> one 16-row tile per wave
     CholGeom geo;
-    geo.ld = pb.L; geo.off = k0; geo.stride = (size_t)pb.L * pb.L; geo.tolp = a.tol;
+    geo.ld = pb.L; geo.off = k0; geo.stride = (size_t)pb.L * pb.L; geo.tolp = a.tol; geo.ext = ext;
     const size_t lds = (size_t)(NB * (128 + 1) + NB * NB + ntile * NB * NB) * sizeof(cd) +
                        18 * sizeof(double);
     hipLaunchKernelGGL((chol_mfma_kernel<1, false, 4, 128, false>), dim3(pb.B), dim3(64 * ntile),
@@ -1466,15 +1476,15 @@ hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w
 
 hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s) {
     if (!chol_supported(pb)) return hipErrorInvalidValue;
-    const char* impl0 = getenv("SBCE_CHOL_IMPL");
-    if (pb.L > kLargeL && !(impl0 && impl0[0] == 'v' && pb.L <= 1024)) return launch_chol_large(pb, a, s);
+    if (a.solve_mode == SBCE_SOLVE_MINNORM) return launch_minnorm(pb, a, s);
+    const char impl = g_debug.chol_impl;            // 'v' VALU kernel, 'f' fused (A/B runs)
+    if (pb.L > kLargeL && !(impl == 'v' && pb.L <= 1024)) return launch_chol_large(pb, a, s);
     const size_t ybytes = (size_t)pb.L * pb.NR * sizeof(cd);
-    const char* impl = getenv("SBCE_CHOL_IMPL");    // "valu" forces the VALU kernel (A/B runs)
-    const bool force_valu = impl && impl[0] == 'v';
+    const bool force_valu = impl == 'v';
     if (!force_valu && pb.L <= 512) {
         // default: batched panel launches; SBCE_CHOL_IMPL=fused keeps the one-workgroup-per-
         // trial kernel (A/B runs)
-        if (!(impl && impl[0] == 'f')) return launch_chol_batched(pb, a, s);
+        if (impl != 'f') return launch_chol_batched(pb, a, s);
         if (ybytes <= 24 * 1024) return launch_mfma<true>(pb, a, ybytes, s);
         return launch_mfma<false>(pb, a, ybytes, s);
     }

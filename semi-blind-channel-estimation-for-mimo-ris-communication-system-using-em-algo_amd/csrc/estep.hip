@@ -2030,10 +2030,8 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     const int steps = (2 * pb.NR + 3) / 4;
     c.nkt_pad = (int)((JB / 16 + 1) / 2 * 2);
 
-    const char* pr = getenv("SBCE_ESTEP_PRUNE");
-    c.prune = !(pr && pr[0] == '0');
-    const char* cnt = getenv("SBCE_ESTEP_COUNT");
-    c.count = cnt && cnt[0] == '1';
+    c.prune = !g_debug.estep_noprune;
+    c.count = g_debug.estep_count;
     c.inv_s2 = 1.0 / (pb.varn * pb.varn);
     c.thr_d = kSkipThr * pb.varn * pb.varn;
     c.reg = 0.1 * pb.varn * pb.varn;
@@ -2043,11 +2041,8 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     c.prep_stride = c.rowb_off + (pb.NT == 4 ? 6 * pb.NR : 0);
     c.rec_words = c.prep_stride + 2 * pb.NR;
     c.tab_d = mfma_tab_d(NO, c.chunk, steps, pb.M, c.nkt_pad, c.rec_words);
-    const char* sw = getenv("SBCE_ESTEP_SPW");           // symbols per wave (A/B runs)
-    c.spw = sw ? atoi(sw) : 4;
-    if (c.spw < 1) c.spw = 1;
-    const char* rb = getenv("SBCE_ESTEP_ROWB");          // "0": off (A/B runs)
-    c.rowb = pb.NT == 4 && c.prune && !(rb && rb[0] == '0');
+    c.spw = g_debug.estep_spw;                           // symbols per wave (A/B runs)
+    c.rowb = pb.NT == 4 && c.prune && !g_debug.estep_norowb;
     lds = 64 * sizeof(cd) + (size_t)kMfmaWaves * c.tab_d * sizeof(double);
     const long nsym = (long)pb.B * pb.Td;
     const long per_block = (long)kMfmaWaves * c.spw;
@@ -2064,9 +2059,8 @@ hipError_t dispatch_mfma_mode(const MfmaConst& c, size_t lds, long blocks, const
         if (c.JA != 256 || c.JB != 256 || c.chunk != 256 || c.nkt_pad != 16 ||
             c.prep_stride != 4 + 2 * NT * NR + 16 + 6 * NR)
             return hipErrorInvalidValue;
-        const char* occ = getenv("SBCE_ESTEP_OCC");   // "2": no VGPR cap (A/B runs)
         if constexpr (NR <= 4) {
-            if (!(occ && occ[0] == '2')) {
+            if (!g_debug.estep_occ2) {                // SBCE_ESTEP_OCC=2: no VGPR cap (A/B)
                 if (mode == SBCE_ESTEP_HARD)
                     hipLaunchKernelGGL((estep_mfma_kernel_occ3<NT, NR, SBCE_ESTEP_HARD, 4, true>),
                                        dim3((unsigned)blocks), dim3(64 * kMfmaWaves), lds, s, a, c);
@@ -2226,8 +2220,7 @@ bool estep_supported(const Problem& pb, int mode) {
 
 hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStream_t s) {
     if (mode >= SBCE_ESTEP_PM && mode <= SBCE_ESTEP_GAUSS) return launch_estep_pm(pb, a, mode, pb.pr, s);
-    const char* impl = getenv("SBCE_ESTEP_IMPL");   // "valu" forces the VALU kernel (A/B runs)
-    const bool force_valu = impl && impl[0] == 'v';
+    const bool force_valu = g_debug.estep_valu;     // VALU kernel (A/B runs)
     MfmaConst mc;
     size_t mlds;
     long mblocks;
@@ -2238,14 +2231,11 @@ hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStre
             PrepConst pc;
             pc.B = pb.B; pc.Td = pb.Td; pc.P = pb.P; pc.M = pb.M; pc.lm = mc.lm;
             pc.nkt = mc.JB >> 4; pc.stride = mc.prep_stride; pc.reg = mc.reg;
-            const char* un = getenv("SBCE_PREP_UNI");
-            pc.uni = !(un && un[0] == '0');
+            pc.uni = !g_debug.prep_nouni;
             // sphere pass instead of the preparation pass (SBCE_ESTEP_SPHERE=0 disables: A/B);
             // n_rx < n_tx (singular H^H H) always leaves the symbol to the sweep: not compiled
-            const char* sp = getenv("SBCE_ESTEP_SPHERE");
-            const bool sphere = a.list && a.tree && pb.NR >= pb.NT && !(sp && sp[0] == '0');
-            const char* bu = getenv("SBCE_SPHERE_BUDGET");      // path list cap per level
-            pc.budget = bu ? atoi(bu) : 128;
+            const bool sphere = a.list && a.tree && pb.NR >= pb.NT && !g_debug.estep_nosphere;
+            pc.budget = g_debug.sphere_budget;                  // path list cap per level
             pc.count = mc.count;
             pc.inv_s2 = mc.inv_s2;
             pc.thr_d = mc.thr_d;
@@ -2256,8 +2246,8 @@ hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStre
             hipError_t e = hipErrorInvalidValue;
             if (sphere) {
                 // sphere pass (tree records, enumeration), then the tile bounds of the listed
-                if (hipMemsetAsync(a.list + nsym, 0, 3 * sizeof(int32_t), s) != hipSuccess)
-                    return hipGetLastError();
+                const hipError_t me = hipMemsetAsync(a.list + nsym, 0, 3 * sizeof(int32_t), s);
+                if (me != hipSuccess) return me;
                 const long nbfs = (nsym + kBfsSpw * kBfsWaves - 1) / (kBfsSpw * kBfsWaves);
                 const dim3 bg((unsigned)nbfs), bblk(64 * kBfsWaves);
                 const bool hard = mode == SBCE_ESTEP_HARD;

@@ -371,9 +371,11 @@ __global__ __launch_bounds__(256) void diag_tol_kernel(MstepArgs a, int L) {
 // ---------------------------------------------------------------- W = L_kk^{-1}
 // One wave per trial: lane j forward-substitutes column j of the inverse of the factored
 // w x w diagonal tile (uniform loads of L, column in LDS).  Dropped pivots (0) give 0.
-__global__ __launch_bounds__(64) void tile_inverse_kernel(MstepArgs a, int L, int k0, int w, int NR) {
+__global__ __launch_bounds__(64) void tile_inverse_kernel(MstepArgs a, int L, int k0, int w, int NR,
+                                                         TileExt ext) {
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
+    if (ext.col && k0 >= ext.col[b]) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     cd(*col)[TB] = reinterpret_cast<cd(*)[TB]>(smem);       // [TB][TB], 64 KB
     const cd* Lk = a.R + (size_t)b * L * L + (size_t)k0 * L + k0;
@@ -387,6 +389,7 @@ __global__ __launch_bounds__(64) void tile_inverse_kernel(MstepArgs a, int L, in
     }
     cd* W = a.winv + (size_t)b * TB * TB;
     for (int r = 0; r < TB; ++r) W[r * TB + j] = (r < w && j < w) ? col[r][j] : czero();
+    if (!ext.fwd) return;
     // fused forward substitution: y_k <- W y_k (every earlier block's L_ik y_i has been
     // subtracted by that block's TRSM launch); lane j owns row j
     cd* yk = a.rhs + ((size_t)b * L + k0) * NR;
@@ -408,10 +411,11 @@ __global__ __launch_bounds__(64) void tile_inverse_kernel(MstepArgs a, int L, in
 //   HERK (HERK = true):  tile (i, j), C = A_ij - L_ik L_jk^H.
 // 4 waves, wave w owns the 32 x 32 quadrant (w >> 1, w & 1) = 2 x 2 MFMA tiles.
 template <bool HERK>
-__global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int kb, int NR) {
+__global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int kb, int NR, TileExt ext) {
     __shared__ cd As[TB][KS + 1], Bs[TB][KS + 1];
     const int b = blockIdx.y;
     if (a.done && a.done[b]) return;
+    if (ext.col && kb * TB >= ext.col[b]) return;
     int ti, tj;
     if (HERK) {
         const int tix = blockIdx.x;
@@ -424,6 +428,7 @@ __global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int 
         ti = kb + 1 + blockIdx.x;
         tj = kb;
     }
+    if (ext.row && ti * TB >= ext.row[b]) return;
     cd* R = a.R + (size_t)b * L * L;
     const int r0 = ti * TB, c0 = tj * TB, k0 = kb * TB;
     const cd* Arow = R + (size_t)r0 * L + k0;                          // A[r][k]
@@ -509,7 +514,7 @@ __global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int 
                 if (r < L && c < L && (HERK || c < k0 + kmax))
                     R[(size_t)r * L + c] = cmk(cre[u][v][q], cim[u][v][q]);
             }
-    if (!HERK) {
+    if (!HERK && ext.fwd) {
         // fused forward substitution: rows r0.. of y -= L_ik y_k (the tile just written)
         __syncthreads();
         cd* y = a.rhs + (size_t)b * L * NR;
@@ -530,9 +535,11 @@ __global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int 
 // in R's strict upper 16 x 16 blocks (Di[c][c] = 1 / L[c][c], Di[c2][c] = conj(R[c][c2])),
 // y_k already holding y_k - sum_{i > k} L_ik^H x_i; backupd_kernel then subtracts
 // L_kj^H x_k from every earlier block j in parallel.  theta = conj(x) after the first block.
-__global__ __launch_bounds__(256) void backdiag_kernel(MstepArgs a, int L, int NR, int k0, int w) {
+__global__ __launch_bounds__(256) void backdiag_kernel(MstepArgs a, int L, int NR, int k0, int w,
+                                                       const int32_t* ext) {
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
+    if (ext && k0 >= ext[b]) return;
     __shared__ cd z[16][8];
     __shared__ cd Dl[16][17];
     const cd* R = a.R + (size_t)b * L * L;
@@ -586,7 +593,7 @@ __global__ __launch_bounds__(256) void backdiag_kernel(MstepArgs a, int L, int N
         }
         __syncthreads();
     }
-    if (k0 == 0) {
+    if (k0 == 0 && a.theta) {
         cd* th = a.theta + (size_t)b * L * NR;
         for (int e = tid; e < L * NR; e += 256) th[e] = cconj(y[e]);
     }
@@ -594,9 +601,11 @@ __global__ __launch_bounds__(256) void backdiag_kernel(MstepArgs a, int L, int N
 
 // Block (j, trial): y_j -= L_kj^H x_k for row block j < k: the tile (k, j) and x_k staged in
 // LDS (coalesced rows), thread per (row r of y_j, right-hand side).
-__global__ __launch_bounds__(256) void backupd_kernel(MstepArgs a, int L, int NR, int k0, int w) {
+__global__ __launch_bounds__(256) void backupd_kernel(MstepArgs a, int L, int NR, int k0, int w,
+                                                      const int32_t* ext) {
     const int j = blockIdx.x, b = blockIdx.y;
     if (a.done && a.done[b]) return;
+    if (ext && k0 >= ext[b]) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     cd(*T)[TB + 1] = reinterpret_cast<cd(*)[TB + 1]>(smem);  // [TB][TB + 1]: T[m][r] = L[k0+m][j0+r]
     cd* xs = reinterpret_cast<cd*>(smem + (size_t)TB * (TB + 1) * sizeof(cd));   // [TB][NR]
@@ -655,8 +664,7 @@ hipError_t launch_rbuild_herm(const Problem& pb, const MstepArgs& a, hipStream_t
         // 16-symbol chunks (19 KB of LDS per block: more resident blocks per CU); measured
         // at cfg1 against 8 / 32 / 64 and 2 / 6 / 8 tiles per wave: 16 x 4 and 16 x 6 lead by
         // ~2 % of the M-step.  SBCE_RB_TC=32: the previous 32-symbol chunks (A/B runs)
-        const char* tc = getenv("SBCE_RB_TC");
-        if (smax <= 68 && !(tc && tc[0] == '3')) return launch_herm<4, 4, 16, 68>(pb, a, smax, s);
+        if (smax <= 68 && !g_debug.rb_tc32) return launch_herm<4, 4, 16, 68>(pb, a, smax, s);
         if (smax <= 68) return launch_herm<4, 4, 32, 68>(pb, a, smax, s);
         return smax <= 130 ? launch_herm<4, 4, 32, 0>(pb, a, smax, s)
                            : launch_herm<4, 4, 8, 0>(pb, a, smax, s);
@@ -673,36 +681,49 @@ hipError_t launch_diag_tol(const Problem& pb, const MstepArgs& a, hipStream_t s)
     return hipGetLastError();
 }
 
+hipError_t launch_tile_factor_step(const Problem& pb, const MstepArgs& a, int k, const TileExt& ex,
+                                   hipStream_t s) {
+    const int nb = (pb.L + TB - 1) / TB;
+    const int k0 = k * TB, w = (pb.L - k0) < TB ? (pb.L - k0) : TB;
+    hipError_t e = launch_chol_tile(pb, a, k0, w, ex.col, s);
+    if (e != hipSuccess) return e;
+    // W = L_kk^-1 (and the fused forward substitution y_k <- W y_k when ex.fwd)
+    const size_t inv_lds = (size_t)TB * TB * sizeof(cd) + (size_t)TB * 8 * sizeof(cd);
+    hipLaunchKernelGGL(tile_inverse_kernel, dim3(pb.B), dim3(64), inv_lds, s, a, pb.L, k0, w, pb.NR, ex);
+    const int below = nb - k - 1;
+    if (below > 0) {
+        hipLaunchKernelGGL(tile_gemm_kernel<false>, dim3(below, pb.B), dim3(256), 0, s, a, pb.L, k,
+                           pb.NR, ex);
+        hipLaunchKernelGGL(tile_gemm_kernel<true>, dim3(below * (below + 1) / 2, pb.B), dim3(256),
+                           0, s, a, pb.L, k, pb.NR, ex);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_back(const Problem& pb, const MstepArgs& a, const int32_t* ext, hipStream_t s) {
+    const int nb = (pb.L + TB - 1) / TB;
+    const size_t upd_lds = (size_t)TB * (TB + 1) * sizeof(cd) + (size_t)TB * 8 * sizeof(cd);
+    hipError_t e;
+    for (int k = nb - 1; k >= 0; --k) {
+        const int k0 = k * TB, w = (pb.L - k0) < TB ? (pb.L - k0) : TB;
+        hipLaunchKernelGGL(backdiag_kernel, dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR, k0, w, ext);
+        if (k > 0)
+            hipLaunchKernelGGL(backupd_kernel, dim3(k, pb.B), dim3(256), upd_lds, s, a, pb.L, pb.NR,
+                               k0, w, ext);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 hipError_t launch_chol_large(const Problem& pb, const MstepArgs& a, hipStream_t s) {
     if (pb.NR > 8) return hipErrorInvalidValue;
     hipError_t e = launch_diag_tol(pb, a, s);
     if (e != hipSuccess) return e;
     const int nb = (pb.L + TB - 1) / TB;
-    const size_t inv_lds = (size_t)TB * TB * sizeof(cd) + (size_t)TB * 8 * sizeof(cd);
-    for (int k = 0; k < nb; ++k) {
-        const int k0 = k * TB, w = (pb.L - k0) < TB ? (pb.L - k0) : TB;
-        if ((e = launch_chol_tile(pb, a, k0, w, s)) != hipSuccess) return e;
-        // W = L_kk^-1 and the fused forward substitution y_k <- W y_k
-        hipLaunchKernelGGL(tile_inverse_kernel, dim3(pb.B), dim3(64), inv_lds, s, a, pb.L, k0, w,
-                           pb.NR);
-        const int below = nb - k - 1;
-        if (below == 0) break;
-        hipLaunchKernelGGL(tile_gemm_kernel<false>, dim3(below, pb.B), dim3(256), 0, s, a, pb.L, k,
-                           pb.NR);
-        hipLaunchKernelGGL(tile_gemm_kernel<true>, dim3(below * (below + 1) / 2, pb.B), dim3(256),
-                           0, s, a, pb.L, k, pb.NR);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
-    const size_t upd_lds = (size_t)TB * (TB + 1) * sizeof(cd) + (size_t)TB * 8 * sizeof(cd);
-    for (int k = nb - 1; k >= 0; --k) {
-        const int k0 = k * TB, w = (pb.L - k0) < TB ? (pb.L - k0) : TB;
-        hipLaunchKernelGGL(backdiag_kernel, dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR, k0, w);
-        if (k > 0)
-            hipLaunchKernelGGL(backupd_kernel, dim3(k, pb.B), dim3(256), upd_lds, s, a, pb.L, pb.NR,
-                               k0, w);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
-    return hipGetLastError();
+    const TileExt full{nullptr, nullptr, 1};
+    for (int k = 0; k < nb; ++k)
+        if ((e = launch_tile_factor_step(pb, a, k, full, s)) != hipSuccess) return e;
+    return launch_tile_back(pb, a, nullptr, s);
 }
 
 }  // namespace sbce

@@ -102,6 +102,30 @@ __device__ __forceinline__ double fast_rsqrt(double x) {
 }
 
 
+// ------------------------------------------------------------------ debug configuration
+// A/B switches of the development runs (SBCE_* environment variables), read ONCE when the
+// library is loaded (api.hip) and again only through sbce_debug_reload_env(): production
+// launches never consult the environment.  Any result-affecting non-default value makes
+// sbce_em / sbce_mstep / sbce_estep mark every trial SBCE_STATUS_DEBUG.
+struct DebugConfig {
+    bool estep_valu;     // SBCE_ESTEP_IMPL=valu   VALU E-step instead of the MFMA sweep
+    bool estep_noprune;  // SBCE_ESTEP_PRUNE=0     no column-tile bounds
+    bool estep_count;    // SBCE_ESTEP_COUNT=1     device counters (results unchanged)
+    int estep_spw;       // SBCE_ESTEP_SPW         symbols per sweep wave (default 4)
+    bool estep_norowb;   // SBCE_ESTEP_ROWB=0      no row-tile bounds
+    bool estep_occ2;     // SBCE_ESTEP_OCC=2       sweep without the VGPR cap
+    bool prep_nouni;     // SBCE_PREP_UNI=0
+    bool estep_nosphere; // SBCE_ESTEP_SPHERE=0    tile sweep only
+    int sphere_budget;   // SBCE_SPHERE_BUDGET     path list cap per level (default 128)
+    char rhs_impl;       // SBCE_RHS_IMPL          0 default, 'r' thread-per-row, 'l' LDS
+    bool rb_tc32;        // SBCE_RB_TC=32          32-symbol R-build chunks
+    bool upd_waves8;     // SBCE_UPD_WAVES=8       eight-tile panel-update blocks
+    int backsub;         // SBCE_BACKSUB           0 default, 1..3 older back substitutions
+    char chol_impl;      // SBCE_CHOL_IMPL         0 default, 'v' VALU, 'f' fused one-workgroup
+};
+extern DebugConfig g_debug;
+bool debug_nondefault();   // a result-affecting switch differs from its default
+
 // ------------------------------------------------------------------ launch API
 struct Problem {
     int B, NT, NR, P, Tp, Td, M, L, K;
@@ -148,9 +172,23 @@ struct MstepArgs {
     cd* prhs;          // [B][L][NR] pilot part of B^H, sum_p u_p y_p (set by pilot_factor; null:
                        // not kept, the B^H kernel sums the pilots itself)
     const int32_t* gate;  // VALU build: only trials with gate[b] != 0 (null: all trials)
-    // large-L path (L > 512) workspace
+    // tiled factorisation workspace (L > 512, and the min-norm solve at every L)
     double* tol;       // [B]     pivot threshold
     cd* winv;          // [B][64][64] inverse of the current diagonal tile
+    // min-norm solve (SBCE_SOLVE_MINNORM, minnorm.hip) workspace
+    cd* gram;          // [B][L][L]  C = G^H G of the rank-cut factor G (lower triangle)
+    cd* grhs;          // [B][L][NR] G^H B^H, then the solves with C in place
+    int32_t* act;      // [B]  active extent: columns of G past act[b] are all dropped
+    double* tol2;      // [B]  pivot threshold of C's Cholesky
+};
+
+// Per-trial extents of one tiled-factorisation launch sequence (mstep_large.hip): column
+// blocks at or past col[b] and row tiles at or past row[b] are skipped (null: L); fwd = 0
+// leaves the right-hand side untouched (no fused forward substitution).
+struct TileExt {
+    const int32_t* col;
+    const int32_t* row;
+    int fwd;
 };
 
 hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStream_t s);
@@ -171,10 +209,20 @@ hipError_t launch_pilot_factor(const Problem& pb, const MstepArgs& a, hipStream_
 hipError_t launch_rbuild_herm(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_chol_large(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_diag_tol(const Problem& pb, const MstepArgs& a, hipStream_t s);  // a.tol[b]
-hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w, hipStream_t s);
+hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w, const int32_t* ext,
+                            hipStream_t s);
+// one column block k of the tiled right-looking factorisation: diagonal tile, its inverse,
+// the TRSM tiles below it and the trailing HERK update
+hipError_t launch_tile_factor_step(const Problem& pb, const MstepArgs& a, int k, const TileExt& e,
+                                   hipStream_t s);
+// L^H x = y on a.rhs by 64-column blocks (theta = conj(x) written when a.theta != null)
+hipError_t launch_tile_back(const Problem& pb, const MstepArgs& a, const int32_t* ext, hipStream_t s);
+// minimum-norm solve (SBCE_SOLVE_MINNORM, minnorm.hip): R, rhs built; writes theta
+hipError_t launch_minnorm(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t chol_debug_clock(unsigned long long* out);   // diagnostic (SBCE_CHOL_SKIP & 64)
 hipError_t chol_debug_clock_reset();
 void chol_debug_skip(int mask);   // diagnostic phase-skip mask (results flagged SBCE_STATUS_DEBUG)
+int chol_debug_skip_mask();       // the current mask (process-wide, every stream)
 hipError_t launch_decisions(const Problem& pb, const cd* mom, cd* xdest, hipStream_t s);
 hipError_t launch_sup_shift_y(const Problem& pb, const cd* yd, const cd* psid, const cd* theta,
                               const cd* xsup, cd* yout, const int32_t* done, hipStream_t s);

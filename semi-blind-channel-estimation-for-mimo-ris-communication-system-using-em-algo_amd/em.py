@@ -32,9 +32,14 @@ variance varn.  The reference's per-iteration ``print(norm(theta))`` is
 available with ``verbose=True``.  Near-singular normal equations do not raise
 (``np.linalg.solve`` only raises on an exactly zero LU pivot, which float
 rounding essentially never produces): the device Cholesky clamps the pivot and
-flags the trial (``last_status``); ``solve='drop'`` instead drops non-HPD
-directions (the lstsq-like policy of PM.py:108).
+flags the trial (``last_status``).  ``solve='lstsq'`` is np.linalg.lstsq of PM.py:108
+(the minimum-norm solution with lstsq's default singular-value cut, include/sbce.h
+SBCE_SOLVE_MINNORM): the reference's policy for rank-deficient normal equations and
+the intended fallback of all_detectorsvsTd.py:238-241.  ``solve='drop'`` drops non-HPD
+pivots (a basic, not minimum-norm, solution; kept for A/B comparisons).
 """
+import ctypes
+
 import numpy as np
 
 from . import _lib
@@ -56,7 +61,8 @@ def _dev(torch, arr, dtype=None):
 _MODES = {"soft": _lib.SBCE_ESTEP_SOFT, "hard": _lib.SBCE_ESTEP_HARD, "pm": _lib.SBCE_ESTEP_PM,
           "pm_soft": _lib.SBCE_ESTEP_PM_SOFT, "zf": _lib.SBCE_ESTEP_ZF,
           "mmse": _lib.SBCE_ESTEP_MMSE, "gauss": _lib.SBCE_ESTEP_GAUSS}
-_SOLVES = {"chol": _lib.SBCE_SOLVE_CHOL, "drop": _lib.SBCE_SOLVE_CHOL_DROP}
+_SOLVES = {"chol": _lib.SBCE_SOLVE_CHOL, "drop": _lib.SBCE_SOLVE_CHOL_DROP,
+           "lstsq": _lib.SBCE_SOLVE_MINNORM}
 
 
 def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_true=None,
@@ -242,7 +248,7 @@ def _pm(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, aps, M, varn, itera, h_initial, h,
 
 
 def em_pm(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera, h_initial, h,
-          n_tx, partition_r, X_d, qamCons, verbose=False, solve="drop"):
+          n_tx, partition_r, X_d, qamCons, verbose=False, solve="lstsq"):
     """Partitioned list-detector EM, every list member weight 1 (PMd/PM.py:47-116).
 
     The list of M**(p+1) candidates (p = int(partition_r / log2 M)) is built per
@@ -252,8 +258,8 @@ def em_pm(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, it
     ``h`` drives the reference's oracle early stop (PM.py:110-112) when given;
     ``X_d`` is accepted for signature parity (the reference only reads its
     length).  ``all_possibleSymbols`` may be None (n_tx = 8 makes it 4.3e9 rows).
-    The reference solves with lstsq (PM.py:108); solve='drop' is its device
-    counterpart (identical on HPD systems)."""
+    The reference solves with lstsq (PM.py:108): solve='lstsq' (default) is its device
+    counterpart, the minimum-norm solution with lstsq's singular-value cut."""
     return _pm(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera,
                h_initial, h, n_tx, partition_r, qamCons, "pm", solve, verbose)
 
@@ -593,6 +599,15 @@ class EMEngine:
         rc = self.lib.sbce_mstep(self.dims, self.ptrs, self.mom.data_ptr(), self.solve, None,
                                  None, self.torch.cuda.current_stream().cuda_stream)
         _lib.check(rc, "sbce_mstep")
+
+    def mstep_phase(self, phase):
+        """One piece of the M-step from the last moments (kernel timing, sbce_debug_mstep_phase):
+        0 pilot factorisation, 1 the R build kernel alone, 2 R and B^H."""
+        fn = self.lib.sbce_debug_mstep_phase
+        fn.restype = ctypes.c_int
+        rc = fn(ctypes.byref(self.dims), ctypes.byref(self.ptrs), ctypes.c_void_p(self.mom.data_ptr()),
+                int(phase), ctypes.c_void_p(self.torch.cuda.current_stream().cuda_stream))
+        _lib.check(rc, "sbce_debug_mstep_phase")
 
     def nmse(self):
         """Per-trial NMSE of the current theta against h (device, sbce_nmse)."""

@@ -208,7 +208,7 @@ def test_singular_system_flags_and_drop_mode(sbce):
                                    # n_tx = 4, 16-QAM with row-tile bounds: 8 receive antennas,
                                    # and 2 (span(h1, h3) is all of C^2: the bounds are 0)
                                    (4, 8, 6, 16, 8, 16, 25), (4, 2, 6, 16, 8, 16, 30)])
-def test_mfma_and_valu_estep_agree(sbce, shape, monkeypatch):
+def test_mfma_and_valu_estep_agree(sbce, shape):
     """The FP64-MFMA E-step (with its preparation pass, with in-kernel preparation, with
     the exact tile bounds disabled, with and without the preparation pass's sphere
     enumeration at several step budgets) and the VALU E-step compute the same posterior
@@ -223,14 +223,12 @@ def test_mfma_and_valu_estep_agree(sbce, shape, monkeypatch):
                                       ("mfma", True, "0", "0", "48"), ("mfma", True, "1", "0", "48"),
                                       ("mfma", True, "1", "1", "1"), ("mfma", True, "1", "1", "6"),
                                       ("valu", True, "1", "1", "48")):
-        monkeypatch.setenv("SBCE_ESTEP_IMPL", impl)
-        monkeypatch.setenv("SBCE_ESTEP_PRUNE", prune)
-        monkeypatch.setenv("SBCE_ESTEP_SPHERE", sph)
-        monkeypatch.setenv("SBCE_SPHERE_BUDGET", bud)
-        out[(impl, ws, prune, sph, bud)] = [
-            sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx, m,
-                             workspace=ws)
-            for m in ("soft", "hard")]
+        with sbce._lib.debug_env(SBCE_ESTEP_IMPL=impl, SBCE_ESTEP_PRUNE=prune,
+                                 SBCE_ESTEP_SPHERE=sph, SBCE_SPHERE_BUDGET=bud):
+            out[(impl, ws, prune, sph, bud)] = [
+                sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx, m,
+                                 workspace=ws)
+                for m in ("soft", "hard")]
     scale = np.abs(b["cons"]).max() ** 2
     ref = out[("valu", True, "1", "1", "48")]
     for key, res in out.items():
@@ -242,7 +240,7 @@ def test_mfma_and_valu_estep_agree(sbce, shape, monkeypatch):
 
 
 @pytest.mark.parametrize("snr", [25, 20, 10, 0])
-def test_sphere_estep_cfg1_geometry(sbce, snr, monkeypatch):
+def test_sphere_estep_cfg1_geometry(sbce, snr):
     """BASELINE cfg-1 geometry (n_tx = n_rx = 4, N_RIS = 64, 16-QAM): the preparation pass's
     sphere enumeration (default) against the tile sweep alone (SBCE_ESTEP_SPHERE=0), soft
     moments and hard decisions, at theta_0 and near the true channel; at 20 dB and above the
@@ -255,13 +253,12 @@ def test_sphere_estep_cfg1_geometry(sbce, snr, monkeypatch):
     for th in (b["theta0"], b["h"] + 0.05 * b["theta0"] / np.abs(b["theta0"]).max()):
         res = {}
         for sph in ("1", "0"):
-            monkeypatch.setenv("SBCE_ESTEP_SPHERE", sph)
-            monkeypatch.setenv("SBCE_ESTEP_COUNT", "1")
-            lib.sbce_debug_estep_sphere(None, 1)
-            res[sph] = [sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], th, varn, 4, m)
-                        for m in ("soft", "hard")]
-            cnt = (ctypes.c_ulonglong * 3)()
-            lib.sbce_debug_estep_sphere(cnt, 0)
+            with sbce._lib.debug_env(SBCE_ESTEP_SPHERE=sph, SBCE_ESTEP_COUNT="1"):
+                lib.sbce_debug_estep_sphere(None, 1)
+                res[sph] = [sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], th, varn, 4, m)
+                            for m in ("soft", "hard")]
+                cnt = (ctypes.c_ulonglong * 3)()
+                lib.sbce_debug_estep_sphere(cnt, 0)
             if sph == "1":
                 # [enumerated, left to the sweep, single surviving path]
                 resolved, listed = cnt[0] + cnt[2], cnt[1]
@@ -395,7 +392,7 @@ def test_pm_soft_full_em_cfg2_geometry_vs_oracle(sbce):
     (4, 8, 127, 16, 200),     # L = 512: largest MFMA Cholesky shape, 8 RHS
     (1, 1, 40, 8, 80),        # L = 41, single RHS
 ])
-def test_mfma_and_valu_cholesky_agree(sbce, shape, monkeypatch):
+def test_mfma_and_valu_cholesky_agree(sbce, shape):
     """The batched-panel MFMA, the fused MFMA and the VALU blocked Cholesky solve the same
     normal equations, and all match numpy.linalg.solve of the R, rhs the device built."""
     n_tx, n_rx, N, T_p, T_d = shape
@@ -408,9 +405,10 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape, monkeypatch):
     # "batched_bs1": batched, with the one-step-prefetch back substitution instead of the
     # one-barrier kernel (default for L <= 272, n_rx <= 4), two-ahead three-barrier kernel
     for impl in ("batched", "fused", "valu", "batched_bs1", "batched_bs2"):
-        monkeypatch.setenv("SBCE_CHOL_IMPL", impl.split("_")[0])
-        monkeypatch.setenv("SBCE_BACKSUB", impl[-1] if "_bs" in impl else "0")
-        out[impl] = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], m, S, 0.05)
+        with sbce._lib.debug_env(SBCE_CHOL_IMPL=impl.split("_")[0],
+                                 SBCE_BACKSUB=impl[-1] if "_bs" in impl else "0"):
+            out[impl] = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], m, S,
+                                         0.05)
     th_m, R, rhs, st = out["batched"]
     assert not st.any()
     for i in range(2):
@@ -655,6 +653,29 @@ def test_engine_matches_em_batch_superimposed_and_gauss(sbce):
     eng = sbce.EMEngine(bg, varn, mode="gauss", solve="drop", varx=1.5)
     assert eng.P == P
     assert np.array_equal(eng.run(2).cpu().numpy(), ref["theta"])
+
+
+def test_debug_switches_are_read_once_and_flag_status(sbce):
+    """Production launches never consult the environment: an SBCE_* switch set after the
+    library loaded changes nothing until sbce_debug_reload_env(), and while a
+    result-affecting switch is active every trial carries SBCE_STATUS_DEBUG."""
+    import os
+    b = sbce.signal_model.synthetic_batch(2, 2, 2, 6, 8, 20, 16, 0.2, seed=3)
+    args = (b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], 0.2, 2, b["theta0"])
+    r0 = sbce.em_batch(*args)
+    assert not (r0["status"] & sbce._lib.SBCE_STATUS_DEBUG).any()
+    os.environ["SBCE_CHOL_IMPL"] = "valu"
+    try:
+        r1 = sbce.em_batch(*args)                 # not reloaded: default kernels, no flag
+        assert np.array_equal(r1["theta"], r0["theta"]) and not r1["status"].any()
+    finally:
+        del os.environ["SBCE_CHOL_IMPL"]
+    with sbce._lib.debug_env(SBCE_CHOL_IMPL="valu"):
+        r2 = sbce.em_batch(*args)
+    assert (r2["status"] & sbce._lib.SBCE_STATUS_DEBUG).all()
+    assert rel(r2["theta"], r0["theta"]) < 1e-9
+    r3 = sbce.em_batch(*args)
+    assert np.array_equal(r3["theta"], r0["theta"]) and not r3["status"].any()
 
 
 def test_debug_skip_mask_flags_every_trial(sbce):

@@ -187,6 +187,46 @@ def test_reduced_normal_equations_equal_kronecker_form():
     assert rel(mstep_solve(R, rhs), np.linalg.solve(A, bvec)) < 1e-10
 
 
+def test_reduced_lstsq_equals_kronecker_form_lstsq(sbce):
+    """PM.py:108 runs np.linalg.lstsq on the K x K sums; on a rank-deficient system
+    (L = 66 > T_p + T_d = 32, weight-1 hypotheses) the reduced-form restatement with
+    rcond = eps * K returns the same minimum-norm theta and rank (n_rx copies)."""
+    from oracle.em_reduced import mstep_lstsq
+    n_tx, n_rx, N, T_p, T_d = 2, 2, 32, 12, 20
+    b = sbce.signal_model.synthetic_batch(1, n_tx, n_rx, N, T_p, T_d, 4, 0.05, seed=21)
+    Psi, x = b["psi_d"][0].T, b["x_d"][0]
+    S = x[:, :, None] * np.conj(x[:, None, :])
+    R, rhs = mstep_build(b["u_p"][0], b["y_p"][0], Psi, b["y_d"][0], x, S)
+    K = R.shape[0] * n_rx
+    A = np.zeros((K, K), complex)
+    bvec = np.zeros((K, 1), complex)
+    for t in range(T_d):
+        Z = np.kron(np.kron(Psi[:, t][None], x[t][None]), np.eye(n_rx))
+        A += np.conj(Z).T @ Z
+        bvec += np.conj(Z).T @ b["y_d"][0][t][:, None]
+    for t in range(T_p):
+        Z = np.kron(b["u_p"][0][t][None], np.eye(n_rx))
+        A += np.conj(Z).T @ Z
+        bvec += np.conj(Z).T @ b["y_p"][0][t][:, None]
+    th_ref, _, rank_ref, _ = np.linalg.lstsq(A, bvec)      # the reference call, default rcond
+    th, rank = mstep_lstsq(R, rhs)
+    assert rank_ref == n_rx * rank and rank <= T_p + T_d
+    assert rel(th, th_ref) < 1e-10
+
+
+def test_gemm_build_equals_einsum_build(sbce):
+    from oracle.em_reduced import mstep_build_gemm
+    b = sbce.signal_model.synthetic_batch(1, 3, 2, 7, 5, 30, 16, 0.1, seed=2)
+    rng = np.random.default_rng(0)
+    m = rng.standard_normal((30, 3)) + 1j * rng.standard_normal((30, 3))
+    C = rng.standard_normal((30, 3, 3)) + 1j * rng.standard_normal((30, 3, 3))
+    S = C @ np.conj(np.swapaxes(C, 1, 2))
+    args = (b["u_p"][0], b["y_p"][0], b["psi_d"][0].T, b["y_d"][0], m, S)
+    R0, r0 = mstep_build(*args)
+    R1, r1 = mstep_build_gemm(*args)
+    assert rel(R1, R0) < 1e-13 and rel(r1, r0) < 1e-13
+
+
 def _fexp_neg_numpy(z):
     """Bit-level numpy mirror of csrc/sbce_internal.h fexp_neg (Cody-Waite + degree-12)."""
     z = np.maximum(z, -745.5)

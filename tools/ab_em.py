@@ -18,6 +18,7 @@ for rnd in range(3):
     for arm in sys.argv[1:]:
         k, v = arm.split("=", 1)
         os.environ[k] = v
+        pkg._lib.reload_debug_env()   # the library reads SBCE_* switches once
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(2):
@@ -28,3 +29,4 @@ for rnd in range(3):
         print(f"round {rnd} {arm:24s} {dt * 1e3:8.2f} ms/run  {20000 / dt:9.0f} EM-it/s  nmse {nm:.12f}",
               flush=True)
         del os.environ[k]
+        pkg._lib.reload_debug_env()   # the library reads SBCE_* switches once

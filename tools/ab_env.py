@@ -32,12 +32,14 @@ for rnd in range(3):
     for arm in arms:
         k, v = arm.split("=", 1)
         os.environ[k] = v
+        pkg._lib.reload_debug_env()   # the library reads SBCE_* switches once
         t_em = timeit(lambda: eng.run(20), 2)
         th = eng.theta.cpu().numpy()
         eng.estep()
         t_m = timeit(eng.mstep, 5)
         t_e = timeit(eng.estep, 5)
         del os.environ[k]
+        pkg._lib.reload_debug_env()   # the library reads SBCE_* switches once
         if ref is None:
             ref = th
         print(f"round {rnd} {arm:28s} EM {t_em:7.2f} ms ({20000 / t_em * 1e3:9.0f} EM-it/s)  "

@@ -32,6 +32,8 @@ for rnd in range(3):
     for arm in sys.argv[1:]:
         k, v = arm.split("=", 1)
         os.environ[k] = v
+        pkg._lib.reload_debug_env()   # the library reads SBCE_* switches once
         print(f"round {rnd} {arm:28s} mstep {timeit(eng.mstep):.4f} ms  estep {timeit(eng.estep):.4f} ms",
               flush=True)
         del os.environ[k]
+        pkg._lib.reload_debug_env()   # the library reads SBCE_* switches once

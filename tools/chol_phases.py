@@ -33,6 +33,7 @@ def timeit(fn, reps=5):
 
 for impl in sys.argv[1:] or ["batched"]:
     os.environ["SBCE_CHOL_IMPL"] = impl
+    pkg._lib.reload_debug_env()   # the library reads SBCE_* switches once
     for skip in (0, 1, 2, 8, 16, 2 | 8, 1 | 2 | 8 | 16):
         LIB.sbce_debug_chol_skip(skip)
         print(f"chol {impl} skip={skip:2d}: mstep {timeit(eng.mstep):.3f} ms", flush=True)

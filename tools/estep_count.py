@@ -20,10 +20,12 @@ for it in (1, 5, 20):
         k, v = arm.split("=", 1)
         os.environ[k] = v
         os.environ["SBCE_ESTEP_COUNT"] = "1"
+        pkg._lib.reload_debug_env()   # the library reads SBCE_* switches once
         cnt = ctypes.c_ulonglong(0)
         lib.sbce_debug_estep_mfma(None, 1)
         eng.estep()
         torch.cuda.synchronize()
         lib.sbce_debug_estep_mfma(ctypes.byref(cnt), 0)
         del os.environ["SBCE_ESTEP_COUNT"], os.environ[k]
+        pkg._lib.reload_debug_env()   # the library reads SBCE_* switches once
         print(f"after {it:2d} EM its  {arm:24s} {cnt.value / (1000 * 256):8.2f} MFMA/symbol", flush=True)

@@ -33,11 +33,13 @@ def timeit(fn, reps=5):
 
 for impl in ("mfma", "valu"):
     os.environ["SBCE_CHOL_IMPL"] = impl
+    pkg._lib.reload_debug_env()   # the library reads SBCE_* switches once
     for skip in (0, 1, 2, 8, 16, 1 | 2 | 8 | 16):
         LIB.sbce_debug_chol_skip(skip)
         print(f"chol {impl} skip={skip:2d}: mstep {timeit(eng.mstep):.3f} ms", flush=True)
 LIB.sbce_debug_chol_skip(0)
 os.environ["SBCE_CHOL_IMPL"] = "mfma"
+pkg._lib.reload_debug_env()   # the library reads SBCE_* switches once
 
 # per-phase s_memtime sums (block 0, waves 0/1) of one MFMA Cholesky launch
 import ctypes  # noqa: E402

@@ -24,6 +24,7 @@ for it in (0, 1, 5, 20):
         k, v = arm.split("=", 1)
         os.environ[k] = v
         os.environ["SBCE_ESTEP_COUNT"] = "1"
+        pkg._lib.reload_debug_env()   # the library reads SBCE_* switches once
         cnt = ctypes.c_ulonglong(0)
         sph = (ctypes.c_ulonglong * 3)()
         lib.sbce_debug_estep_mfma(None, 1)
@@ -33,6 +34,7 @@ for it in (0, 1, 5, 20):
         lib.sbce_debug_estep_mfma(ctypes.byref(cnt), 0)
         lib.sbce_debug_estep_sphere(sph, 0)
         del os.environ["SBCE_ESTEP_COUNT"]
+        pkg._lib.reload_debug_env()   # the library reads SBCE_* switches once
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         eng.estep()
         e0.record()
@@ -42,6 +44,7 @@ for it in (0, 1, 5, 20):
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / 5
         del os.environ[k]
+        pkg._lib.reload_debug_env()   # the library reads SBCE_* switches once
         print(f"after {it:2d} EM its  {arm:24s} single {sph[2] / nsym:6.3f} enum {sph[0] / nsym:6.3f} "
               f"listed {sph[1] / nsym:6.3f} "
               f"{cnt.value / nsym:7.2f} MFMA/symbol  E-step {ms:7.3f} ms", flush=True)
