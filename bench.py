@@ -193,6 +193,48 @@ def cpu_baseline(cfg, varn, seed, iters=2, mode="soft", part_r=0):
                       f"(NumPy float64, BLAS threads={threads or 'default'}), {dt:.2f} s"}
 
 
+def cpu_baseline_reference_structured(cfg, varn, seed, budget_s=20.0):
+    """the reference's own loop structure (oracle/em_loop.py: dense Kronecker
+    regressor Z_{t,j} per hypothesis, K x K accumulation of every hypothesis, LAPACK solve on the
+    K x K system -- PMd/Proposed_method_NMSEvsTp.py:50-83 in float64 instead of mpmath) timed at
+    the plumbing shape (BASELINE configs[0]: 2x2, N_RIS = 16, T_p = 16, T_d = 50, 4-QAM), then
+    extrapolated to the bench workload with the loop's O(T_d J K^2) cost model."""
+    import importlib
+    from oracle.em_loop import em_loop
+    pkg = importlib.import_module(
+        "semi-blind-channel-estimation-for-mimo-ris-communication-system-using-em-algo_amd")
+    pn_tx, pn_rx, pN, pT_p, pT_d, pM = 2, 2, 16, 16, 50, 4
+    b = pkg.signal_model.synthetic_batch(1, pn_tx, pn_rx, pN, pT_p, pT_d, pM, varn,
+                                         seed=seed + 777)
+    Y_d = [y[:, None] for y in b["y_d"][0]]
+    Y_p = [y[:, None] for y in b["y_p"][0]]
+    Z_p = [np.kron(u[None], np.eye(pn_rx)) for u in b["u_p"][0]]
+    aps = pkg.qam.all_possible_symbols(b["cons"], pn_tx)
+    args = (Y_d, Y_p, pT_d, pT_p, Z_p, b["psi_d"][0].T, aps, pM, varn)
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        em_loop(*args, 1, b["theta0"][0], skip_zero=False)
+        n += 1
+        if time.perf_counter() - t0 > budget_s / 4 or n >= 20:
+            break
+    t_plumb = (time.perf_counter() - t0) / n
+
+    def work(n_tx, n_rx, N, T_d, M):
+        return T_d * float(M) ** n_tx * ((N + 1) * n_tx * n_rx) ** 2
+
+    n_tx, n_rx, N, T_p, T_d, M, _, _ = cfg
+    t_cfg = t_plumb * work(n_tx, n_rx, N, T_d, M) / work(pn_tx, pn_rx, pN, pT_d, pM)
+    threads = os.environ.get("OMP_NUM_THREADS")
+    return {"value": 1.0 / t_cfg, "unit": "EM-iterations/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle/em_loop.py (reference loop structure, float64) at the plumbing "
+                       f"shape 2x2 N_RIS=16 T_p=16 T_d=50 4-QAM: {t_plumb:.3f} s per "
+                       f"trial-iteration ({n} timed); extrapolated by T_d J K^2 "
+                       f"({work(n_tx, n_rx, N, T_d, M) / work(pn_tx, pn_rx, pN, pT_d, pM):.3g}x) "
+                       f"to this workload: {t_cfg:.3g} s per trial-iteration; "
+                       f"BLAS threads={threads or 'default'}")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -426,6 +468,8 @@ def main():
         line["cpu_baseline"] = cpu_baseline(cfg, varn, args.seed,
                                             iters=2 if args.config in ("cfg1", "plumbing") else 1,
                                             mode=mode, part_r=part_r)
+        line["cpu_baseline_reference_structured"] = cpu_baseline_reference_structured(
+            cfg, varn, args.seed)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

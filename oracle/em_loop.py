@@ -32,13 +32,15 @@ def _pilot_terms(Y_p, Z_p):
 
 
 def em_loop(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, itera,
-            h_initial, hard=False, return_trace=False):
+            h_initial, hard=False, return_trace=False, skip_zero=True):
     """Exact soft EM — PMd/Proposed_method_NMSEvsTp.py:50-83 (identical contract at
     PMd/Proposed_method_NMSEvsTd.py:44-76, PMd/SNR/all_Detectors.py:242-274).
 
     ``hard=True`` gives the hard-ML ("log-max") E-step of
     PMd/ML_detecctor.py:65-77 / PMd/all_detectorsvsTd.py:143-155: only the
     posterior argmax (first index on ties, ``np.argmax``) enters the M-step.
+    ``skip_zero=False`` accumulates zero-weight hypotheses too, as the reference loop does
+    (:70-71): the full O(T_d J K^2) work, for bench.py's reference-structured CPU baseline.
     """
     n_rx = Y_d[0].shape[0]
     aps = np.asarray(all_possibleSymbols)
@@ -62,7 +64,7 @@ def em_loop(Y_d, Y_p, T_d, T_p, Z_p, PsiTilde_td, all_possibleSymbols, M, varn, 
                 w = np.exp(logw - logw.max())
                 w /= w.sum()                        # :69 beta_exp
             for j in range(J):
-                if w[j] == 0.0:
+                if skip_zero and w[j] == 0.0:
                     continue
                 Z = Zs[j]
                 numer += w[j] * (np.conj(Z).T @ Y_d[t])     # :70

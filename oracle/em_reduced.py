@@ -137,16 +137,20 @@ def mstep_solve(R, rhs):
 
 
 def em_reduced(Y_d, Y_p, U_p, Psi, aps, varn, itera, theta0, mode="soft",
-               return_trace=False):
+               return_trace=False, h=None):
     """Reduced-form EM over one trial.  Inputs in array form:
-    Y_d (T_d, n_rx), Y_p (T_p, n_rx), U_p (T_p, L), Psi (P, T_d), aps (J, n_tx)."""
+    Y_d (T_d, n_rx), Y_p (T_p, n_rx), U_p (T_p, L), Psi (P, T_d), aps (J, n_tx).
+    h: the oracle early stop |‖theta‖ - ‖h‖| < 1 after an iteration l != 0 of
+    PMd/all_detectorsvsTd.py:169-171 (em_ml) / :291-293 (em)."""
     theta = np.asarray(theta0, dtype=complex).reshape(-1)
     trace = []
-    for _ in range(itera):
+    for l in range(itera):
         m, S, _, _ = estep_moments(theta, Y_d, Psi, aps, varn, mode)
         R, rhs = mstep_build(U_p, Y_p, Psi, Y_d, m, S)
         theta = mstep_solve(R, rhs)
         trace.append(theta.copy())
+        if h is not None and abs(np.linalg.norm(theta) - np.linalg.norm(h)) < 1 and l != 0:
+            break
     return (theta, trace) if return_trace else theta
 
 

@@ -123,15 +123,25 @@ def observe(h, U, n_rx, noise):
     return U @ H.T + noise
 
 
-def initial_estimate(U_p, Y_p, n_rx):
+def initial_estimate(U_p, Y_p, n_rx, pinv="numpy"):
     """h_initial = pinv(vstack Z_p) vstack Y_p (PMd/Proposed_method_NMSEvsTp.py:129), in
-    reduced form H_0 = Y_p^T pinv(U_p^T) (pinv(U (x) I) = pinv(U) (x) I)."""
-    H0 = np.asarray(Y_p).T @ np.linalg.pinv(np.asarray(U_p).T)
+    reduced form H_0 = Y_p^T pinv(U_p^T) (pinv(U (x) I) = pinv(U) (x) I: the same singular
+    values, n_rx times each).  pinv="numpy": np.linalg.pinv's default cut 1e-15 sigma_max;
+    pinv="scipy": scipy.linalg.pinv's max(M, N) eps sigma_max on the (T_p n_rx) x K matrix --
+    the one all_detectorsvsTd.py:341 uses (`from scipy import linalg`), which matters when the
+    pilots leave rounding-level singular values (T_p < L)."""
+    U = np.asarray(U_p)
+    if pinv == "scipy":
+        rc = max(U.shape[0] * n_rx, U.shape[1] * n_rx) * np.finfo(float).eps
+        P = np.linalg.pinv(U.T, rcond=rc) if U.size else np.zeros(U.shape, dtype=complex)
+    else:
+        P = np.linalg.pinv(U.T)
+    H0 = np.asarray(Y_p).T @ P
     return H0.T.reshape(-1)
 
 
 def received_signals(T_p, T_d, Psi_tp, Psi_td, n_rx, n_tx, X_d, X_p, h, varn, rs=None,
-                     with_initial=True):
+                     with_initial=True, pinv="numpy"):
     """(Y_p, Y_d, U_p, U_d, h_initial) of PMd/Proposed_method_NMSEvsTp.py:114-130.
 
     Noise draws: one normal(0, sqrt(varn/2), (n_rx, 2)) per pilot, then per data
@@ -147,7 +157,7 @@ def received_signals(T_p, T_d, Psi_tp, Psi_td, n_rx, n_tx, X_d, X_p, h, varn, rs
                     for _ in range(T_d)])
     Y_p = observe(h, U_p, n_rx, n_p)
     Y_d = observe(h, U_d, n_rx, n_d)
-    h0 = initial_estimate(U_p, Y_p, n_rx) if with_initial else None
+    h0 = initial_estimate(U_p, Y_p, n_rx, pinv) if with_initial else None
     return Y_p, Y_d, U_p, U_d, h0
 
 

@@ -7,6 +7,9 @@ estimator with every trial of a sweep point batched into ONE sbce_em call.
   ser_vs_snr   "Proposed method/SER/log_max_SER.py":124-167 (log-max EM decisions)
   nmse_vs_tp_superimposed  "Parallel/ParallelProtocol_Tp.py":106-136 (superimposed pilots)
   nmse_vs_tp_gaussian      "Proposed method/MIMO_Gaussian_proposed.py":158-177 (Gaussian prior)
+  nmse_grid_detectors      "Proposed method/all_detectorsvsTd.py":345-405 (five EMs per T_d
+                           point), extended over an SNR axis (BASELINE configs[4])
+  llf_vs_iteration         "Proposed method/IterationsvsLLF.py":119-157 (LLF per EM iteration)
 
 Data generation (host, NumPy):
   replay=True   the reference's exact legacy-RandomState call order after
@@ -339,3 +342,126 @@ def nmse_vs_tp_gaussian(T_p=(8, 12, 16, 20, 24, 28, 32, 36, 40), T_d=50, N=32, n
         acc.add(k, nmse_batch(Hh.reshape(len(trials), -1), Hf).cpu().numpy())
     acc.allreduce(dist)
     return np.asarray(T_p), acc.mean_nmse()
+
+
+# (E-step mode, reference EM of all_detectorsvsTd.py, its plot label :407-411)
+DETECTORS = {
+    "pm_soft": ("em_pm :176-249 (posterior-weighted list, partition_r)", "Soft decision-PM"),
+    "hard": ("em_ml :135-173 (log-max)", "Non - Superimposed log-max"),
+    "zf": ("em_zf :95-133", "Zero forcing"),
+    "mmse": ("em_mmse :54-93", "MMSE"),
+    "soft": ("em :260-295 (exact posterior)", "Non - Superimposed"),
+}
+
+
+def gen_detectors(T_d=(15, 30, 45, 60, 75, 90), SNR=None, T_p=20, N=15, n_rx=2, n_tx=2,
+                  monte_iter=1, M=4, varn=0.1, power=10.0, seed=0, replay=True, varh=1.0,
+                  keep=None):
+    """Data of PMd/all_detectorsvsTd.py:371-382 in its draw order: per trial channelMatrix,
+    pilotSymbols(T_p); per T_d point symbols(T_d), irsMatrix (pilot phases (N+1) x T_p DFT
+    with a zero last row, T_d uniform data-phase columns), the ones row inserted, then
+    receivedSignals (h_initial by scipy.linalg.pinv, :341) -- once with the script's varn
+    (SNR=None), or once per SNR point in SNR order (the grid extension of BASELINE
+    configs[4]; varn = power / 10^(SNR/10), SNR/all_Detectors.py:351-354).  Returns (points[k_td][k_snr] = trial dicts, varns)."""
+    varns = [float(varn)] if SNR is None else [float(v) for v in sm.snr_to_varn(SNR, power)]
+    keep = set(range(monte_iter)) if keep is None else set(keep)
+    points = [[[] for _ in varns] for _ in T_d]
+    if replay:
+        np.random.seed(seed)
+    for i in range(monte_iter):
+        rs = None if replay else _trial_rng(seed, i)
+        if not replay and i not in keep:
+            continue
+        h = sm.channel_matrix(n_tx, n_rx, N, varh, rs=rs)
+        X_p = sm.pilot_symbols(n_tx, M, T_p, rs=rs)
+        for k, td in enumerate(T_d):
+            X_d, _ = sm.symbols(n_tx, M, td, rs=rs)
+            Ptp, Ptd = sm.irs_matrix(T_p, td, N, pilot="dft_n", rs=rs)
+            Ptd = sm.insert_direct(Ptd)
+            for j, vn in enumerate(varns):
+                Y_p, Y_d, U_p, _, h0 = sm.received_signals(T_p, td, Ptp, Ptd, n_rx, n_tx, X_d,
+                                                           X_p, h, vn, rs=rs, pinv="scipy")
+                if i in keep:
+                    points[k][j].append(dict(Y_d=Y_d, Y_p=Y_p, Psi_d=Ptd, U_p=U_p, h0=h0, h=h))
+    return points, varns
+
+
+def nmse_grid_detectors(T_d=(15, 30, 45, 60, 75, 90), SNR=None, T_p=20, N=15, n_rx=2, n_tx=2,
+                        itera=5, monte_iter=1, M=4, varn=0.1, power=10.0, partition_r=1, seed=0,
+                        replay=True, detectors=tuple(DETECTORS), early_stop=True, varh=1.0):
+    """Mean NMSE of the five EMs of PMd/all_detectorsvsTd.py (:384-405) per T_d point, and
+    per SNR point when SNR is given (BASELINE configs[4]: 20 SNR x 8 T_d, 64-QAM).
+
+    One batched sbce_em per (T_d, SNR, detector) over this rank's trials; every EM keeps the
+    script's oracle early stop on the true h (:87-89, :128-130, :169-171, :243-245,
+    :291-293) unless early_stop=False, and its np.linalg.solve M-step (SBCE_SOLVE_CHOL).
+    The accumulators of the whole grid are all-reduced once.  Returns (T_d, SNR or None,
+    {detector: (len(T_d), len(SNR or [varn])) mean NMSE})."""
+    dist, world, rank = _dist()
+    mine = shard(monte_iter, world, rank).tolist()
+    points, varns = gen_detectors(T_d, SNR, T_p, N, n_rx, n_tx, monte_iter, M, varn, power, seed,
+                                  replay, varh, keep=mine)
+    cons = qam_constellation(M)
+    nd, nt, ns = len(detectors), len(T_d), len(varns)
+    acc = Accumulators(nd * nt * ns)
+    for k in range(nt):
+        for j in range(ns):
+            trials = points[k][j]
+            if not trials:
+                continue
+            b = _pack(trials, None)
+            for di, det in enumerate(detectors):
+                r = em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], cons, varns[j], itera,
+                             b["theta0"], mode=det, partition_r=partition_r if det == "pm_soft" else 0,
+                             h_true=b["h"] if early_stop else None)
+                acc.add((di * nt + k) * ns + j, _nmse(r["theta"], b["h"]))
+    acc.allreduce(dist)
+    mean = acc.mean_nmse().reshape(nd, nt, ns)
+    return (np.asarray(T_d), None if SNR is None else np.asarray(SNR),
+            {det: mean[di] for di, det in enumerate(detectors)})
+
+
+def gen_llf(T_d=50, T_p=4, N=32, n_rx=2, n_tx=2, monte_iter=3, M=4, varn=0.1, seed=0,
+            replay=True, varh=1.0, keep=None):
+    """Data of PMd/IterationsvsLLF.py:140-149 in its draw order per trial: channelMatrix
+    (row-major flatten of h, :16), symbols(T_d), irsMatrix (pilot phases N x T_p DFT over N, :90-92), ones rows inserted into
+    the pilot and data phases (:144-145), pilotSymbols, receivedSignals."""
+    keep = set(range(monte_iter)) if keep is None else set(keep)
+    trials = []
+    if replay:
+        np.random.seed(seed)
+    for i in range(monte_iter):
+        rs = None if replay else _trial_rng(seed, i)
+        if not replay and i not in keep:
+            continue
+        h = sm.channel_matrix(n_tx, n_rx, N, varh, order="C", rs=rs)
+        X_d, _ = sm.symbols(n_tx, M, T_d, rs=rs)
+        Ptp, Ptd = sm.irs_matrix(T_p, T_d, N, pilot="dft_n", rs=rs)
+        Ptp = sm.insert_direct(Ptp[:N])
+        Ptd = sm.insert_direct(Ptd)
+        X_p = sm.pilot_symbols(n_tx, M, T_p, rs=rs)
+        Y_p, Y_d, U_p, _, h0 = sm.received_signals(T_p, T_d, Ptp, Ptd, n_rx, n_tx, X_d, X_p, h,
+                                                   varn, rs=rs)
+        if i in keep:
+            trials.append(dict(Y_d=Y_d, Y_p=Y_p, Psi_d=Ptd, U_p=U_p, h0=h0, h=h,
+                               X_d=np.stack([x.reshape(-1) for x in X_d])))
+    return trials
+
+
+def llf_vs_iteration(T_d=50, T_p=4, N=32, n_rx=2, n_tx=2, itera=5, monte_iter=3, M=4, varn=0.1,
+                     seed=0, replay=True, varh=1.0):
+    """Mean log-likelihood per EM iteration (PMd/IterationsvsLLF.py:139-154): the exact EM
+    (:45-77) with the script's genie LLF (:76: un-squared norms, Z_d from the TRUE data
+    symbols), averaged over trials (gen_llf data).  Returns (iterations, mean LLF, mean final
+    NMSE)."""
+    dist, world, rank = _dist()
+    trials = gen_llf(T_d, T_p, N, n_rx, n_tx, monte_iter, M, varn, seed, replay, varh,
+                     keep=shard(monte_iter, world, rank).tolist())
+    acc = Accumulators(1, n_iters=itera)
+    if trials:
+        b = _pack(trials, None)
+        r = em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], qam_constellation(M), varn, itera,
+                     b["theta0"], mode="soft", x_d_true=np.stack([t["X_d"] for t in trials]))
+        acc.add(0, _nmse(r["theta"], b["h"]), llf_values=r["llf"])
+    acc.allreduce(dist)
+    return np.arange(itera), acc.mean_llf()[0], float(acc.mean_nmse()[0])

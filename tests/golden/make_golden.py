@@ -357,6 +357,85 @@ def case_gaussian():
     return "gaussian", out
 
 
+def case_alldet(name, N, n_tx, n_rx, T_d, T_p, M, varn, itera, partition_r, seed):
+    """PMd/all_detectorsvsTd.py at ONE T_d point of its sweep, with the script's own helpers in
+    its driver's draw order (:371-382: channelMatrix, pilotSymbols, then per T_d symbols,
+    irsMatrix, ones row, receivedSignals) and its five EMs (:384-388): em_pm (soft list,
+    :176-249), em_ml (:135-173), em_zf (:95-133), em_mmse (:54-93), em (:260-295).  Every EM
+    reads the global h for the oracle early stop."""
+    ns = load_defs(os.path.join(PMD, "all_detectorsvsTd.py"), N=N, n_tx=n_tx,
+                   beta_min=0.0, beta_max=2 * np.pi)
+    np.random.seed(seed)
+    h = quiet(ns["channelMatrix"], n_tx, n_rx, N, 1)
+    X_p = ns["pilotSymbols"](n_tx, M, T_p)
+    X_d, aps, cons = ns["symbols"](n_tx, M, T_d)
+    Ptp, Ptd = ns["irsMatrix"](T_p, T_d, N, 0.0, 1)
+    Ptd = np.insert(Ptd, 0, np.ones((1, T_d), dtype="complex128"), axis=0)
+    Y_p, Y_d, Z_p, Z_d, h0 = ns["receivedSignals"](T_p, T_d, Ptp, Ptd, n_rx, n_tx, X_d, X_p, h,
+                                                   varn, M)
+    ns["h"] = h
+    ns["qamCons"] = cons
+    ns["Z_d"] = Z_d                      # em_mmse's LLF line (:91) reads the global Z_d
+    common = (Y_d, Y_p, T_d, T_p, Z_p, Ptd)
+    th = {
+        "pm": quiet(ns["em_pm"], *common, M, varn, itera, h0, h, n_tx, partition_r, X_d, cons),
+        "ml": quiet(ns["em_ml"], *common, aps, M, varn, itera, h0),
+        "zf": quiet(ns["em_zf"], *common, aps, M, varn, itera, h0, h),
+        "mmse": quiet(ns["em_mmse"], *common, aps, M, varn, itera, h0, h),
+        "em": quiet(ns["em"], *common, aps, M, varn, itera, h0),
+    }
+    d = dict(h=h, X_d=X_d, aps=aps, X_p=X_p, Ptp=Ptp, Ptd=Ptd, Y_p=Y_p, Y_d=Y_d, Z_p=Z_p, h0=h0)
+    extra = {f"{k}_theta": np.asarray(v).reshape(-1) for k, v in th.items()}
+    extra.update({f"{k}_nmse": nmse(v, h) for k, v in th.items()})
+    return name, _pack(d, N=N, n_tx=n_tx, n_rx=n_rx, T_d=T_d, T_p=T_p, M=M, varn=varn,
+                       itera=itera, partition_r=partition_r, seed=seed, cons=cons, **extra)
+
+
+def case_cfg1_kernel():
+    """The BASELINE cfg-1 kernel instantiation (n_tx = n_rx = 4, 16-QAM: J = 65,536 hypotheses
+    per symbol) through the north-star em (PMd/Proposed_method_NMSEvsTp.py:50-83, gmpy2 ->
+    mpmath) at a size the mp-object reference finishes in minutes: N = 1, T_p = 8, T_d = 2,
+    two iterations, a low SNR (varn = 3) so that the posterior weights are genuinely soft."""
+    N, n_tx, n_rx, T_d, T_p, M, varn, itera, seed = 1, 4, 4, 2, 8, 16, 3.0, 2, 41
+    ns = load_defs(os.path.join(PMD, "Proposed_method_NMSEvsTp.py"),
+                   N=N, n_tx=n_tx, n_rx=n_rx, beta_min=0.0, beta_max=2 * np.pi)
+    d = _gen_northstar(ns, seed, N, n_tx, n_rx, T_d, T_p, M, varn)
+    res = {}
+    for it in (1, itera):
+        th = quiet(ns["em"], d["Y_d"], d["Y_p"], T_d, T_p, d["Z_p"], d["Ptd"], d["aps"],
+                   M, varn, it, d["h0"])
+        res[f"theta_it{it}"] = np.asarray(th).reshape(-1)
+    return "cfg1_kernel", _pack(d, N=N, n_tx=n_tx, n_rx=n_rx, T_d=T_d, T_p=T_p, M=M, varn=varn,
+                                itera=itera, seed=seed, **res)
+
+
+def case_llf_driver():
+    """PMd/IterationsvsLLF.py's own driver (:139-154) with its own helpers and draw order
+    (channelMatrix, symbols, irsMatrix + ones rows, pilotSymbols, receivedSignals, em with
+    the genie LLF :76) at reduced sizes: the per-trial LLF curves and the data."""
+    N, n_tx, n_rx, T_d, T_p, M, varn, itera, monte_iter, seed = 8, 2, 2, 20, 4, 4, 0.1, 3, 2, 23
+    ns = load_defs(os.path.join(PMD, "IterationsvsLLF.py"), N=N, n_tx=n_tx, n_rx=n_rx,
+                   beta_min=0.0, beta_max=2 * np.pi)
+    np.random.seed(seed)
+    out = dict(N=N, n_tx=n_tx, n_rx=n_rx, T_d=T_d, T_p=T_p, M=M, varn=varn, itera=itera,
+               monte_iter=monte_iter, seed=seed)
+    for i in range(monte_iter):
+        h = quiet(ns["channelMatrix"], n_tx, n_rx, N, 1)
+        X_d, aps = ns["symbols"](n_tx, M, T_d)[:2]
+        Ptp, Ptd = ns["irsMatrix"](T_p, T_d, N, 0.0, 1)
+        Ptp = np.insert(Ptp, 0, np.ones((1, T_p), dtype="complex128"), axis=0)
+        Ptd = np.insert(Ptd, 0, np.ones((1, T_d), dtype="complex128"), axis=0)
+        X_p = ns["pilotSymbols"](n_tx, M, T_p)
+        Y_p, Y_d, Z_p, Z_d, h0 = ns["receivedSignals"](T_p, T_d, Ptp, Ptd, n_rx, n_tx, X_d, X_p,
+                                                       h, varn, M, N)
+        th, llf = quiet(ns["em"], Y_d, Y_p, T_d, T_p, Z_p, Z_d, Ptd, aps, M, varn, itera, h0,
+                        n_tx)
+        out.update({f"h{i}": h, f"Y_d{i}": np.stack(Y_d)[..., 0], f"Y_p{i}": np.stack(Y_p)[..., 0],
+                    f"theta{i}": np.asarray(th).reshape(-1),
+                    f"llf{i}": np.asarray(llf, dtype=float).reshape(-1)})
+    return "llf_driver", out
+
+
 def case_qam():
     """Constellation tables of the vendored komm QAM (PMd/QAM.py:320-322)."""
     return "qam", {f"cons{M}": _cons(M) for M in (4, 16, 64, 256)}
@@ -364,6 +443,10 @@ def case_qam():
 
 CASES = {
     "qam": (case_qam, ()),
+    # all_detectorsvsTd.py's own constants (:345-363) at its first T_d point
+    "alldet_td15": (case_alldet, ("alldet_td15", 15, 2, 2, 15, 20, 4, 0.1, 5, 1, 3)),
+    "cfg1_kernel": (case_cfg1_kernel, ()),
+    "llf_driver": (case_llf_driver, ()),
     "pm_nt4": (case_pm, ("pm_nt4", 3, 4, 4, 24, 8, 4, 0.1, 3, 12, 0, 2)),
     "pm_nt3_m16": (case_pm, ("pm_nt3_m16", 4, 3, 3, 24, 10, 16, 0.3, 3, 13, 1, 1)),
     "ser_logmax": (case_ser, ()),

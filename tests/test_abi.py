@@ -54,6 +54,32 @@ int main(void) {
                                      L.Dims.varx.offset]
 
 
+def test_integration_snippet_matches_abi(sbce):
+    """INTEGRATION.md's raw ctypes binding (section 3) is what a maintainer copies: its
+    struct definitions must equal _lib.py's, field by field, and therefore the C layout
+    (test_struct_layout_matches_c), or sbce_em reads past the caller's structs."""
+    md = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    sec = md[md.index("## 3. Raw ctypes binding"):md.index("## 4.")]
+    code = re.search(r"```python\n(.*?)```", sec, re.S).group(1)
+    # the class definitions and the ABI version only (the rest needs a GPU and buffers)
+    head = code[:code.index("lib = ctypes.CDLL")]
+    ns = {}
+    exec(head, ns)
+    L = sbce._lib
+    assert ns["SBCE_ABI_VERSION"] == L.SBCE_ABI_VERSION
+    for name in ("Dims", "Ptrs"):
+        doc, lib = ns[name], getattr(L, name)
+        assert [(f, t) for f, t in doc._fields_] == [(f, t) for f, t in lib._fields_], name
+        assert ctypes.sizeof(doc) == ctypes.sizeof(lib)
+    # every field the C header declares appears in the snippet, in order
+    src = open(HEADER).read()
+    for cname, pyname in (("sbce_dims", "Dims"), ("sbce_ptrs", "Ptrs")):
+        body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, re.S).group(1)
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        cfields = re.findall(r"(\w+)\s*;", body)
+        assert cfields == [f for f, _ in ns[pyname]._fields_], (cname, cfields)
+
+
 def test_workspace_and_validation_without_gpu(sbce):
     L = sbce._lib
     lib = L.load()

@@ -171,6 +171,30 @@ def test_cfg1_shape_full_em_vs_oracle(sbce):
     assert abs(nmse(r["theta"][0], b["h"][0]) / nmse(th0, b["h"][0]) - 1) < 1e-3
 
 
+def test_cfg1_nmse_trajectory_20_iterations_vs_oracle(sbce):
+    """The headline workload's NMSE, pinned: BASELINE cfg 1 (4x4, N_RIS = 64, T_p = 16,
+    T_d = 256, 16-QAM, 20 dB) on the first 8 trials of bench.py's synthetic batch, all 20 EM
+    iterations, against the oracle's trajectories (tests/golden/cfg1_traj.npz, made by
+    tests/golden/make_cfg1_traj.py).  North-star bar: NMSE within 1e-3 relative at every
+    iteration; measured agreement is reported per iteration."""
+    g = golden("cfg1_traj")
+    n = g["nmse"].shape[0]
+    varn = float(sbce.signal_model.snr_to_varn(float(g["snr"])))
+    b = sbce.signal_model.synthetic_batch(int(g["B"]), 4, 4, 64, 16, 256, 16, varn,
+                                          seed=int(g["seed"]))
+    sl = slice(0, n)
+    args = (b["y_d"][sl], b["y_p"][sl], b["psi_d"][sl], b["u_p"][sl], b["cons"], varn)
+    worst = []
+    for it in range(1, int(g["itera"]) + 1):
+        r = sbce.em_batch(*args, it, b["theta0"][sl])
+        nm = np.array([nmse(r["theta"][i], b["h"][i]) for i in range(n)])
+        err = np.abs(nm / g["nmse"][:, it] - 1).max()
+        worst.append(err)
+        assert err < 1e-3, (it, err)
+    assert rel(r["theta"], g["theta"]) < 1e-6, rel(r["theta"], g["theta"])
+    print("cfg1 trajectory: max relative NMSE deviation per iteration", np.array(worst))
+
+
 def test_batch_equals_single_and_is_deterministic(sbce):
     varn = 0.2
     b = sbce.signal_model.synthetic_batch(5, 2, 2, 6, 8, 20, 16, varn, seed=3)

@@ -442,3 +442,65 @@ def test_gaussian_sweep_replays_reference_data(sbce):
         assert np.array_equal(t["Psi_d"], d[f"Ptd{k}"])
         assert rel(t["Y_d"], d[f"Y_d{k}"]) < 1e-13 and rel(t["Y_p"], d[f"Y_p{k}"]) < 1e-13
         assert rel(t["h0"], sbce.reduce_gaussian_channel(d[f"H0{k}"], n_tx, n_rx)) < 1e-12
+
+
+# ---------------------------------------------------------------- all_detectorsvsTd / LLF drivers
+def test_detector_grid_replays_reference_data(sbce):
+    """sweeps.gen_detectors reproduces PMd/all_detectorsvsTd.py's data (its own helpers, its
+    driver's draw order :371-382) at the fixture's T_d point."""
+    d = golden("alldet_td15")
+    points, varns = sbce.sweeps.gen_detectors((int(d["T_d"]),), None, int(d["T_p"]), int(d["N"]),
+                                              int(d["n_rx"]), int(d["n_tx"]), 1, int(d["M"]),
+                                              float(d["varn"]), seed=int(d["seed"]))
+    t = points[0][0][0]
+    assert rel(t["h"], d["h"]) < 1e-15
+    assert rel(t["Y_d"], d["Y_d"]) < 1e-13 and rel(t["Y_p"], d["Y_p"]) < 1e-13
+    assert rel(t["h0"], d["h0"]) < 1e-10
+    assert rel(t["Psi_d"], d["Ptd"]) < 1e-15
+
+
+def test_detector_oracles_match_reference_five_ems():
+    """The oracle restatements of all_detectorsvsTd.py's five EMs (oracle early stop on the
+    true h in every one) against the reference's own outputs at one T_d point."""
+    from oracle.pm import em_pm
+    from oracle.detectors import em_detector
+    d = golden("alldet_td15")
+    n_rx, n_tx, itera = int(d["n_rx"]), int(d["n_tx"]), int(d["itera"])
+    Up = u_from_zp(d["Z_p"], n_rx)
+    varn, h = float(d["varn"]), d["h"]
+    args = (d["Y_d"], d["Y_p"], Up, d["Ptd"])
+    got = {
+        "pm": em_pm(*args, varn, itera, d["h0"], n_tx, n_rx, int(d["partition_r"]), d["cons"],
+                    soft=True, h=h),
+        "ml": em_reduced(*args, d["aps"], varn, itera, d["h0"], mode="hard", h=h),
+        "zf": em_detector(*args, d["aps"], varn, itera, d["h0"], n_tx, n_rx, "zf", h=h),
+        "mmse": em_detector(*args, d["aps"], varn, itera, d["h0"], n_tx, n_rx, "mmse", h=h),
+        "em": em_reduced(*args, d["aps"], varn, itera, d["h0"], h=h),
+    }
+    for k, th in got.items():
+        assert rel(th, d[f"{k}_theta"]) < 1e-9, k
+        assert abs(nmse(th, h) / float(d[f"{k}_nmse"]) - 1) < 1e-9, k
+
+
+def test_llf_driver_replays_reference(sbce):
+    """sweeps.gen_llf reproduces PMd/IterationsvsLLF.py's driver data, and the oracle's genie
+    LLF (:76) on them equals the reference's per-trial LLF curves."""
+    from oracle.em_loop import llf_genie
+    d = golden("llf_driver")
+    n_tx, n_rx, T_d, T_p, M = (int(d[k]) for k in ("n_tx", "n_rx", "T_d", "T_p", "M"))
+    varn, itera = float(d["varn"]), int(d["itera"])
+    trials = sbce.sweeps.gen_llf(T_d, T_p, int(d["N"]), n_rx, n_tx, int(d["monte_iter"]), M, varn,
+                                 seed=int(d["seed"]))
+    aps = sbce.qam.all_possible_symbols(sbce.qam.qam_constellation(M), n_tx)
+    for i, t in enumerate(trials):
+        assert rel(t["h"], d[f"h{i}"]) < 1e-15 and rel(t["Y_d"], d[f"Y_d{i}"]) < 1e-13
+        th, trace = em_reduced(t["Y_d"], t["Y_p"], t["U_p"], t["Psi_d"], aps, varn, itera, t["h0"],
+                               return_trace=True)
+        assert rel(th, d[f"theta{i}"]) < 1e-10
+        Z_p = [np.kron(u[None], np.eye(n_rx)) for u in t["U_p"]]
+        Z_d = [np.kron(np.kron(t["Psi_d"][:, k][None], t["X_d"][k][None]), np.eye(n_rx))
+               for k in range(T_d)]
+        llf = [llf_genie(th_l, t["Y_p"][..., None], Z_p, t["Y_d"][..., None], Z_d, T_d, T_p, n_tx, M,
+                         varn)
+               for th_l in trace]
+        assert np.allclose(llf, d[f"llf{i}"], rtol=1e-11, atol=0)
