@@ -93,7 +93,7 @@ extern "C" {
                                    (the intended fallback of all_detectorsvsTd.py:238-241):
                                    R's rank is cut at eps*K*lambda_max(R) (lstsq's default
                                    rcond = eps*max(K,K) on the K x K system, whose singular
-                                   values are R's eigenvalues), lambda_max by 6 Lanczos steps;
+                                   values are R's eigenvalues), lambda_max by 4 Lanczos steps;
                                    R = G G^H by a Cholesky that drops the pivots below 32x the
                                    cut (above its rounding noise), theta = conj(G (G^H G)^-2
                                    G^H B^H).  Equal to lstsq when no pivot lies between 4x the

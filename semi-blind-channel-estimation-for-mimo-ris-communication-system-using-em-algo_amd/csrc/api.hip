@@ -66,7 +66,7 @@ size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 struct Carve {
     size_t mom, R, rhs, done, ysh, prep, list, tree, tol, winv, ppsi, pS, pflag, prhs, gram, grhs,
-        act, tol2, total;
+        act, tol2, dvec, total;
     bool has_prep, has_prhs;
 };
 
@@ -120,7 +120,8 @@ Carve carve(const Problem& pb) {
     c.grhs = align_up(c.gram + (size_t)pb.B * pb.L * pb.L * sizeof(cd));
     c.act = align_up(c.grhs + (size_t)pb.B * pb.L * pb.NR * sizeof(cd));
     c.tol2 = align_up(c.act + (size_t)pb.B * sizeof(int32_t));
-    c.total = align_up(c.tol2 + (size_t)pb.B * sizeof(double));
+    c.dvec = align_up(c.tol2 + (size_t)pb.B * sizeof(double));
+    c.total = align_up(c.dvec + (size_t)pb.B * pb.L * sizeof(double));
     return c;
 }
 
@@ -138,6 +139,7 @@ void set_large(MstepArgs& ma, char* ws, const Carve& c) {
     ma.grhs = (cd*)(ws + c.grhs);
     ma.act = (int32_t*)(ws + c.act);
     ma.tol2 = (double*)(ws + c.tol2);
+    ma.dvec = (double*)(ws + c.dvec);
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -375,6 +377,18 @@ int sbce_debug_mstep_phase(const sbce_dims* d, const sbce_ptrs* p, const void* m
     if (phase == 0) return rbuild_herm_supported(pb) ? hip_rc(launch_pilot_factor(pb, ma, s)) : SBCE_OK;
     if (phase == 1 && rbuild_herm_supported(pb)) return hip_rc(launch_rbuild_herm(pb, ma, s));
     return hip_rc(launch_mstep_build(pb, ma, s, rbuild_herm_supported(pb)));
+}
+
+// Diagnostic, not part of include/sbce.h: the per-trial pivot threshold tau = 32 eps K lambda_max
+// the last min-norm M-step left in the workspace (tol_out [B] doubles, host or device memory).
+int sbce_debug_minnorm_tol(const sbce_dims* d, const sbce_ptrs* p, double* tol_out, void* hip_stream) {
+    Problem pb;
+    if (!make_problem(d, pb) || !tol_out) return SBCE_EINVAL;
+    int rc = check_ptrs(p, pb, true);
+    if (rc) return rc;
+    const Carve c = carve(pb);
+    return hip_rc(hipMemcpyAsync(tol_out, (char*)p->workspace + c.tol, (size_t)pb.B * sizeof(double),
+                                 hipMemcpyDefault, (hipStream_t)hip_stream));
 }
 
 // Diagnostic, not part of include/sbce.h: re-read the SBCE_* debug switches from the

@@ -8,7 +8,7 @@
 // directions of R with eigenvalue > eps K lambda_max(R) and returns the minimum-norm solution
 // on them.  On the GPU, per trial:
 //
-//   lanczos_tol_kernel  lambda_max(R) by 6 Lanczos steps (one workgroup per trial streaming
+//   lanczos_tol_kernel  lambda_max(R) by 4 Lanczos steps (one workgroup per trial streaming
 //                       R's lower triangle once per step); cut = eps K max(lambda, max diag R);
 //   tiled Cholesky of R (mstep_large.hip) whose pivots at or below tau = 32 cut are dropped
 //                       (their columns zeroed), R = G G^H with G lower triangular; act_kernel
@@ -40,7 +40,7 @@ namespace {
 typedef double d4v __attribute__((ext_vector_type(4)));
 constexpr int TB = 64;            // tile of the blocked factorisation (mstep_large.hip)
 constexpr int KS = 16;            // k-chunk of the Gram tiles
-constexpr int kLanczosSteps = 6;
+constexpr int kLanczosSteps = 4;   // lambda_max to ~10 % (the cut carries a 32x margin)
 constexpr double kCutSafety = 32.0;   // tau = kCutSafety * cut (see the header comment)
 constexpr double kEps = 2.220446049250313e-16;   // numpy.finfo(float).eps
 
@@ -88,108 +88,133 @@ __device__ double tridiag_max_eig(const double* al, const double* be, int k) {
 }
 
 // ---------------------------------------------------------------- lambda_max -> cut
-// One workgroup (4 waves) per trial.  Matvec y = R v from the lower triangle, each 64 x 64
-// tile read once: lane = row r of the tile, wave = 16-column quarter; the row products stay in
-// the lane (summed over the row block's tiles, then over the 4 waves), the column products
-// conj(R[r][c]) v[r] (strict lower part) are summed over the 64 lanes by a recursive-halving
-// reduce-scatter (32 shuffles for the 16 complex columns).  v (and y when it fits) in LDS.
+// One workgroup of kLzWaves waves per trial.  Matvec y = R v from the lower triangle, each
+// 64 x 64 tile read once by one wave (tile J of row block I -> wave J % kLzWaves), row by row:
+// lane = column, so every load is one coalesced 1 KB row segment.  The column products
+// conj(R[r][c]) v[r] (strict lower part) accumulate in the lane and go to y[c] after the tile
+// (one writer per y entry per row block); the row products R[r][c] v[c] are reduce-scattered
+// over the lanes 16 rows at a time, kept per lane across the wave's tiles of the row block and
+// summed over the waves in a fixed order -- deterministic.  v (and y when it fits) in LDS.
+constexpr int kLzWaves = 8;
 template <bool YLDS>
-__global__ __launch_bounds__(256) void lanczos_tol_kernel(MstepArgs a, int L, int K) {
+__global__ __launch_bounds__(64 * kLzWaves) void lanczos_tol_kernel(MstepArgs a, int L, int K) {
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ cd part[4][64];
-    __shared__ double red[4];
+    __shared__ double part[kLzWaves][TB][2];
+    __shared__ double red[kLzWaves];
+    __shared__ double al[kLanczosSteps], be[kLanczosSteps];
     cd* v = reinterpret_cast<cd*>(smem);
     cd* scr = a.gram + (size_t)b * L * L;          // free until the Gram build
     cd* y = YLDS ? v + L : scr;
     cd* vp = scr + L;
     const cd* R = a.R + (size_t)b * L * L;
+    constexpr int NTH = 64 * kLzWaves;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nb = (L + TB - 1) / TB;
+    auto bsum = [&](double x) {
+        for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off);
+        __syncthreads();
+        if (lane == 0) red[wave] = x;
+        __syncthreads();
+        double t = 0.0;
+        for (int w = 0; w < kLzWaves; ++w) t += red[w];
+        return t;
+    };
     double md = 0.0;
     const double v0 = 1.0 / sqrt((double)L);
-    for (int i = tid; i < L; i += 256) {
-        md = fmax(md, R[(size_t)i * L + i].x);
+    for (int i = tid; i < L; i += NTH) {
+        const double di = R[(size_t)i * L + i].x;
+        md = fmax(md, di);
+        a.dvec[(size_t)b * L + i] = di;     // the Schur complement's diagonal before any column
         v[i] = cmk(v0, 0.0);
         vp[i] = czero();
     }
-    md = block_max(md, red);
-    double al[kLanczosSteps], be[kLanczosSteps];
+    for (int off = 32; off >= 1; off >>= 1) md = fmax(md, __shfl_xor(md, off));
+    __syncthreads();
+    if (lane == 0) red[wave] = md;
+    __syncthreads();
+    for (int w = 0; w < kLzWaves; ++w) md = fmax(md, red[w]);
     int ks = 0;
     double bprev = 0.0;
     for (int st = 0; st < kLanczosSteps; ++st) {
-        for (int i = tid; i < L; i += 256) y[i] = czero();
+        for (int i = tid; i < L; i += NTH) y[i] = czero();
         __syncthreads();
         for (int I = 0; I < nb; ++I) {
-            const int r = I * TB + lane;
-            const bool rv = r < L;
-            const cd vr = rv ? v[r] : czero();
-            cd s = czero();
-            for (int J = 0; J <= I; ++J) {
-                const int c0 = J * TB + wave * 16;
-                cd g[16];
+            const int r0 = I * TB;
+            const int nr = (L - r0) < TB ? (L - r0) : TB;
+            // after the reduce-scatter lane l holds value l >> 1 of the 16-row chunk: row l >> 2,
+            // component (l >> 1) & 1 (lanes l and l ^ 1 hold the same sum)
+            double rowacc[4] = {0.0, 0.0, 0.0, 0.0};
+            for (int J = wave; J <= I; J += kLzWaves) {
+                const int c = J * TB + lane;
+                const bool cv = c < L;
+                const cd vc = cv ? v[c] : czero();
+                cd cacc = czero();
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const int c = c0 + j;
-                    g[j] = (rv && c < L && (J < I || c <= r)) ? R[(size_t)r * L + c] : czero();
-                }
-                double d[32];
+                for (int q = 0; q < 4; ++q) {
+                    double d[32];
+                    cd g[16];
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const int c = c0 + j;
-                    const cd vc = c < L ? v[c] : czero();
-                    s = cfma(s, g[j], vc);
-                    // column product conj(R[r][c]) v[r], strictly below the diagonal
-                    const cd gc = (J < I || c < r) ? g[j] : czero();
-                    d[2 * j] = fma(gc.x, vr.x, gc.y * vr.y);
-                    d[2 * j + 1] = fma(gc.x, vr.y, -gc.y * vr.x);
-                }
-                // reduce-scatter over the 64 lanes: lane ends with the total of value lane >> 1
-#pragma unroll
-                for (int m = 32, n = 32; m >= 2; m >>= 1, n >>= 1) {
-                    const bool hi = (lane & m) != 0;
-#pragma unroll
-                    for (int i = 0; i < n / 2; ++i) {
-                        const double keep = hi ? d[n / 2 + i] : d[i];
-                        const double send = hi ? d[i] : d[n / 2 + i];
-                        d[i] = keep + __shfl_xor(send, m);
+                    for (int i = 0; i < 16; ++i) {
+                        const int r = r0 + 16 * q + i;
+                        g[i] = (cv && 16 * q + i < nr && (J < I || c <= r)) ? R[(size_t)r * L + c]
+                                                                           : czero();
                     }
-                }
-                const double tot = d[0] + __shfl_xor(d[0], 1);
-                if ((lane & 1) == 0) {
-                    const int idx = lane >> 1, c = c0 + (idx >> 1);
-                    if (c < L) {
-                        double* yc = reinterpret_cast<double*>(y + c) + (idx & 1);
-                        *yc += tot;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int r = r0 + 16 * q + i;
+                        const cd p = cmul(g[i], vc);                      // row product
+                        d[2 * i] = p.x;
+                        d[2 * i + 1] = p.y;
+                        if (J < I || c < r) cacc = cfmac(cacc, (16 * q + i < nr) ? v[r] : czero(), g[i]);
                     }
+                    // reduce-scatter of the 16 rows' products: lane ends with value lane >> 1
+#pragma unroll
+                    for (int m = 32, n = 32; m >= 2; m >>= 1, n >>= 1) {
+                        const bool hi = (lane & m) != 0;
+#pragma unroll
+                        for (int i = 0; i < n / 2; ++i) {
+                            const double keep = hi ? d[n / 2 + i] : d[i];
+                            const double send = hi ? d[i] : d[n / 2 + i];
+                            d[i] = keep + __shfl_xor(send, m);
+                        }
+                    }
+                    rowacc[q] += d[0] + __shfl_xor(d[0], 1);
                 }
+                if (cv) y[c] = cadd(y[c], cacc);
             }
-            part[wave][lane] = s;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if ((lane & 1) == 0) part[wave][16 * q + (lane >> 2)][(lane >> 1) & 1] = rowacc[q];
             __syncthreads();
-            if (wave == 0 && rv) {
-                const cd p = cadd(cadd(part[0][lane], part[1][lane]), cadd(part[2][lane], part[3][lane]));
-                y[r] = cadd(y[r], p);
+            if (tid < 2 * nr) {
+                const int rr = tid >> 1, comp = tid & 1;
+                double t = 0.0;
+                for (int w = 0; w < kLzWaves; ++w) t += part[w][rr][comp];
+                reinterpret_cast<double*>(y + r0 + rr)[comp] += t;
             }
             __syncthreads();
         }
         // three-term recurrence: alpha = v^H y, w = y - alpha v - beta vp
         double pa = 0.0;
-        for (int i = tid; i < L; i += 256) pa = fma(v[i].x, y[i].x, fma(v[i].y, y[i].y, pa));
-        const double alpha = block_sum(pa, red);
+        for (int i = tid; i < L; i += NTH) pa = fma(v[i].x, y[i].x, fma(v[i].y, y[i].y, pa));
+        const double alpha = bsum(pa);
         double pw = 0.0;
-        for (int i = tid; i < L; i += 256) {
+        for (int i = tid; i < L; i += NTH) {
             const cd w = csub(csub(y[i], cscale(v[i], alpha)), cscale(vp[i], bprev));
             y[i] = w;
             pw += cabs2(w);
         }
-        const double beta = sqrt(block_sum(pw, red));
-        al[st] = alpha;
-        be[st] = beta;
+        const double beta = sqrt(bsum(pw));
+        if (tid == 0) {
+            al[st] = alpha;
+            be[st] = beta;
+        }
         ks = st + 1;
         if (!(beta > 1e-13 * fabs(alpha)) || st + 1 == kLanczosSteps) break;
         const double ib = 1.0 / beta;
-        for (int i = tid; i < L; i += 256) {
+        for (int i = tid; i < L; i += NTH) {
             vp[i] = v[i];
             v[i] = cscale(y[i], ib);
         }
@@ -203,16 +228,17 @@ __global__ __launch_bounds__(256) void lanczos_tol_kernel(MstepArgs a, int L, in
 }
 
 // ---------------------------------------------------------------- early exit
-// Before column block k0: if every remaining diagonal entry of the Schur complement is at or
-// below the cut, all later pivots would be dropped: act[b] = k0 ends the trial's factorisation.
+// Before column group k0: if every remaining diagonal entry of the Schur complement (dvec, kept
+// by mstep_large.hip's dvec_kernel) is at or below the cut, all later pivots would be dropped:
+// act[b] = k0 ends the trial's factorisation.
 __global__ __launch_bounds__(256) void act_kernel(MstepArgs a, int L, int k0) {
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
     if (a.act[b] <= k0) return;
     __shared__ double red[4];
-    const cd* R = a.R + (size_t)b * L * L;
+    const double* dv = a.dvec + (size_t)b * L;
     double m = 0.0;
-    for (int i = k0 + threadIdx.x; i < L; i += 256) m = fmax(m, R[(size_t)i * L + i].x);
+    for (int i = k0 + threadIdx.x; i < L; i += 256) m = fmax(m, dv[i]);
     m = block_max(m, red);
     if (threadIdx.x == 0) {
         const double tol = a.tol[b];
@@ -490,27 +516,32 @@ __global__ __launch_bounds__(256) void gz_kernel(MstepArgs a, int L, int NR) {
     }
 }
 
+hipError_t launch_act(const Problem& pb, const MstepArgs& a, int k0, hipStream_t s) {
+    hipLaunchKernelGGL(act_kernel, dim3(pb.B), dim3(256), 0, s, a, pb.L, k0);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t launch_minnorm(const Problem& pb, const MstepArgs& a, hipStream_t s) {
-    if (pb.NR > 8 || !a.gram || !a.grhs || !a.act || !a.tol2 || !a.winv || !a.tol)
+    if (pb.NR > 8 || !a.gram || !a.grhs || !a.act || !a.tol2 || !a.winv || !a.tol || !a.dvec)
         return hipErrorInvalidValue;
     const int L = pb.L, nb = (L + TB - 1) / TB;
     hipError_t e;
     if ((e = hipMemsetD32Async((hipDeviceptr_t)a.act, L, (size_t)pb.B, s)) != hipSuccess) return e;
     // rank cut from lambda_max(R)
     const size_t vbytes = (size_t)L * sizeof(cd);
-    if (2 * vbytes + 8 * 1024 <= 160 * 1024)
-        hipLaunchKernelGGL(lanczos_tol_kernel<true>, dim3(pb.B), dim3(256), 2 * vbytes, s, a, L, pb.K);
+    const size_t fixed = (size_t)kLzWaves * 64 * sizeof(cd) + kLzWaves * sizeof(double);
+    if (2 * vbytes + fixed <= 160 * 1024)
+        hipLaunchKernelGGL(lanczos_tol_kernel<true>, dim3(pb.B), dim3(64 * kLzWaves), 2 * vbytes, s, a,
+                           L, pb.K);
     else
-        hipLaunchKernelGGL(lanczos_tol_kernel<false>, dim3(pb.B), dim3(256), vbytes, s, a, L, pb.K);
+        hipLaunchKernelGGL(lanczos_tol_kernel<false>, dim3(pb.B), dim3(64 * kLzWaves), vbytes, s, a,
+                           L, pb.K);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // R = G G^H, pivots at or below the cut dropped; B^H left untouched
     const TileExt exR{a.act, nullptr, 0};
-    for (int k = 0; k < nb; ++k) {
-        hipLaunchKernelGGL(act_kernel, dim3(pb.B), dim3(256), 0, s, a, L, k * TB);
-        if ((e = launch_tile_factor_step(pb, a, k, exR, s)) != hipSuccess) return e;
-    }
+    if ((e = launch_tile_factor(pb, a, exR, launch_act, s)) != hipSuccess) return e;
     // C = G^H G, c = G^H B^H
     hipLaunchKernelGGL(gram_kernel, dim3(nb * (nb + 1) / 2, pb.B), dim3(256), 0, s, a, L);
     hipLaunchKernelGGL(ghb_kernel, dim3(nb, pb.B), dim3(256), 0, s, a, L, pb.NR);
@@ -521,8 +552,7 @@ hipError_t launch_minnorm(const Problem& pb, const MstepArgs& a, hipStream_t s) 
     c.R = a.gram; c.rhs = a.grhs; c.theta = nullptr; c.tol = a.tol2; c.status = nullptr;
     c.solve_mode = SBCE_SOLVE_CHOL;
     const TileExt exC{a.act, a.act, 1};
-    for (int k = 0; k < nb; ++k)
-        if ((e = launch_tile_factor_step(pb, c, k, exC, s)) != hipSuccess) return e;
+    if ((e = launch_tile_factor(pb, c, exC, nullptr, s)) != hipSuccess) return e;
     if ((e = launch_tile_back(pb, c, a.act, s)) != hipSuccess) return e;
     const size_t upd_lds = (size_t)TB * (TB + 1) * sizeof(cd) + (size_t)TB * 8 * sizeof(cd);
     for (int k = 0; k < nb; ++k) {

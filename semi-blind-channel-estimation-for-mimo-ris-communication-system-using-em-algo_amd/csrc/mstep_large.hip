@@ -34,6 +34,7 @@ namespace {
 typedef double d4v __attribute__((ext_vector_type(4)));
 constexpr int TB = 64;      // tile of the blocked factorisation and of the R build
 constexpr int KS = 16;      // k-chunk staged in LDS by the tile GEMM
+constexpr int kTileGroup = 4;   // column blocks per trailing update (tile_herk_kernel K <= 256)
 
 __device__ __forceinline__ d4v mfma4(double a, double b, d4v c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -529,6 +530,136 @@ __global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int 
     }
 }
 
+// ---------------------------------------------------------------- grouped trailing update
+// A_ij -= sum_{k in [kb_lo, kb_lo + nkb)} L_ik L_jk^H on the 64 x 64 tiles (i, j) with
+// j in [tj_lo, tj_hi), i >= j: the K loop runs over up to nkb column blocks inside the kernel,
+// so a tile's accumulator makes ONE trip through HBM per group of column blocks instead of
+// one per block (tile_gemm_kernel<HERK> with K = 64 moved 18x the algorithmic bytes at cfg 2).
+// Blocks of one trial sit on one XCD (block id % 8) so the panel rows the trial's tiles share
+// are L2 hits.  ext.col: K and the tiles are clipped to the trial's active extent (min-norm
+// early exit: columns past it are dropped and never read again).
+__global__ __launch_bounds__(256) void tile_herk_kernel(MstepArgs a, int L, int kb_lo, int nkb,
+                                                        int tj_lo, int tj_hi, int ntiles,
+                                                        TileExt ext) {
+    __shared__ cd As[TB][KS + 1], Bs[TB][KS + 1];
+    const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
+    const int b = (slot / ntiles) * 8 + xcd, tix = slot - (slot / ntiles) * ntiles;
+    if (b >= a.nbatch) return;
+    if (a.done && a.done[b]) return;
+    const int nb = (L + TB - 1) / TB;
+    int ti, tj;
+    if (tj_hi >= nb) {                      // the whole trailing triangle from tj_lo
+        int x = (int)((sqrt(8.0 * tix + 1.0) - 1.0) * 0.5);
+        while ((x + 1) * (x + 2) / 2 <= tix) ++x;
+        while (x * (x + 1) / 2 > tix) --x;
+        ti = tj_lo + x;
+        tj = tj_lo + (tix - x * (x + 1) / 2);
+    } else {                                // a few columns: tiles column by column
+        int t = tix;
+        tj = tj_lo;
+        while (t >= nb - tj) { t -= nb - tj; ++tj; }
+        ti = tj + t;
+    }
+    const int k0 = kb_lo * TB;
+    int kend = (kb_lo + nkb) * TB < L ? (kb_lo + nkb) * TB : L;
+    if (ext.col) {
+        const int act = ext.col[b];
+        if (tj * TB >= act) return;         // dropped columns: never read again
+        kend = kend < act ? kend : act;
+    }
+    if (k0 >= kend) return;
+    if (ext.row && ti * TB >= ext.row[b]) return;
+    cd* R = a.R + (size_t)b * L * L;
+    const int r0 = ti * TB, c0 = tj * TB;
+    const cd* Arow = R + (size_t)r0 * L;
+    const cd* Brow = R + (size_t)c0 * L;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
+
+    d4v cre[2][2], cim[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int r = r0 + wr + 16 * u + lk + 4 * q, c = c0 + wc + 16 * v + li;
+                const cd x = (r < L && c < L) ? R[(size_t)r * L + c] : czero();
+                cre[u][v][q] = x.x;
+                cim[u][v][q] = x.y;
+            }
+    constexpr int PF = TB * KS / 256;               // entries per thread and operand
+    cd pa[PF], pbv[PF];
+    auto fetch = [&](int kc) {
+#pragma unroll
+        for (int h = 0; h < PF; ++h) {
+            const int e = tid + 256 * h, r = e / KS, k = e - r * KS;
+            const bool kin = kc + k < kend;
+            pa[h] = (kin && r0 + r < L) ? Arow[(size_t)r * L + kc + k] : czero();
+            pbv[h] = (kin && c0 + r < L) ? Brow[(size_t)r * L + kc + k] : czero();
+        }
+    };
+    fetch(k0);
+    for (int kc = k0; kc < kend; kc += KS) {
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < PF; ++h) {
+            const int e = tid + 256 * h, r = e / KS, k = e - r * KS;
+            As[r][k] = pa[h];
+            Bs[r][k] = pbv[h];
+        }
+        __syncthreads();
+        if (kc + KS < kend) fetch(kc + KS);
+#pragma unroll
+        for (int s4 = 0; s4 < KS / 4; ++s4) {
+            cd av[2], bv[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) av[u] = As[wr + 16 * u + li][4 * s4 + lk];
+#pragma unroll
+            for (int v = 0; v < 2; ++v) bv[v] = Bs[wc + 16 * v + li][4 * s4 + lk];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    // C -= A conj(B)^T:  re -= ar br + ai bi ; im -= ai br - ar bi
+                    cre[u][v] = mfma4(-av[u].x, bv[v].x, cre[u][v]);
+                    cre[u][v] = mfma4(-av[u].y, bv[v].y, cre[u][v]);
+                    cim[u][v] = mfma4(-av[u].y, bv[v].x, cim[u][v]);
+                    cim[u][v] = mfma4(av[u].x, bv[v].y, cim[u][v]);
+                }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int r = r0 + wr + 16 * u + lk + 4 * q, c = c0 + wc + 16 * v + li;
+                if (r < L && c < L) R[(size_t)r * L + c] = cmk(cre[u][v][q], cim[u][v][q]);
+            }
+}
+
+// dvec[b][j] -= sum_{m in [c0, c1)} |L[j][m]|^2 for rows j >= r0 = c1 (c1 clipped to the active
+// extent): the diagonal of the Schur complement after a group, for the min-norm early exit.
+// One wave per row (coalesced row segments), lanes reduced in a fixed order.
+__global__ __launch_bounds__(256) void dvec_kernel(MstepArgs a, int L, int c0, int r0, TileExt ext) {
+    const int b = blockIdx.y;
+    if (a.done && a.done[b]) return;
+    int c1 = r0;
+    if (ext.col) c1 = c1 < ext.col[b] ? c1 : ext.col[b];
+    if (c0 >= c1) return;
+    const int j = r0 + blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (j >= L) return;
+    const cd* row = a.R + (size_t)b * L * L + (size_t)j * L;
+    double sq = 0.0;
+    for (int m = c0 + lane; m < c1; m += 64) sq += cabs2(row[m]);
+    for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
+    if (lane == 0) a.dvec[(size_t)b * L + j] -= sq;
+}
+
 // ---------------------------------------------------------------- back substitution
 // L^H x = y by 64-column blocks from the last: backdiag_kernel (one workgroup per trial)
 // solves the diagonal tile, x_k = L_kk^{-H} y_k, in 16-row blocks through the inverses kept
@@ -681,6 +812,19 @@ hipError_t launch_diag_tol(const Problem& pb, const MstepArgs& a, hipStream_t s)
     return hipGetLastError();
 }
 
+static hipError_t launch_herk(const Problem& pb, const MstepArgs& a, int kb_lo, int nkb, int tj_lo,
+                              int tj_hi, const TileExt& ex, hipStream_t s) {
+    const int nb = (pb.L + TB - 1) / TB;
+    long ntiles = 0;
+    for (int tj = tj_lo; tj < tj_hi; ++tj) ntiles += nb - tj;
+    if (ntiles <= 0) return hipSuccess;
+    const long nblk = 8L * ((pb.B + 7) / 8) * ntiles;
+    if (nblk > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(tile_herk_kernel, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L, kb_lo, nkb,
+                       tj_lo, tj_hi, (int)ntiles, ex);
+    return hipGetLastError();
+}
+
 hipError_t launch_tile_factor_step(const Problem& pb, const MstepArgs& a, int k, const TileExt& ex,
                                    hipStream_t s) {
     const int nb = (pb.L + TB - 1) / TB;
@@ -691,13 +835,44 @@ hipError_t launch_tile_factor_step(const Problem& pb, const MstepArgs& a, int k,
     const size_t inv_lds = (size_t)TB * TB * sizeof(cd) + (size_t)TB * 8 * sizeof(cd);
     hipLaunchKernelGGL(tile_inverse_kernel, dim3(pb.B), dim3(64), inv_lds, s, a, pb.L, k0, w, pb.NR, ex);
     const int below = nb - k - 1;
-    if (below > 0) {
+    if (below > 0)
         hipLaunchKernelGGL(tile_gemm_kernel<false>, dim3(below, pb.B), dim3(256), 0, s, a, pb.L, k,
                            pb.NR, ex);
-        hipLaunchKernelGGL(tile_gemm_kernel<true>, dim3(below * (below + 1) / 2, pb.B), dim3(256),
-                           0, s, a, pb.L, k, pb.NR, ex);
-    }
     return hipGetLastError();
+}
+
+// Blocked LEFT-looking factorisation by groups of kTileGroup column blocks (256 columns): per
+// group, ONE update of the group's columns (rows below them too) by every earlier column
+// (tile_herk_kernel, the K loop in the kernel), then per block k of the group the diagonal
+// tile, its inverse, the TRSM tiles below it and the narrow update of the group's remaining
+// columns by block k.  No trailing update is ever made: on a rank-deficient R (the min-norm
+// solve) the columns past the numerical rank are never touched, so the work stops at the
+// rank (cfg 4: ~530 of 4100 columns) instead of sweeping the whole trailing matrix.
+// act_check (min-norm): before each group, act_kernel ends a trial's factorisation when the
+// Schur complement's diagonal (a.dvec, kept current by dvec_kernel) is below the cut.
+hipError_t launch_tile_factor(const Problem& pb, const MstepArgs& a, const TileExt& ex,
+                              hipError_t (*act_check)(const Problem&, const MstepArgs&, int, hipStream_t),
+                              hipStream_t s) {
+    const int nb = (pb.L + TB - 1) / TB;
+    hipError_t e;
+    for (int g0 = 0; g0 < nb; g0 += kTileGroup) {
+        const int g1 = (g0 + kTileGroup) < nb ? (g0 + kTileGroup) : nb;
+        if (act_check && (e = act_check(pb, a, g0 * TB, s)) != hipSuccess) return e;
+        if (g0 > 0 && (e = launch_herk(pb, a, 0, g0, g0, g1, ex, s)) != hipSuccess) return e;
+        for (int k = g0; k < g1; ++k) {
+            if ((e = launch_tile_factor_step(pb, a, k, ex, s)) != hipSuccess) return e;
+            if (k + 1 < g1 && (e = launch_herk(pb, a, k, 1, k + 1, g1, ex, s)) != hipSuccess)
+                return e;
+        }
+        if (act_check && g1 < nb) {
+            // the Schur complement's diagonal past the group: dvec[j] -= sum_{m in group} |L_jm|^2
+            const int r0 = g1 * TB;
+            hipLaunchKernelGGL(dvec_kernel, dim3((pb.L - r0 + 3) / 4, pb.B), dim3(256), 0, s, a,
+                               pb.L, g0 * TB, r0, ex);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_tile_back(const Problem& pb, const MstepArgs& a, const int32_t* ext, hipStream_t s) {
@@ -719,10 +894,8 @@ hipError_t launch_chol_large(const Problem& pb, const MstepArgs& a, hipStream_t 
     if (pb.NR > 8) return hipErrorInvalidValue;
     hipError_t e = launch_diag_tol(pb, a, s);
     if (e != hipSuccess) return e;
-    const int nb = (pb.L + TB - 1) / TB;
     const TileExt full{nullptr, nullptr, 1};
-    for (int k = 0; k < nb; ++k)
-        if ((e = launch_tile_factor_step(pb, a, k, full, s)) != hipSuccess) return e;
+    if ((e = launch_tile_factor(pb, a, full, nullptr, s)) != hipSuccess) return e;
     return launch_tile_back(pb, a, nullptr, s);
 }
 

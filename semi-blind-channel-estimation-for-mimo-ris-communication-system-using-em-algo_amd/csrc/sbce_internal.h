@@ -180,6 +180,7 @@ struct MstepArgs {
     cd* grhs;          // [B][L][NR] G^H B^H, then the solves with C in place
     int32_t* act;      // [B]  active extent: columns of G past act[b] are all dropped
     double* tol2;      // [B]  pivot threshold of C's Cholesky
+    double* dvec;      // [B][L] diagonal of R's Schur complement (left-looking early exit)
 };
 
 // Per-trial extents of one tiled-factorisation launch sequence (mstep_large.hip): column
@@ -211,10 +212,15 @@ hipError_t launch_chol_large(const Problem& pb, const MstepArgs& a, hipStream_t 
 hipError_t launch_diag_tol(const Problem& pb, const MstepArgs& a, hipStream_t s);  // a.tol[b]
 hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w, const int32_t* ext,
                             hipStream_t s);
-// one column block k of the tiled right-looking factorisation: diagonal tile, its inverse,
-// the TRSM tiles below it and the trailing HERK update
+// one column block k of the tiled right-looking factorisation: diagonal tile, its inverse and
+// the TRSM tiles below it (the trailing updates are launch_tile_factor's)
 hipError_t launch_tile_factor_step(const Problem& pb, const MstepArgs& a, int k, const TileExt& e,
                                    hipStream_t s);
+// the whole tiled factorisation, trailing updates grouped (mstep_large.hip); act_check, when
+// given, runs before each column block (the min-norm early exit)
+hipError_t launch_tile_factor(const Problem& pb, const MstepArgs& a, const TileExt& e,
+                              hipError_t (*act_check)(const Problem&, const MstepArgs&, int, hipStream_t),
+                              hipStream_t s);
 // L^H x = y on a.rhs by 64-column blocks (theta = conj(x) written when a.theta != null)
 hipError_t launch_tile_back(const Problem& pb, const MstepArgs& a, const int32_t* ext, hipStream_t s);
 // minimum-norm solve (SBCE_SOLVE_MINNORM, minnorm.hip): R, rhs built; writes theta

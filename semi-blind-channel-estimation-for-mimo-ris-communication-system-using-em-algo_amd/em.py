@@ -484,9 +484,10 @@ def estep_batch(y_d, psi_d, cons, theta, varn, n_tx, mode="soft", partition_r=0,
     return mom[..., :n_tx], mom[..., n_tx:].reshape(B, T_d, n_tx, n_tx)
 
 
-def mstep_batch(y_d, y_p, psi_d, u_p, cons, m, S, varn, solve="chol"):
+def mstep_batch(y_d, y_p, psi_d, u_p, cons, m, S, varn, solve="chol", return_tol=False):
     """One device M-step (sbce_mstep) from given moments: returns theta (B,K),
-    R (B,L,L), rhs (B,L,n_rx), status (B,)."""
+    R (B,L,L), rhs (B,L,n_rx), status (B,) [, tol (B,): the min-norm pivot threshold
+    32 eps K lambda_max(R) (sbce_debug_minnorm_tol), return_tol=True with solve='lstsq']."""
     torch = _torch()
     lib = _lib.load()
     B, T_d, n_rx = np.shape(y_d)
@@ -502,13 +503,22 @@ def mstep_batch(y_d, y_p, psi_d, u_p, cons, m, S, varn, solve="chol"):
     stream = torch.cuda.current_stream().cuda_stream
     _lib.check(lib.sbce_mstep(dims, ptrs, Mo.data_ptr(), _SOLVES[solve], R.data_ptr(),
                               rhs.data_ptr(), stream), "sbce_mstep")
+    tol = None
+    if return_tol:
+        tol = np.zeros(B)
+        fn = lib.sbce_debug_minnorm_tol
+        fn.restype = ctypes.c_int
+        torch.cuda.current_stream().synchronize()
+        _lib.check(fn(ctypes.byref(dims), ctypes.byref(ptrs), tol.ctypes.data_as(ctypes.c_void_p),
+                      ctypes.c_void_p(stream)), "sbce_debug_minnorm_tol")
     torch.cuda.current_stream().synchronize()
     th = keep[5].cpu().numpy()
     # the device keeps only R's lower triangle (its strict upper part is factorisation
     # workspace): return the Hermitian completion
     R = np.tril(R.cpu().numpy())
     R = R + np.conj(np.swapaxes(np.tril(R, -1), 1, 2))
-    return th, R, rhs.cpu().numpy(), keep[7].cpu().numpy()
+    out = (th, R, rhs.cpu().numpy(), keep[7].cpu().numpy())
+    return out + (tol,) if return_tol else out
 
 
 def nmse_batch(theta, h):

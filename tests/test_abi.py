@@ -98,8 +98,9 @@ def test_workspace_and_validation_without_gpu(sbce):
               + 1000 * Lw * 4 * 16                        # pilot part of B^H (once per run)
               + 1000 * 64 * 64 * 16                       # tiled factorisation: tile inverse
               + 1000 * Lw * Lw * 16 + 1000 * Lw * 4 * 16  # min-norm solve: C = G^H G, G^H B^H
-              + 1000 * 4 + 1000 * 8)                      # min-norm: extents, C's threshold
-    assert expect <= n <= expect + 13 * 256 + 4000
+              + 1000 * 4 + 1000 * 8                       # min-norm: extents, C's threshold
+              + 1000 * Lw * 8)                            # min-norm: Schur-complement diagonal
+    assert expect <= n <= expect + 14 * 256 + 4000
     bad = L.Dims(1, 9, 4, 65, 16, 256, 16, 0, 0.1)     # n_tx > 8
     nb = ctypes.c_size_t(0)
     assert lib.sbce_workspace_bytes(ctypes.byref(bad), ctypes.byref(nb)) == -1

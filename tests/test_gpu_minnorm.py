@@ -59,6 +59,43 @@ def test_minnorm_rank_deficient_vs_lstsq(sbce, shape):
         assert not st[i] & sbce._lib.SBCE_STATUS_RANK       # exact rank deficiency: clean gap
 
 
+def _lanczos_lambda(R, steps=4):
+    """4 Lanczos steps from the normalised ones vector (minnorm.hip lanczos_tol_kernel)."""
+    L = R.shape[0]
+    v = np.ones(L, complex) / np.sqrt(L)
+    vp = np.zeros(L, complex)
+    beta, al, be = 0.0, [], []
+    for _ in range(steps):
+        w = R @ v
+        a = np.vdot(v, w).real
+        w = w - a * v - beta * vp
+        beta = np.linalg.norm(w)
+        al.append(a)
+        be.append(beta)
+        vp, v = v, w / beta
+    T = np.diag(al) + np.diag(be[:-1], 1) + np.diag(be[:-1], -1)
+    return np.linalg.eigvalsh(T)[-1]
+
+
+@pytest.mark.parametrize("shape", [(2, 2, 32, 12, 20), (4, 4, 149, 16, 200), (8, 8, 80, 32, 90)])
+def test_minnorm_cut_from_lanczos(sbce, shape):
+    """The device's pivot threshold is 32 eps K max(lambda_4, max diag R), lambda_4 the largest
+    Ritz value of 4 Lanczos steps from the ones vector (the same recurrence in numpy), and
+    lambda_4 brackets lambda_max(R) from below within 20 %."""
+    n_tx, n_rx, N, T_p, T_d = shape
+    b = sbce.signal_model.synthetic_batch(2, n_tx, n_rx, N, T_p, T_d, 16, 0.05, seed=23)
+    m, S = _hard_moments(b["x_d"])
+    th, R, rhs, st, tol = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"],
+                                           m, S, 0.05, solve="lstsq", return_tol=True)
+    L = R.shape[1]
+    for i in range(2):
+        lam = max(_lanczos_lambda(R[i]), R[i].diagonal().real.max())
+        want = 32 * EPS * L * n_rx * lam
+        assert abs(tol[i] / want - 1) < 1e-9, (tol[i], want)
+        lmax = np.linalg.eigvalsh(R[i])[-1]
+        assert 0.8 * lmax <= lam <= lmax * (1 + 1e-12)
+
+
 @pytest.mark.parametrize("shape", [(2, 2, 8, 12, 40), (4, 4, 16, 16, 80), (4, 4, 149, 16, 700)])
 def test_minnorm_equals_solve_on_hpd_systems(sbce, shape):
     """Full-rank R: the minimum-norm solution is the unique solution (np.linalg.solve)."""
