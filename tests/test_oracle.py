@@ -504,3 +504,14 @@ def test_llf_driver_replays_reference(sbce):
                          varn)
                for th_l in trace]
         assert np.allclose(llf, d[f"llf{i}"], rtol=1e-11, atol=0)
+
+
+def test_oracle_matches_reference_at_cfg1_kernel_instantiation():
+    """n_tx = n_rx = 4, 16-QAM (J = 65,536, the cfg-1 E-step) through the reference em()
+    itself (tests/golden/make_golden.py case_cfg1_kernel): the reduced-form oracle agrees."""
+    d = golden("cfg1_kernel")
+    n_rx = int(d["n_rx"])
+    Up = u_from_zp(d["Z_p"], n_rx)
+    for it in (1, int(d["itera"])):
+        th = em_reduced(d["Y_d"], d["Y_p"], Up, d["Ptd"], d["aps"], float(d["varn"]), it, d["h0"])
+        assert rel(th, d[f"theta_it{it}"]) < 1e-11, it
