@@ -67,15 +67,20 @@ def metric_name(n_tx, N, T_p, T_d):
 
 
 # kernels of one E-step / M-step launch sequence (rocprofv3 names, tools/pmc_summary.py keys)
-ESTEP_KERNELS = ["estep_tree_kernel", "estep_bfs_kernel", "estep_bounds_kernel", "estep_prep_kernel",
+ESTEP_KERNELS = ["estep_tree_kernel", "estep_bfs_kernel", "estep_pair_kernel", "estep_bounds_kernel", "estep_prep_kernel",
                  "estep_mfma_kernel_occ3", "estep_mfma_kernel"]
-MSTEP_KERNELS = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_kernel", "rhs_lds_kernel",
+MSTEP_KERNELS = ["pilot_factor_kernel", "pilot_rhs_kernel", "rbuild_herm_kernel", "rbuild_kernel", "rhs_lds_kernel",
                  "rhs_dma_kernel", "rhs_kernel", "diag_tol_kernel", "panel_update_kernel", "panel_factor_kernel",
                  "backsub_kernel", "backsub2_kernel", "backsub3_kernel",
                  "backsub4_kernel", "chol_mfma_kernel"]
-MSTEP_KERNELS_LARGE = ["pilot_factor_kernel", "rbuild_herm_kernel", "rbuild_wide_kernel",
-                       "rhs_kernel", "diag_tol_kernel", "chol_mfma_kernel", "tile_inverse_kernel",
-                       "tile_gemm_kernel", "backdiag_kernel", "backupd_kernel"]
+MSTEP_KERNELS_LARGE = ["pilot_factor_kernel", "pilot_rhs_kernel", "rbuild_herm_kernel",
+                       "rbuild_wide_kernel", "rhs_kernel", "rhs_dma_kernel", "rhs_lds_kernel",
+                       "diag_tol_kernel", "chol_mfma_kernel", "tile_inverse_kernel",
+                       "tile_gemm_kernel", "tile_herk_kernel", "dvec_kernel", "act_kernel",
+                       "backdiag_kernel", "backupd_kernel",
+                       # the minimum-norm solve (csrc/minnorm.hip)
+                       "lanczos_tol_kernel", "gram_kernel", "gram_tol_kernel", "ghb_kernel",
+                       "fwddiag_kernel", "fwdupd_kernel", "gz_kernel"]
 # launched exactly once per M-step (the divisor of the phase's PMC totals; the pilot
 # factorisation runs once per EM run, so its bytes are spread over the run's M-steps)
 MSTEP_ANCHORS = ["rhs_dma_kernel", "rhs_lds_kernel", "rhs_kernel"]
@@ -339,17 +344,22 @@ def main():
         cnt = ctypes.c_ulonglong(0)
         sph = (ctypes.c_ulonglong * 3)()
         with pkg._lib.debug_env(SBCE_ESTEP_COUNT="1"):
+            npair = ctypes.c_ulonglong(0)
             lib.sbce_debug_estep_mfma(None, 1)
             lib.sbce_debug_estep_sphere(None, 1)
+            lib.sbce_debug_estep_pair(None, 1)
             eng.estep()
             torch.cuda.synchronize()
             lib.sbce_debug_estep_mfma(ctypes.byref(cnt), 0)
             lib.sbce_debug_estep_sphere(sph, 0)
+            lib.sbce_debug_estep_pair(ctypes.byref(npair), 0)
         mfma_issued = int(cnt.value)
         nsym = float(B * T_d)
-        # where the symbols' posteriors were computed: single surviving path
-        # in the tree pass, breadth-first enumeration, or the MFMA tile sweep
-        sphere = {"single_path": sph[2] / nsym, "enumerated": sph[0] / nsym, "swept": sph[1] / nsym}
+        # where the symbols' posteriors were computed: single surviving
+        # path in the tree pass, breadth-first enumeration, factorised weights (the listed
+        # symbols of a wide posterior), or the MFMA tile sweep
+        sphere = {"single_path": sph[2] / nsym, "enumerated": sph[0] / nsym,
+                  "factorised": npair.value / nsym, "swept": (sph[1] - npair.value) / nsym}
     e0.record(stream)
     for _ in range(args.kernel_reps):
         eng.mstep()

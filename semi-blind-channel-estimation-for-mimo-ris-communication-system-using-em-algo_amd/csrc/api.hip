@@ -17,7 +17,7 @@ DebugConfig g_debug;
 
 namespace {
 constexpr DebugConfig kDebugDefault = {false, false, false, 4, false, false, false, false, 128,
-                                       0, false, false, 0, 0};
+                                       0, false, false, 0, 0, false};
 constexpr int kSphereBudgetMax = 256;      // estep.hip kBfsPmax
 
 void read_debug_env(DebugConfig& c) {
@@ -41,6 +41,7 @@ void read_debug_env(DebugConfig& c) {
     if ((v = env("SBCE_UPD_WAVES"))) c.upd_waves8 = v[0] == '8';
     if ((v = env("SBCE_BACKSUB"))) c.backsub = (v[0] >= '1' && v[0] <= '3') ? v[0] - '0' : 0;
     if ((v = env("SBCE_CHOL_IMPL"))) c.chol_impl = (v[0] == 'v' || v[0] == 'f') ? v[0] : 0;
+    if ((v = env("SBCE_ESTEP_PAIR"))) c.estep_nopair = v[0] == '0';
 }
 
 __attribute__((constructor)) void load_debug_env() { read_debug_env(g_debug); }
@@ -54,7 +55,8 @@ bool debug_nondefault() {
            c.estep_occ2 != d.estep_occ2 || c.prep_nouni != d.prep_nouni ||
            c.estep_nosphere != d.estep_nosphere || c.sphere_budget != d.sphere_budget ||
            c.rhs_impl != d.rhs_impl || c.rb_tc32 != d.rb_tc32 || c.upd_waves8 != d.upd_waves8 ||
-           c.backsub != d.backsub || c.chol_impl != d.chol_impl || (chol_debug_skip_mask() & 31);
+           c.backsub != d.backsub || c.chol_impl != d.chol_impl || c.estep_nopair != d.estep_nopair ||
+           (chol_debug_skip_mask() & 31);
 }
 
 }  // namespace sbce
@@ -96,7 +98,7 @@ Carve carve(const Problem& pb) {
     const int ps = estep_prep_stride(pb);
     c.has_prep = ps > 0;
     c.list = align_up(c.prep + (size_t)pb.B * pb.Td * ps * sizeof(double));
-    c.tree = align_up(c.list + (2 * (size_t)pb.B * pb.Td + kEstepListCnt) * sizeof(int32_t));
+    c.tree = align_up(c.list + (3 * (size_t)pb.B * pb.Td + 2 * kEstepListCnt) * sizeof(int32_t));
     c.tol = c.has_prep ? align_up(c.tree + (size_t)pb.B * pb.Td * kTreeRecDoubles * sizeof(double))
                        : c.list;
     c.ppsi = c.pS = c.pflag = c.winv = c.tol;
@@ -412,6 +414,13 @@ int sbce_debug_estep_mfma(unsigned long long* out, int reset) {
 int sbce_debug_estep_sphere(unsigned long long* out3, int reset) {
     if (!reset && !out3) return SBCE_EINVAL;
     return hip_rc(estep_debug_sphere(out3, reset));
+}
+
+// Diagnostic, not part of include/sbce.h: listed symbols the factorised-weight pass resolved
+// (estep_pair.hip) since the last reset (counted only with SBCE_ESTEP_COUNT=1).
+int sbce_debug_estep_pair(unsigned long long* out, int reset) {
+    if (!reset && !out) return SBCE_EINVAL;
+    return hip_rc(estep_debug_pair(out, reset));
 }
 
 int sbce_ser(const sbce_dims* d, const void* x_dest, const void* x_d_true, double* ser_out,

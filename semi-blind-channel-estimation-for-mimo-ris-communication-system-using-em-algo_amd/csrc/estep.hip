@@ -1242,6 +1242,7 @@ struct PrepConst {
     int budget;        // DFS steps per symbol before the symbol is left to the sweep
     int count;         // SBCE_ESTEP_COUNT=1: tally resolved / listed symbols (g_estep_sphere)
     int hard;          // hard (argmin) E-step: sphere radius without the soft threshold
+    int pair;          // route wide-tree symbols that pass the screen to the factorised pass
     double inv_s2, thr_d;
 };
 
@@ -1328,7 +1329,7 @@ template <int NT, int NR>
 __device__ __forceinline__ double prep_candidate(const cd (&H)[NT][NR], const cd (&y)[NR],
                                                  const cd (&Lm)[NT][NT], const double (&dinv)[NT],
                                                  const cd (&zf)[NT], const cd* cons, int M,
-                                                 double& sc) {
+                                                 double& sc, cd (&x)[NT]) {
     cd z[NT];
 #pragma unroll
     for (int i = 0; i < NT; ++i) z[i] = zf[i];
@@ -1339,7 +1340,6 @@ __device__ __forceinline__ double prep_candidate(const cd (&H)[NT][NR], const cd
         for (int k = i + 1; k < NT; ++k) s = csub(s, cmul(cconj(Lm[k][i]), z[k]));
         z[i] = cscale(s, dinv[i]);
     }
-    cd x[NT];
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
         double bd = INFINITY;
@@ -1366,6 +1366,32 @@ __device__ __forceinline__ double prep_candidate(const cd (&H)[NT][NR], const cd
         d0 += cabs2(res);
     }
     return d0;
+}
+
+// Screen of the factorised-weight pass (estep_pair.hip), NT = 4: a lower bound of its range
+// test D = sum_f (max f - f(x_c)) from the four cross-stream log tables alone,
+// E_ab(x_a, x_b) = -2 Re(conj(x_a) h_a^H h_b x_b) / s2: the constellation holds -x_a, so
+// max E_ab >= |E_ab(x_c)| and each term is >= 2 max(0, -E_ab(x_c)).  A symbol whose screen
+// exceeds the pass's limit goes to the sweep without its tables being built.
+template <int NT, int NR>
+__device__ __forceinline__ double pair_screen(const cd (&H)[NT][NR], const cd (&x)[NT], double inv_s2) {
+    if constexpr (NT != 4) {
+        return INFINITY;
+    } else {
+        double lo = 0.0;
+#pragma unroll
+        for (int a0 = 0; a0 < 2; ++a0)
+#pragma unroll
+            for (int b0 = 2; b0 < 4; ++b0) {
+                cd G = czero();
+#pragma unroll
+                for (int r = 0; r < NR; ++r) G = cfmac(G, H[b0][r], H[a0][r]);    // h_a^H h_b
+                const cd t = cmul(G, x[b0]);
+                const double e = -2.0 * inv_s2 * fma(x[a0].x, t.x, x[a0].y * t.y);
+                lo += 2.0 * fmax(0.0, -e);
+            }
+        return lo;
+    }
 }
 
 // Column-tile bounds (column_tile_bounds) and, for NT = 4, the row-tile bound vectors of
@@ -1564,7 +1590,8 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
     cd Lm[NT][NT], zf[NT];
     double piv[NT], dinv[NT], sc;
     ridge_chol<NT, NR>(H, y, c.reg, Lm, piv, dinv, zf);
-    out[0] = prep_candidate<NT, NR>(H, y, Lm, dinv, zf, cons, c.M, sc);
+    cd xc[NT];
+    out[0] = prep_candidate<NT, NR>(H, y, Lm, dinv, zf, cons, c.M, sc, xc);
     out[1] = sc;
     prep_bounds<NT, NR>(H, y, out, cons, c);
 }
@@ -1629,7 +1656,7 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
     bool single = false;
     if (live) {
     cd Lm[NT][NT], zf[NT];
-    double piv[NT], dinv[NT], d0, sc;
+    double piv[NT], dinv[NT], d0, sc, screen;
     int lev[NT];
     double c0 = 0.0;
     {
@@ -1646,9 +1673,11 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
                 out[5 + 2 * (q * NR + r)] = H[q][r].y;
             }
         ridge_chol<NT, NR>(H, y, c.reg, Lm, piv, dinv, zf);
-        d0 = prep_candidate<NT, NR>(H, y, Lm, dinv, zf, cons, c.M, sc);
+        cd xc[NT];
+        d0 = prep_candidate<NT, NR>(H, y, Lm, dinv, zf, cons, c.M, sc, xc);
         out[0] = d0;
         out[1] = sc;
+        screen = pair_screen<NT, NR>(H, xc, c.inv_s2);
         // reliability of stream q: g_q = [(G + reg I)^-1]_qq = sum_k |(L^-1)_kq|^2
         cd W[NT][NT];
         double g[NT];
@@ -1780,6 +1809,7 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
     rec[1] = R0;
     rec[2] = sc;
     rec[3] = (double)packed;
+    rec[kTrec - 1] = screen;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
         rec[4 + j] = ui[j];
@@ -1845,7 +1875,7 @@ __global__ __launch_bounds__(64 * kBfsWaves) void estep_bfs_kernel(EstepArgs a, 
     const int mask = c.M - 1, lm = c.lm;
     const int pmax = c.budget < kBfsPmax ? c.budget : kBfsPmax;
     const u64 lt = (1ull << lane) - 1ull;
-    unsigned listed_mask = 0, resolved_n = 0;
+    unsigned listed_mask = 0, pair_mask = 0, resolved_n = 0;
     // tree records by LDS-DMA, the next symbol's in flight while the current one is enumerated
     // (lanes 0-15 carry the record's 256 bytes; the others re-read its first 16 bytes)
     __shared__ __attribute__((aligned(16))) double s_rec[kBfsWaves][2][128];
@@ -1983,19 +2013,27 @@ __global__ __launch_bounds__(64 * kBfsWaves) void estep_bfs_kernel(EstepArgs a, 
                 }
             }
         }
+        // a listed symbol whose screen admits the factorised-weight pass goes to that pass
+        const bool to_pair = listed && c.pair && rec[kTrec - 1] <= kPairDmax;
         wave_sync();
-        if (listed) listed_mask |= 1u << (gi - g0);
+        if (to_pair) pair_mask |= 1u << (gi - g0);
+        else if (listed) listed_mask |= 1u << (gi - g0);
         else ++resolved_n;
     }
-    // the wave's listed symbols join the sweep's work list: one atomic per wave
-    const int nl = __builtin_popcount(listed_mask);
-    if (nl) {
+    // the wave's listed symbols join the sweep's (or the factorised pass's) work list: one
+    // atomic per wave and list
+    auto append = [&](unsigned msk, int32_t* cntp, int32_t* lst) {
+        const int n = __builtin_popcount(msk);
+        if (!n) return;
         int base = 0;
-        if (lane == 0) base = atomicAdd(a.list + nsym, nl);
+        if (lane == 0) base = atomicAdd(cntp, n);
         base = __shfl(base, 0);
-        if (lane < kBfsSpw && ((listed_mask >> lane) & 1))
-            a.list[base + __builtin_popcount(listed_mask & ((1u << lane) - 1u))] = elist[g0 + lane];
-    }
+        if (lane < kBfsSpw && ((msk >> lane) & 1))
+            lst[base + __builtin_popcount(msk & ((1u << lane) - 1u))] = elist[g0 + lane];
+    };
+    append(listed_mask, a.list + nsym, a.list);
+    append(pair_mask, a.list + nsym + 3, a.list + 2 * nsym + 2 * kEstepListCnt);
+    const int nl = __builtin_popcount(listed_mask) + __builtin_popcount(pair_mask);
     if (c.count && lane == 0) {
         atomicAdd(&g_estep_sphere[0], (unsigned long long)resolved_n);
         atomicAdd(&g_estep_sphere[1], (unsigned long long)nl);
@@ -2240,13 +2278,14 @@ hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStre
             pc.inv_s2 = mc.inv_s2;
             pc.thr_d = mc.thr_d;
             pc.hard = mode == SBCE_ESTEP_HARD;
+            pc.pair = estep_pair_supported(pb, mode) ? 1 : 0;
             if (!sphere) as.list = nullptr;
             const long nsym = (long)pb.B * pb.Td;
             const dim3 pg((unsigned)((nsym + 255) / 256)), pblk(256);
             hipError_t e = hipErrorInvalidValue;
             if (sphere) {
                 // sphere pass (tree records, enumeration), then the tile bounds of the listed
-                const hipError_t me = hipMemsetAsync(a.list + nsym, 0, 3 * sizeof(int32_t), s);
+                const hipError_t me = hipMemsetAsync(a.list + nsym, 0, 5 * sizeof(int32_t), s);
                 if (me != hipSuccess) return me;
                 const long nbfs = (nsym + kBfsSpw * kBfsWaves - 1) / (kBfsSpw * kBfsWaves);
                 const dim3 bg((unsigned)nbfs), bblk(64 * kBfsWaves);
@@ -2257,8 +2296,6 @@ hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStre
     if (hard) hipLaunchKernelGGL((estep_bfs_kernel<nt, 2>), bg, bblk, 0, s, as, pc); \
     else hipLaunchKernelGGL((estep_bfs_kernel<nt, 1>), bg, bblk, 0, s, as, pc); \
     e = hipGetLastError(); \
-    if (e == hipSuccess) { hipLaunchKernelGGL((estep_bounds_kernel<nt, nr>), pg, pblk, 0, s, as, pc); \
-                           e = hipGetLastError(); } \
     break;
                     SBCE_SPH(2, 2) SBCE_SPH(2, 3) SBCE_SPH(2, 4) SBCE_SPH(2, 5)
                     SBCE_SPH(2, 6) SBCE_SPH(2, 7) SBCE_SPH(2, 8)
@@ -2266,6 +2303,22 @@ hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStre
                     SBCE_SPH(3, 8)
                     SBCE_SPH(4, 4) SBCE_SPH(4, 5) SBCE_SPH(4, 6) SBCE_SPH(4, 7) SBCE_SPH(4, 8)
 #undef SBCE_SPH
+                }
+                // wide posteriors of the cfg-1 geometry: the factorised-weight pass resolves the
+                // symbols the enumeration routed to it and lists the ones it cannot represent
+                // for the tile bounds and the sweep
+                if (e == hipSuccess && pc.pair) e = launch_estep_pair(pb, as, mc.prep_stride, mc.count, s);
+                if (e == hipSuccess) {
+                    switch (pb.NT * 16 + pb.NR) {
+#define SBCE_BND(nt, nr) case nt * 16 + nr: \
+    hipLaunchKernelGGL((estep_bounds_kernel<nt, nr>), pg, pblk, 0, s, as, pc); e = hipGetLastError(); break;
+                        SBCE_BND(2, 2) SBCE_BND(2, 3) SBCE_BND(2, 4) SBCE_BND(2, 5)
+                        SBCE_BND(2, 6) SBCE_BND(2, 7) SBCE_BND(2, 8)
+                        SBCE_BND(3, 3) SBCE_BND(3, 4) SBCE_BND(3, 5) SBCE_BND(3, 6) SBCE_BND(3, 7)
+                        SBCE_BND(3, 8)
+                        SBCE_BND(4, 4) SBCE_BND(4, 5) SBCE_BND(4, 6) SBCE_BND(4, 7) SBCE_BND(4, 8)
+#undef SBCE_BND
+                    }
                 }
             } else {
                 switch (pb.NT * 16 + pb.NR) {

@@ -254,12 +254,16 @@ __global__ __launch_bounds__(256) void act_kernel(MstepArgs a, int L, int k0) {
 // Tile (ti, tj), ti >= tj, of the active extent: C_IJ = sum_{K >= ti} G_KI^H G_KJ over G's row
 // tiles; the diagonal tile of a column block (K == I) is masked to its lower triangle (its strict
 // upper part holds the factor's 16 x 16 inverse blocks).  4 waves, each a 32 x 32 quadrant of
-// 2 x 2 MFMA tiles; 16-row chunks of both column strips staged in LDS.
-__global__ __launch_bounds__(256) void gram_kernel(MstepArgs a, int L) {
+// 2 x 2 MFMA tiles; 16-row chunks of both column strips staged in LDS.  The tiles of a trial run
+// back to back on one XCD (blocks are dealt round-robin over the 8 XCDs), so the strips shared
+// by the concurrently running tiles of a row or column are re-read from that XCD's L2.
+__global__ __launch_bounds__(256) void gram_kernel(MstepArgs a, int L, int ntiles) {
     __shared__ cd As[KS][TB + 1], Bs[KS][TB + 1];
-    const int b = blockIdx.y;
+    const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
+    const int b = (slot / ntiles) * 8 + xcd;
+    if (b >= a.nbatch) return;
     if (a.done && a.done[b]) return;
-    const int tix = blockIdx.x;
+    const int tix = slot - (slot / ntiles) * ntiles;
     int x = (int)((sqrt(8.0 * tix + 1.0) - 1.0) * 0.5);
     while ((x + 1) * (x + 2) / 2 <= tix) ++x;
     while (x * (x + 1) / 2 > tix) --x;
@@ -543,7 +547,11 @@ hipError_t launch_minnorm(const Problem& pb, const MstepArgs& a, hipStream_t s) 
     const TileExt exR{a.act, nullptr, 0};
     if ((e = launch_tile_factor(pb, a, exR, launch_act, s)) != hipSuccess) return e;
     // C = G^H G, c = G^H B^H
-    hipLaunchKernelGGL(gram_kernel, dim3(nb * (nb + 1) / 2, pb.B), dim3(256), 0, s, a, L);
+    {
+        const int ntiles = nb * (nb + 1) / 2;
+        const long nblk = (long)ntiles * ((pb.B + 7) / 8 * 8);
+        hipLaunchKernelGGL(gram_kernel, dim3((unsigned)nblk), dim3(256), 0, s, a, L, ntiles);
+    }
     hipLaunchKernelGGL(ghb_kernel, dim3(nb, pb.B), dim3(256), 0, s, a, L, pb.NR);
     hipLaunchKernelGGL(gram_tol_kernel, dim3(pb.B), dim3(256), 0, s, a, L);
     if ((e = hipGetLastError()) != hipSuccess) return e;

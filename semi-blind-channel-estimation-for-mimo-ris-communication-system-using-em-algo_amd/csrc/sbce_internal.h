@@ -122,6 +122,7 @@ struct DebugConfig {
     bool upd_waves8;     // SBCE_UPD_WAVES=8       eight-tile panel-update blocks
     int backsub;         // SBCE_BACKSUB           0 default, 1..3 older back substitutions
     char chol_impl;      // SBCE_CHOL_IMPL         0 default, 'v' VALU, 'f' fused one-workgroup
+    bool estep_nopair;   // SBCE_ESTEP_PAIR=0      no factorised-weight pass (estep_pair.hip)
 };
 extern DebugConfig g_debug;
 bool debug_nondefault();   // a result-affecting switch differs from its default
@@ -145,12 +146,17 @@ struct EstepArgs {
     double* prep;      // [B*Td][estep_prep_stride] workspace of the MFMA sweep, or null
                        // (then the sweep kernel prepares each symbol itself)
     int32_t* list;     // [B*Td] symbols the sphere pass left to the sweep, 16 counters
-                       // (0 listed, 1 grabbed by the sweep, 2 listed for the enumeration),
-                       // [B*Td] symbols the tree pass left to the enumeration; null: no sphere
+                       // (0 listed, 1 grabbed by the sweep, 2 listed for the enumeration,
+                       // 3 listed for the factorised-weight pass, 4 grabbed by it), [B*Td]
+                       // symbols the tree pass left to the enumeration, 16 spare, [B*Td]
+                       // symbols the enumeration left to the factorised-weight pass;
+                       // null: no sphere
     double* tree;      // [B*Td][32] the sphere pass's per-symbol search-tree records
 };
-constexpr int kTreeRecDoubles = 32;
+constexpr int kTreeRecDoubles = 32;   // (word 31: the factorised-weight pass's screen)
 constexpr int kEstepListCnt = 16;      // int32 counters after the sweep's list
+// the factorised-weight pass (estep_pair.hip) takes a symbol whose range D is at most this
+constexpr double kPairDmax = 640.0;
 
 struct MstepArgs {
     const cd* yd;
@@ -238,6 +244,11 @@ hipError_t launch_ser(const Problem& pb, const cd* xdest, const cd* xtrue, doubl
                       hipStream_t s);
 hipError_t estep_debug_mfma(unsigned long long* out, int reset);   // SBCE_ESTEP_COUNT=1
 hipError_t estep_debug_sphere(unsigned long long* out3, int reset);   // [enumerated, listed, single path]
+// factorised-weight soft E-step (estep_pair.hip) for the sphere pass's listed symbols
+bool estep_pair_supported(const Problem& pb, int mode);
+hipError_t launch_estep_pair(const Problem& pb, const EstepArgs& a, int stride, int count,
+                             hipStream_t s);
+hipError_t estep_debug_pair(unsigned long long* out, int reset);      // SBCE_ESTEP_COUNT=1
 hipError_t launch_gauss_rank1(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_gauss_expand(const Problem& pb, const cd* theta, cd* out, hipStream_t s);
 hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* out,

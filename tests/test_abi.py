@@ -90,8 +90,8 @@ def test_workspace_and_validation_without_gpu(sbce):
               + 1000 * 256 * 4 * 16                       # moments, R, rhs, shifted y
               + 1000 * 256 * (4 + 2 * 16 + 16 + 6 * 4) * 8  # E-step prep (H_eff, bounds,
                                                             # row-bound vectors)
-              + (2 * 1000 * 256 + 16) * 4                   # sphere pass: sweep and enumeration
-                                                            # lists + counters
+              + (3 * 1000 * 256 + 32) * 4                   # sphere pass: sweep, enumeration and
+                                                            # factorised-pass lists + counters
               + 1000 * 256 * 32 * 8                         # sphere pass: search-tree records
               + 1000 * 16 * 65 * 16 + 1000 * 16 * 16 * 16  # factored pilots psi', x' x'^H
               + 1000 * 4 + 1000 * 8                       # pilot flags, pivot thresholds
