@@ -1070,6 +1070,192 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
     if (tid == 0 && st && a.status) atomicOr(&a.status[b], st);
 }
 
+// ---------------------------------------------------------------- fused panel step
+// panel_fused_kernel (panel jb > 0 with at most 16 row tiles): the panel update AND its factor
+// for one trial per workgroup of NWF waves, row tile tau owned by wave tau % NWF:
+//   U: C_tau = A[rows tau, jb:jb+32] - L[rows tau, 0:jb] L[jb:jb+32, 0:jb]^H into registers, the
+//      panel's top rows staged per KBU-column chunk in LDS by LDS-DMA once for all tiles;
+//   F: panel_factor_kernel's sequence on the register tiles: D_A (wave 0) and its y block, TRSM
+//      of every tile against it (row tile 1's X_A1 published), the in-panel update of the B
+//      halves, D_B (wave 1), TRSM of the B halves.
+// L is written once and the panel never makes the HBM round trip between an update and a factor
+// launch.  Measured slower at cfg1 (A/B only, SBCE_CHOL_IMPL=u): see launch_chol_batched.
+constexpr int NWF = 8;
+__global__ __launch_bounds__(64 * NWF) __attribute__((amdgpu_waves_per_eu(4)))
+void panel_fused_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip) {
+    // Bp (update phase) and the waves' TRSM scratch (factor phase) share the LDS
+    __shared__ __attribute__((aligned(16))) cd smem_u[(PW * (KBU + 1)) > (NWF * NB * NB) ? (PW * (KBU + 1))
+                                                                                      : (NWF * NB * NB)];
+    __shared__ cd DiA[NB * NB], DiB[NB * NB], XA1[NB * NB];
+    __shared__ cd ybA[NB * 8], ybB[NB * 8];
+    __shared__ double dinv[NB];
+    __shared__ int flag;
+    cd* Bp = smem_u;
+    const int b = blockIdx.x;
+    if (a.done && a.done[b]) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    const int w2 = (L - jb) < PW ? (L - jb) : PW;
+    const int wA = w2 < NB ? w2 : NB, wB = w2 - NB;
+    const int jbB = jb + NB;
+    const double tol = a.tol[b];
+    cd* R = a.R + (size_t)b * L * L;
+    cd* y = a.rhs + (size_t)b * L * NR;
+    if (tid == 0) flag = 0;
+    // ---- U: the two row tiles of this wave ----
+    d4v cre[2][2], cim[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int tau = wave + NWF * u;
+        const int nv = tau == 0 ? 1 : 2;        // tile 0's right half: strict upper triangle
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            cre[u][v] = d4v{0.0, 0.0, 0.0, 0.0};
+            cim[u][v] = d4v{0.0, 0.0, 0.0, 0.0};
+            if (tau < ntile && v < nv) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int rr = jb + tau * NB + lk + 4 * q, c = 16 * v + li;
+                    if (rr < L && c < w2) {
+                        const cd x = R[(size_t)rr * L + jb + c];
+                        cre[u][v][q] = x.x;
+                        cim[u][v][q] = x.y;
+                    }
+                }
+            }
+        }
+    }
+    for (int kb0 = 0; kb0 < jb; kb0 += KBU) {
+        const int kbs = (jb - kb0) < KBU ? (jb - kb0) : KBU;        // multiple of 16
+        __syncthreads();
+        // panel top rows by LDS-DMA: wave w stages rows 4w .. 4w+3 (64 lanes = a row's KBU
+        // slots); lanes past kbs / rows past w2 read row jb
+#pragma unroll
+        for (int c4 = 0; c4 < PW / NWF; ++c4) {
+            const int c = wave * (PW / NWF) + c4;
+            const cd* src = R + (size_t)jb * L + kb0;
+            if (c < w2 && lane < kbs) src = R + (size_t)(jb + c) * L + kb0 + lane;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)(Bp + c * (KBU + 1)),
+                                             16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int tau = wave + NWF * u;
+            if (tau >= ntile) continue;                          // wave-uniform
+            const int nv = tau == 0 ? 1 : 2;
+            int r = jb + tau * NB + li;
+            r = r < L ? r : L - 1;                               // rows past L: harmless reads
+            const cd* arow = R + (size_t)r * L + kb0 + lk;
+            cd av[4];
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) av[s2] = arow[4 * s2];
+            for (int k0 = 0; k0 < kbs; k0 += 16) {
+                cd an[4];
+                const bool more = k0 + 16 < kbs;
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) an[s2] = more ? arow[k0 + 16 + 4 * s2] : czero();
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) {
+                    const cd v = av[s2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        if (h >= nv) break;
+                        const cd t = Bp[(16 * h + li) * (KBU + 1) + k0 + 4 * s2 + lk];
+                        cre[u][h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre[u][h], 0, 0, 0);
+                        cre[u][h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre[u][h], 0, 0, 0);
+                        cim[u][h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim[u][h], 0, 0, 0);
+                        cim[u][h] = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim[u][h], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) av[s2] = an[s2];
+            }
+        }
+    }
+    // ---- F: the tiles' y rows in flight, then D_A (wave 0) ----
+    double ydA[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int tau = wave + NWF * u;
+        load_ycomp(y, L, NR, jb + tau * NB, li, lk, tau >= 1 && tau < ntile, ydA[u]);
+    }
+    __syncthreads();                                             // Bp reads done: scratch reuse
+    cd* X = smem_u + wave * NB * NB;
+    if (wave == 0) {
+        for (int e = lane; e < NB * NR; e += 64) ybA[e] = (e < wA * NR) ? y[jb * NR + e] : czero();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = cmk(cre[0][0][q], cim[0][0][q]);
+        wave_sync();
+        factor_diag_lds(X, wA, lane, tol, a.solve_mode, DiA, dinv, &flag, R + (size_t)jb * L + jb, L);
+        forward_y_lds(DiA, ybA, y + jb * NR, wA, NR, lane);
+    }
+    __syncthreads();
+    // TRSM of the A halves; row tile 1 (= sub-panel B's rows) publishes X_A1 and stages its
+    // updated y rows in ybB
+    cd xv[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int tau = wave + NWF * u;
+        if (tau < 1 || tau >= ntile) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = cmk(cre[u][0][q], cim[u][0][q]);
+        wave_sync();
+        trsm_tile16(R, y, DiA, X, ybA, L, NR, jb + tau * NB, jb, wA, li, lk, xv[u], ydA[u],
+                    tau == 1 ? ybB : nullptr);
+        if (tau == 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) XA1[li * NB + lk + 4 * q] = xv[u][q];
+        }
+        wave_sync();
+    }
+    __syncthreads();
+    // in-panel update of the B halves (tile 1's is B's diagonal block), D_B by wave 1
+    double ydB[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int tau = wave + NWF * u;
+        if (tau < 1 || tau >= ntile || wB <= 0) continue;
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            const cd v = xv[u][s2], t = XA1[li * NB + 4 * s2 + lk];
+            cre[u][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre[u][1], 0, 0, 0);
+            cre[u][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre[u][1], 0, 0, 0);
+            cim[u][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim[u][1], 0, 0, 0);
+            cim[u][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim[u][1], 0, 0, 0);
+        }
+        // the y rows after the A update (this lane wrote them), for the B TRSM
+        load_ycomp(y, L, NR, jb + tau * NB, li, lk, tau >= 2, ydB[u]);
+    }
+    if (wave == 1 && wB > 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = cmk(cre[0][1][q], cim[0][1][q]);
+        wave_sync();
+        factor_diag_lds(X, wB, lane, tol, a.solve_mode, DiB, dinv, &flag, R + (size_t)jbB * L + jbB, L);
+        forward_y_lds(DiB, ybB, y + jbB * NR, wB, NR, lane);
+    }
+    __syncthreads();
+    if (wB > 0) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int tau = wave + NWF * u;
+            if (tau < 2 || tau >= ntile) continue;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = cmk(cre[u][1][q], cim[u][1][q]);
+            wave_sync();
+            cd xb[4];
+            trsm_tile16(R, y, DiB, X, ybB, L, NR, jb + tau * NB, jbB, wB, li, lk, xb, ydB[u]);
+            wave_sync();
+        }
+    }
+    const int st = ((flag & 1) ? SBCE_STATUS_NONHPD : 0) | ((flag & 2) ? SBCE_STATUS_RANK : 0) |
+                   ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
+    if (tid == 0 && st && a.status) atomicOr(&a.status[b], st);
+}
+
 // Back substitution L^H x = y (y staged in LDS) and theta = conj(x), one workgroup per trial.
 __global__ __launch_bounds__(256) void backsub_kernel(MstepArgs a, int L, int NR, int skip) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1337,6 +1523,16 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
     for (int j = 0; j < npan; ++j) {
         const int jb = j * PW;
         const int rem = (pb.L - jb + NB - 1) / NB;               // 16-row tiles from jb
+        // SBCE_CHOL_IMPL=u (A/B runs): update and factor of a panel of at most 16 row tiles in
+        // one launch -- 8-17 % slower per panel at cfg1: a trial's register-resident panel
+        // (128 KB) allows two trials per CU, so the 1000 trials take two rounds and each pays
+        // the serial diagonal chain the separate factor launch runs once for all of them
+        if (j > 0 && rem <= 2 * NWF && pb.NR <= 8 && g_debug.chol_impl == 'u') {
+            hipLaunchKernelGGL(panel_fused_kernel, dim3(pb.B), dim3(64 * NWF), 0, s, a, pb.L, pb.NR,
+                               jb, rem, skip);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            continue;
+        }
         if (j > 0) {
             // four-tile blocks; SBCE_UPD_WAVES=8: eight-tile blocks (A/B runs: 4 % slower at
             // cfg1 -- the panel rows' re-reads by the blocks of a trial are L2 hits)

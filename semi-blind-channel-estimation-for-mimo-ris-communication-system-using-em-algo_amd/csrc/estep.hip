@@ -1329,7 +1329,9 @@ template <int NT, int NR>
 __device__ __forceinline__ double prep_candidate(const cd (&H)[NT][NR], const cd (&y)[NR],
                                                  const cd (&Lm)[NT][NT], const double (&dinv)[NT],
                                                  const cd (&zf)[NT], const cd* cons, int M,
-                                                 double& sc, cd (&x)[NT]) {
+                                                 double& sc, int& xidx) {
+    cd x[NT];
+    xidx = 0;
     cd z[NT];
 #pragma unroll
     for (int i = 0; i < NT; ++i) z[i] = zf[i];
@@ -1350,6 +1352,7 @@ __device__ __forceinline__ double prep_candidate(const cd (&H)[NT][NR], const cd
             if (dd < bd) { bd = dd; bs = s; }
         }
         x[q] = cons[bs];
+        xidx |= bs << (8 * q);
     }
     double d0 = 0.0;
     sc = 0.0;
@@ -1368,17 +1371,32 @@ __device__ __forceinline__ double prep_candidate(const cd (&H)[NT][NR], const cd
     return d0;
 }
 
-// Screen of the factorised-weight pass (estep_pair.hip), NT = 4: a lower bound of its range
-// test D = sum_f (max f - f(x_c)) from the four cross-stream log tables alone,
-// E_ab(x_a, x_b) = -2 Re(conj(x_a) h_a^H h_b x_b) / s2: the constellation holds -x_a, so
-// max E_ab >= |E_ab(x_c)| and each term is >= 2 max(0, -E_ab(x_c)).  A symbol whose screen
-// exceeds the pass's limit goes to the sweep without its tables being built.
+// Screen of the factorised-weight pass (estep_pair.hip), NT = 4: an UPPER bound of its range
+// D = sum_f (max f - f(x_c)) over the six log tables, from the candidate x_c alone:
+//   max A <= 0                        ->  A term <= ||y - h_0 x_c0 - h_1 x_c1||^2 / s2,
+//   max B <= ||y||^2 / s2             ->  B term <= ||y - h_2 x_c2 - h_3 x_c3||^2 / s2,
+//   max E_ab <= 2 |h_a^H h_b| max|c|^2 / s2.
+// The enumeration routes a symbol it gives up on to the pass only when this bound is within the
+// pass's limit, so the pass never has to hand a symbol back.
+// Returns the x_c-dependent part (in units of 1/s2) and sets gsum >= sum_ab 2 |h_a^H h_b|, the
+// coefficient of max|c|^2 (known after the Babai descent): D <= (part + gsum max|c|^2) / s2.
 template <int NT, int NR>
-__device__ __forceinline__ double pair_screen(const cd (&H)[NT][NR], const cd (&x)[NT], double inv_s2) {
+__device__ __forceinline__ double pair_screen(const cd (&H)[NT][NR], const cd (&y)[NR], int xidx,
+                                              const cd* cons, double& gsum) {
+    gsum = 0.0;
     if constexpr (NT != 4) {
         return INFINITY;
     } else {
-        double lo = 0.0;
+        cd x[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) x[q] = cons[(xidx >> (8 * q)) & 255];
+        double na = 0.0, nb = 0.0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            na += cabs2(csub(csub(y[r], cmul(H[0][r], x[0])), cmul(H[1][r], x[1])));
+            nb += cabs2(csub(csub(y[r], cmul(H[2][r], x[2])), cmul(H[3][r], x[3])));
+        }
+        double up = na + nb;
 #pragma unroll
         for (int a0 = 0; a0 < 2; ++a0)
 #pragma unroll
@@ -1387,10 +1405,10 @@ __device__ __forceinline__ double pair_screen(const cd (&H)[NT][NR], const cd (&
 #pragma unroll
                 for (int r = 0; r < NR; ++r) G = cfmac(G, H[b0][r], H[a0][r]);    // h_a^H h_b
                 const cd t = cmul(G, x[b0]);
-                const double e = -2.0 * inv_s2 * fma(x[a0].x, t.x, x[a0].y * t.y);
-                lo += 2.0 * fmax(0.0, -e);
+                gsum += 2.0 * (fabs(G.x) + fabs(G.y));                      // >= 2 |G|
+                up += 2.0 * fma(x[a0].x, t.x, x[a0].y * t.y);               // -E_ab(x_c) s2
             }
-        return lo;
+        return up;
     }
 }
 
@@ -1590,8 +1608,8 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
     cd Lm[NT][NT], zf[NT];
     double piv[NT], dinv[NT], sc;
     ridge_chol<NT, NR>(H, y, c.reg, Lm, piv, dinv, zf);
-    cd xc[NT];
-    out[0] = prep_candidate<NT, NR>(H, y, Lm, dinv, zf, cons, c.M, sc, xc);
+    int xidx;
+    out[0] = prep_candidate<NT, NR>(H, y, Lm, dinv, zf, cons, c.M, sc, xidx);
     out[1] = sc;
     prep_bounds<NT, NR>(H, y, out, cons, c);
 }
@@ -1656,7 +1674,7 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
     bool single = false;
     if (live) {
     cd Lm[NT][NT], zf[NT];
-    double piv[NT], dinv[NT], d0, sc, screen;
+    double piv[NT], dinv[NT], d0, sc, screen, gsum;
     int lev[NT];
     double c0 = 0.0;
     {
@@ -1673,11 +1691,14 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
                 out[5 + 2 * (q * NR + r)] = H[q][r].y;
             }
         ridge_chol<NT, NR>(H, y, c.reg, Lm, piv, dinv, zf);
-        cd xc[NT];
-        d0 = prep_candidate<NT, NR>(H, y, Lm, dinv, zf, cons, c.M, sc, xc);
+        int xidx;
+        d0 = prep_candidate<NT, NR>(H, y, Lm, dinv, zf, cons, c.M, sc, xidx);
         out[0] = d0;
         out[1] = sc;
-        screen = pair_screen<NT, NR>(H, xc, c.inv_s2);
+        screen = pair_screen<NT, NR>(H, y, xidx, cons, gsum);
+        // computed here, while H and y are live anyway (left to the compiler, the computation
+        // sinks to the record store at the end and keeps H_eff live across the whole kernel)
+        asm volatile("" : "+v"(screen), "+v"(gsum));
         // reliability of stream q: g_q = [(G + reg I)^-1]_qq = sum_k |(L^-1)_kq|^2
         cd W[NT][NT];
         double g[NT];
@@ -1809,7 +1830,7 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
     rec[1] = R0;
     rec[2] = sc;
     rec[3] = (double)packed;
-    rec[kTrec - 1] = screen;
+    rec[kTrec - 1] = fma(gsum, cmax2, screen) * c.inv_s2;   // the pass's range bound
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
         rec[4 + j] = ui[j];
@@ -2013,7 +2034,7 @@ __global__ __launch_bounds__(64 * kBfsWaves) void estep_bfs_kernel(EstepArgs a, 
                 }
             }
         }
-        // a listed symbol whose screen admits the factorised-weight pass goes to that pass
+        // a listed symbol whose range bound admits the factorised-weight pass goes to that pass
         const bool to_pair = listed && c.pair && rec[kTrec - 1] <= kPairDmax;
         wave_sync();
         if (to_pair) pair_mask |= 1u << (gi - g0);

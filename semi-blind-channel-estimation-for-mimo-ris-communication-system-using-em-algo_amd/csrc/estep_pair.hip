@@ -21,10 +21,9 @@
 // maxima) - l(x_c), x_c the prep pass's candidate (a real hypothesis, l(x_c) <= max l).  For
 // D <= kPairDmax every weight within e^-50 of the maximum is a normal double (> e^-700) and no
 // partial product overflows: the symbol is resolved here.  Otherwise (D grows like 1/varn^2:
-// high SNR) it joins the list the column-tile bounds and the sweep work through.  The
-// enumeration routes a symbol here only when the tree pass's cheap lower bound of D
-// (estep.hip pair_screen, tree record word 31) is within the limit: at high SNR the pass never
-// sees the listed symbols.
+// high SNR) the sweep weighs it.  The enumeration routes a symbol here only when the tree pass's
+// upper bound of D (estep.hip pair_screen, tree record word 31) is within the limit, so the exact
+// test below is a safety net (a failing symbol would join the sweep's list).
 #include "sbce_internal.h"
 
 namespace sbce {

@@ -156,3 +156,32 @@ def test_bench_roofline_traffic_uses_committed_pmc():
         pmc2 = json.load(f)
     assert bench.phase_traffic(pmc2, bench.MSTEP_KERNELS_LARGE, bench.MSTEP_ANCHORS) is not None
     assert bench.phase_traffic({}, bench.MSTEP_KERNELS, bench.MSTEP_ANCHORS) is None
+
+
+def test_committed_roofline_fractions_are_physical():
+    """the roofline fraction must follow from the work the kernel executes.  From
+    the committed round profiles alone (profiles/r03): the dominant kernel's executed flops
+    (bench.py's count) over its rocprofv3 average duration is at most the FP64 peak and at most
+    the measured FP64 MFMA pipe rate (with 5 % timing slack), and the bench line's own frac
+    agrees with that recomputation."""
+    import csv
+    import importlib.util
+    import json
+    spec = importlib.util.spec_from_file_location("sbce_bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    d = os.path.join(ROOT, "profiles", "r03")
+    line = [l for l in open(os.path.join(d, "bench_cfg1.log")) if l.startswith("{")][-1]
+    roof = json.loads(line)["roofline"]
+    assert roof["kernel"] == "rbuild_herm_kernel"
+    flops = bench.rbuild_flops_per_trial_iter(4, 64, 16, 256) * 1000
+    assert abs(roof["flops_per_launch"] / flops - 1) < 1e-12
+    with open(os.path.join(d, "kernel_stats_cfg1.csv")) as f:
+        row = [r for r in csv.DictReader(f) if "rbuild_herm_kernel" in r["Name"]][0]
+    tflops = flops / (float(row["AverageNs"]) * 1e-9) / 1e12
+    assert tflops / bench.FP64_PEAK_TFLOPS <= 1.0
+    assert tflops / roof["measured_pipe_tflops"] <= 1.05
+    assert roof["frac"] <= 1.0 and roof["frac_of_measured_pipe"] <= 1.05
+    # the bench's live HIP-event timing and the profiler's average agree
+    assert abs(roof["ms"] / (float(row["AverageNs"]) * 1e-6) - 1) < 0.05
+    assert roof["traffic_ratio"] >= 1.0 - 0.05
