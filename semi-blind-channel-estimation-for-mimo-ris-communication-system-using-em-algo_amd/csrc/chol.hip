@@ -717,15 +717,12 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip, CholGeom g) {
 // Blocks of one trial sit on one XCD.
 constexpr int KBU = 64;
 constexpr int PW = 32;    // panel width: two 16-column sub-panels
-template <int NWU>        // waves (= row tiles) per block: the staged panel rows serve NWU tiles
-__global__ __launch_bounds__(64 * NWU) void panel_update_kernel(MstepArgs a, int L, int jb, int ntile,
-                                                                int gpt, int skip) {
-    // skip: DIAGNOSTIC (timing only, results invalid): 1 no update
-    __shared__ __attribute__((aligned(16))) cd Bp[PW * (KBU + 1)];
-    const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
-    const int b = (slot / gpt) * 8 + xcd, grp = slot - (slot / gpt) * gpt;
-    if (b >= a.nbatch) return;
-    if (a.done && a.done[b]) return;
+// Body of the update of trial b, row-tile group grp, by the columns [0, kend) (kend = jb: the
+// whole left part; the look-ahead step passes kend = jb - PW).  Bp: PW * (KBU + 1) LDS entries.
+// G3: the complex products by three real MFMAs instead of four (csub_step, sbce_internal.h).
+template <int NWU, bool G3 = false>
+__device__ __forceinline__ void panel_update_body(const MstepArgs& a, int L, int jb, int kend, int ntile,
+                                                  int b, int grp, int skip, cd* Bp) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
@@ -739,11 +736,12 @@ __global__ __launch_bounds__(64 * NWU) void panel_update_kernel(MstepArgs a, int
     const cd* arow = R + (size_t)r * L + lk;
     // tile 0's right half lies in the strict upper triangle: neither loaded nor stored
     const int nv = tau == 0 ? 1 : 2;
-    d4v cre[2], cim[2];
+    d4v cre[2], cim[2], c2[2];
 #pragma unroll
     for (int v = 0; v < 2; ++v) {
         cre[v] = d4v{0.0, 0.0, 0.0, 0.0};
         cim[v] = d4v{0.0, 0.0, 0.0, 0.0};
+        c2[v] = d4v{0.0, 0.0, 0.0, 0.0};
         if (active && v < nv) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -755,9 +753,10 @@ __global__ __launch_bounds__(64 * NWU) void panel_update_kernel(MstepArgs a, int
                 }
             }
         }
+        csub_init<G3>(cre[v], cim[v], c2[v]);
     }
-    for (int kb0 = 0; kb0 < ((skip & 1) ? 0 : jb); kb0 += KBU) {
-        const int kbs = (jb - kb0) < KBU ? (jb - kb0) : KBU;        // multiple of 16
+    for (int kb0 = 0; kb0 < ((skip & 1) ? 0 : kend); kb0 += KBU) {
+        const int kbs = (kend - kb0) < KBU ? (kend - kb0) : KBU;    // multiple of 16
         cd av[4];
         if (active) {
 #pragma unroll
@@ -789,12 +788,8 @@ __global__ __launch_bounds__(64 * NWU) void panel_update_kernel(MstepArgs a, int
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         if (h >= nv) break;                  // wave-uniform
-                        const cd t = Bp[(16 * h + li) * (KBU + 1) + k0 + 4 * s2 + lk];
-                        // C -= A conj(B)^T:  re -= ar tr + ai ti ;  im -= ai tr - ar ti
-                        cre[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre[h], 0, 0, 0);
-                        cre[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre[h], 0, 0, 0);
-                        cim[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim[h], 0, 0, 0);
-                        cim[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim[h], 0, 0, 0);
+                        // C -= A conj(B)^T
+                        csub_step<G3>(cre[h], cim[h], c2[h], v, Bp[(16 * h + li) * (KBU + 1) + k0 + 4 * s2 + lk]);
                     }
                 }
 #pragma unroll
@@ -809,10 +804,23 @@ __global__ __launch_bounds__(64 * NWU) void panel_update_kernel(MstepArgs a, int
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int rr = row0 + lk + 4 * q, c = 16 * v + li;
-                if (rr < L && c < w2) R[(size_t)rr * L + jb + c] = cmk(cre[v][q], cim[v][q]);
+                const cd o = csub_out<G3>(cre[v], cim[v], c2[v], q);
+                if (rr < L && c < w2) R[(size_t)rr * L + jb + c] = o;
             }
         }
     }
+}
+
+template <int NWU, bool G3 = false>   // waves (= row tiles) per block: the staged panel rows serve NWU tiles
+__global__ __launch_bounds__(64 * NWU) void panel_update_kernel(MstepArgs a, int L, int jb, int ntile,
+                                                                int gpt, int skip) {
+    // skip: DIAGNOSTIC (timing only, results invalid): 1 no update
+    __shared__ __attribute__((aligned(16))) cd Bp[PW * (KBU + 1)];
+    const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
+    const int b = (slot / gpt) * 8 + xcd, grp = slot - (slot / gpt) * gpt;
+    if (b >= a.nbatch) return;
+    if (a.done && a.done[b]) return;
+    panel_update_body<NWU, G3>(a, L, jb, jb, ntile, b, grp, skip, Bp);
 }
 
 // 16 x 16 tile of R (rows row0.., columns c0.., w valid columns) into per-lane registers:
@@ -834,26 +842,33 @@ __device__ __forceinline__ void load_tile16(const cd* R, int L, int row0, int c0
 // comes out of the TRSM), B1 = [Re Y | Im Y], B2 = [-Im Y | Re Y]; lane (li, lk) ends with
 // component (li < NR: re, else im) of right-hand side li mod NR for rows lk + 4q, and
 // yd[q] holds the same component of those rows before the update (load_ycomp).  NR <= 8.
+template <bool G3 = false>
 __device__ __forceinline__ void trsm_tile16(cd* R, cd* y, const cd* Di, const cd* X, const cd* yb,
                                             int L, int NR, int row0, int c0, int w, int li,
                                             int lk, cd* xv, const double* yd, cd* ylds = nullptr) {
-    d4v xre = {0.0, 0.0, 0.0, 0.0}, xim = {0.0, 0.0, 0.0, 0.0};
+    d4v xre = {0.0, 0.0, 0.0, 0.0}, xim = {0.0, 0.0, 0.0, 0.0}, x2 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int s2 = 0; s2 < NB / 4; ++s2) {
         const cd d = Di[li * NB + 4 * s2 + lk];    // A[j][k] = conj(Di[j][4s+k])
         const cd c = X[li * NB + 4 * s2 + lk];     // B[k][i] = C[i][4s+k]
         // X^T = conj(Di) C^T:  re += dr cr + di ci ;  im += dr ci - di cr
-        xre = __builtin_amdgcn_mfma_f64_16x16x4f64(d.x, c.x, xre, 0, 0, 0);
-        xre = __builtin_amdgcn_mfma_f64_16x16x4f64(d.y, c.y, xre, 0, 0, 0);
-        xim = __builtin_amdgcn_mfma_f64_16x16x4f64(d.x, c.y, xim, 0, 0, 0);
-        xim = __builtin_amdgcn_mfma_f64_16x16x4f64(-d.y, c.x, xim, 0, 0, 0);
+        if constexpr (G3) {       // P1 = dr cr, P2 = di ci, P3 = (dr + di)(cr - ci): im = P1 - P2 - P3
+            xre = __builtin_amdgcn_mfma_f64_16x16x4f64(d.x, c.x, xre, 0, 0, 0);
+            x2 = __builtin_amdgcn_mfma_f64_16x16x4f64(d.y, c.y, x2, 0, 0, 0);
+            xim = __builtin_amdgcn_mfma_f64_16x16x4f64(d.x + d.y, c.x - c.y, xim, 0, 0, 0);
+        } else {
+            xre = __builtin_amdgcn_mfma_f64_16x16x4f64(d.x, c.x, xre, 0, 0, 0);
+            xre = __builtin_amdgcn_mfma_f64_16x16x4f64(d.y, c.y, xre, 0, 0, 0);
+            xim = __builtin_amdgcn_mfma_f64_16x16x4f64(d.x, c.y, xim, 0, 0, 0);
+            xim = __builtin_amdgcn_mfma_f64_16x16x4f64(-d.y, c.x, xim, 0, 0, 0);
+        }
     }
     const bool live = row0 + li < L;
     cd* crow = R + (size_t)(live ? row0 + li : L - 1) * L + c0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int j = lk + 4 * q;
-        xv[q] = cmk(xre[q], xim[q]);
+        xv[q] = G3 ? cmk(xre[q] + x2[q], xre[q] - x2[q] - xim[q]) : cmk(xre[q], xim[q]);
         if (live && j < w) crow[j] = xv[q];
     }
     const bool isre = li < NR, on = li < 2 * NR;
@@ -900,16 +915,19 @@ __device__ __forceinline__ void load_ycomp(const cd* y, int L, int NR, int row0,
 //   waves 1-3, row tiles tau >= 2: TRSM against D_A, then the in-panel rank-16 update
 //           C_B,tau -= X_A,tau X_A1^H written back to R;                          barrier
 //   all waves, tau >= 2: TRSM of C_B,tau against D_B.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip) {
+// LDS of the factor body (cd entries): Xs (4 waves' 16 x 16 scratch), DiA, DiB, XA1, ybA, ybB
+constexpr int kFacXs = 0, kFacDiA = 4 * NB * NB, kFacDiB = kFacDiA + NB * NB, kFacXA1 = kFacDiB + NB * NB,
+              kFacYbA = kFacXA1 + NB * NB, kFacYbB = kFacYbA + NB * 8, kFacLds = kFacYbB + NB * 8;
+template <bool G3 = false>
+__device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int NR, int jb, int ntile,
+                                                  int b, int skip, cd* sm, double* dinv, int& flag) {
     // skip: DIAGNOSTIC phase mask (timing only, results invalid): 2 diag factors, 8 trsm tiles
-    __shared__ cd DiA[NB * NB], DiB[NB * NB], XA1[NB * NB];
-    __shared__ cd Xs[4 * NB * NB];
-    __shared__ cd ybA[NB * 8], ybB[NB * 8];     // the sub-panels' y blocks after D^-1
-    __shared__ double dinv[NB];
-    __shared__ int flag;
-    const int b = blockIdx.x;
-    if (a.done && a.done[b]) return;
+    cd* DiA = sm + kFacDiA;
+    cd* DiB = sm + kFacDiB;
+    cd* XA1 = sm + kFacXA1;
+    cd* Xs = sm + kFacXs;
+    cd* ybA = sm + kFacYbA;     // the sub-panels' y blocks after D^-1
+    cd* ybB = sm + kFacYbB;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
@@ -936,6 +954,7 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
     // by no one in this launch) arrives by LDS-DMA in DiB (unused until factor B; no
     // registers held across factor A), y block A in ybA, before factor A starts
     if (wave == 0) {
+        __builtin_amdgcn_s_setprio(3);                       // the serial chain issues first
         cd t1[4];
         double y1[4];
         load_tile16(R, L, jbB, jb, wA, lane, ntile > 1, t1);        // row tile 1, A part
@@ -967,7 +986,7 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
             for (int h = 0; h < 4; ++h) X[lane + 64 * h] = t1[h];
             wave_sync();
             // row tile 1 = sub-panel B's rows: its updated y rows are staged raw in ybB
-            trsm_tile16(R, y, DiA, X, ybA, L, NR, jbB, jb, wA, li, lk, xv, y1, ybB);
+            trsm_tile16<G3>(R, y, DiA, X, ybA, L, NR, jbB, jb, wA, li, lk, xv, y1, ybB);
 #pragma unroll
             for (int q = 0; q < 4; ++q) XA1[li * NB + lk + 4 * q] = xv[q];
         }
@@ -977,7 +996,7 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
     if (wave == 0) {
         if (wB > 0) {
             // B's diagonal tile: C_B1 -= X_A1 X_A1^H, then factor
-            d4v cre = {0.0, 0.0, 0.0, 0.0}, cim = {0.0, 0.0, 0.0, 0.0};
+            d4v cre = {0.0, 0.0, 0.0, 0.0}, cim = {0.0, 0.0, 0.0, 0.0}, c2;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int rr = lk + 4 * q;
@@ -988,16 +1007,11 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
                 }
             }
             wave_sync();                                         // DiB is overwritten next
+            csub_init<G3>(cre, cim, c2);
 #pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) {
-                const cd v = xv[s2], t = XA1[li * NB + 4 * s2 + lk];
-                cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre, 0, 0, 0);
-                cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre, 0, 0, 0);
-                cim = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim, 0, 0, 0);
-                cim = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim, 0, 0, 0);
-            }
+            for (int s2 = 0; s2 < 4; ++s2) csub_step<G3>(cre, cim, c2, xv[s2], XA1[li * NB + 4 * s2 + lk]);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = cmk(cre[q], cim[q]);
+            for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = csub_out<G3>(cre, cim, c2, q);
             wave_sync();
             if (!(skip & 2)) {
                 factor_diag_lds(X, wB, lane, tol, a.solve_mode, DiB, dinv, &flag,
@@ -1012,7 +1026,7 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
             const int row0 = jb + tau * NB;
 #pragma unroll
             for (int h = 0; h < 4; ++h) X[lane + 64 * h] = cur[h];
-            d4v cre = {0.0, 0.0, 0.0, 0.0}, cim = {0.0, 0.0, 0.0, 0.0};
+            d4v cre = {0.0, 0.0, 0.0, 0.0}, cim = {0.0, 0.0, 0.0, 0.0}, c2;
             if (wB > 0) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -1028,20 +1042,15 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
             load_tile16(R, L, row0 + 3 * NB, jb, wA, lane, tau + 3 < ntile, cur);   // next
             load_ycomp(y, L, NR, row0 + 3 * NB, li, lk, tau + 3 < ntile, ycur);
             wave_sync();
-            trsm_tile16(R, y, DiA, X, ybA, L, NR, row0, jb, wA, li, lk, xv, yv);
+            trsm_tile16<G3>(R, y, DiA, X, ybA, L, NR, row0, jb, wA, li, lk, xv, yv);
             if (wB > 0) {
+                csub_init<G3>(cre, cim, c2);
 #pragma unroll
-                for (int s2 = 0; s2 < 4; ++s2) {
-                    const cd v = xv[s2], t = XA1[li * NB + 4 * s2 + lk];
-                    cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre, 0, 0, 0);
-                    cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre, 0, 0, 0);
-                    cim = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim, 0, 0, 0);
-                    cim = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim, 0, 0, 0);
-                }
+                for (int s2 = 0; s2 < 4; ++s2) csub_step<G3>(cre, cim, c2, xv[s2], XA1[li * NB + 4 * s2 + lk]);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int rr = row0 + lk + 4 * q;
-                    if (rr < L && li < wB) R[(size_t)rr * L + jbB + li] = cmk(cre[q], cim[q]);
+                    if (rr < L && li < wB) R[(size_t)rr * L + jbB + li] = csub_out<G3>(cre, cim, c2, q);
                 }
             }
             wave_sync();
@@ -1061,13 +1070,142 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
             load_tile16(R, L, row0 + 4 * NB, jbB, wB, lane, tau + 4 < ntile, cur);
             load_ycomp(y, L, NR, row0 + 4 * NB, li, lk, tau + 4 < ntile, ycur);
             wave_sync();
-            trsm_tile16(R, y, DiB, X, ybB, L, NR, row0, jbB, wB, li, lk, xv, yv);
+            trsm_tile16<G3>(R, y, DiB, X, ybB, L, NR, row0, jbB, wB, li, lk, xv, yv);
             wave_sync();
         }
     }
     const int st = ((flag & 1) ? SBCE_STATUS_NONHPD : 0) | ((flag & 2) ? SBCE_STATUS_RANK : 0) |
                    ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
     if (tid == 0 && st && a.status) atomicOr(&a.status[b], st);
+}
+
+template <bool G3 = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip) {
+    __shared__ __attribute__((aligned(16))) cd sm[kFacLds];
+    __shared__ double dinv[NB];
+    __shared__ int flag;
+    const int b = blockIdx.x;
+    if (a.done && a.done[b]) return;
+    panel_factor_body<G3>(a, L, NR, jb, ntile, b, skip, sm, dinv, flag);
+}
+
+// ---------------------------------------------------------------- look-ahead panel step
+// Rank-PW update of panel j (columns [jb, jb+32), every row tile) by panel j-1's columns
+// [jb-32, jb), written back to R: the part of panel j's left-looking update that the
+// look-ahead step could not make in the previous launch (panel j-1 was being factored there).
+// Lp: PW * (PW + 1) LDS entries (panel j-1's rows jb .. jb+31, the shared B operand).
+__device__ __forceinline__ void panel_preupdate(const MstepArgs& a, int L, int jb, int ntile, int b,
+                                                cd* Lp) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    const int w2 = (L - jb) < PW ? (L - jb) : PW;
+    const int k0c = jb - PW;
+    cd* R = a.R + (size_t)b * L * L;
+    for (int e = tid; e < PW * PW; e += 256) {
+        const int c = e >> 5, k = e & (PW - 1);
+        Lp[c * (PW + 1) + k] = c < w2 ? R[(size_t)(jb + c) * L + k0c + k] : czero();
+    }
+    __syncthreads();
+    for (int tau = wave; tau < ntile; tau += 4) {             // wave-uniform
+        const int row0 = jb + tau * NB;
+        int r = row0 + li;
+        r = r < L ? r : L - 1;                                   // rows past L: harmless reads
+        const cd* arow = R + (size_t)r * L + k0c + lk;
+        cd av[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) av[s2] = arow[4 * s2];
+        const int nv = tau == 0 ? 1 : 2;                         // tile 0's right half: upper triangle
+        d4v cre[2], cim[2];
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            cre[v] = d4v{0.0, 0.0, 0.0, 0.0};
+            cim[v] = d4v{0.0, 0.0, 0.0, 0.0};
+            if (v < nv) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int rr = row0 + lk + 4 * q, c = 16 * v + li;
+                    if (rr < L && c < w2) {
+                        const cd x = R[(size_t)rr * L + jb + c];
+                        cre[v][q] = x.x;
+                        cim[v][q] = x.y;
+                    }
+                }
+            }
+        }
+#pragma unroll 1
+        for (int k0 = 0; k0 < PW; k0 += 16) {
+            cd an[4];
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) an[s2] = k0 == 0 ? arow[16 + 4 * s2] : czero();
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const cd v = av[s2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if (h >= nv) break;                          // wave-uniform
+                    const cd t = Lp[(16 * h + li) * (PW + 1) + k0 + 4 * s2 + lk];
+                    cre[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre[h], 0, 0, 0);
+                    cre[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre[h], 0, 0, 0);
+                    cim[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim[h], 0, 0, 0);
+                    cim[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim[h], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) av[s2] = an[s2];
+        }
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            if (v >= nv) break;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rr = row0 + lk + 4 * q, c = 16 * v + li;
+                if (rr < L && c < w2) R[(size_t)rr * L + jb + c] = cmk(cre[v][q], cim[v][q]);
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// One launch per panel j with two block roles (look-ahead): role F (one workgroup per trial)
+// applies panel j-1's rank-32 update to panel j and factors it (panel_factor_body); role U
+// (gptU four-tile groups per trial) updates panel j+1 by the columns [0, jb) -- everything
+// already factored.  The two roles touch disjoint columns, so the latency-bound diagonal
+// chains of F run beside U's MFMA streaming instead of in a launch of their own; a trial's
+// blocks are adjacent in dispatch order (F first) and sit on one XCD.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+void panel_la_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int gptU, int ntileU, int skip) {
+    __shared__ __attribute__((aligned(16))) cd sm[(PW * (KBU + 1)) > kFacLds ? (PW * (KBU + 1)) : kFacLds];
+    __shared__ double dinv[NB];
+    __shared__ int flag;
+    const int id = blockIdx.x, xcd = id & 7, k = id >> 3;
+    const int nT = (a.nbatch + 7) >> 3;                       // trials per XCD
+    // dispatch order per XCD: F and U blocks alternate until every F is out, then the rest of U
+    bool isF;
+    int it, grp = 0;
+    if (gptU == 0) { isF = true; it = k; }
+    else if (k < 2 * nT) {
+        isF = !(k & 1);
+        const int u = k >> 1;
+        it = isF ? u : u / gptU;
+        grp = isF ? 0 : u - (u / gptU) * gptU;
+    } else {
+        isF = false;
+        const int u = k - nT;
+        it = u / gptU;
+        grp = u - it * gptU;
+    }
+    const int b = it * 8 + xcd;
+    if (b >= a.nbatch) return;
+    if (a.done && a.done[b]) return;
+    if (!isF) {
+        panel_update_body<4>(a, L, jb + PW, jb, ntileU, b, grp, skip, sm);
+        return;
+    }
+    __builtin_amdgcn_s_setprio(2);                           // F before U; its chain wave first
+    if (jb > 0 && !(skip & 1)) panel_preupdate(a, L, jb, ntile, b, sm);
+    panel_factor_body(a, L, NR, jb, ntile, b, skip, sm, dinv, flag);
 }
 
 // ---------------------------------------------------------------- fused panel step
@@ -1520,7 +1658,21 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
     if (e != hipSuccess) return e;
     const int npan = (pb.L + PW - 1) / PW;
     const int upd_waves = g_debug.upd_waves8 ? 8 : 4;
-    for (int j = 0; j < npan; ++j) {
+    const bool lookahead = g_debug.chol_impl == 'l';   // A/B only: measured slower
+    if (lookahead) {
+        // look-ahead steps: launch j factors panel j and updates panel j+1 by panels 0..j-1
+        for (int j = 0; j < npan; ++j) {
+            const int jb = j * PW;
+            const int rem = (pb.L - jb + NB - 1) / NB;
+            const int remU = j + 1 < npan ? (pb.L - jb - PW + NB - 1) / NB : 0;
+            const int gptU = (jb > 0 && remU > 0) ? (remU + 3) / 4 : 0;
+            const long nblk = 8L * ((pb.B + 7) / 8) * (1 + gptU);
+            hipLaunchKernelGGL(panel_la_kernel, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L, pb.NR, jb,
+                               rem, gptU, remU, skip);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+    }
+    for (int j = 0; j < npan && !lookahead; ++j) {
         const int jb = j * PW;
         const int rem = (pb.L - jb + NB - 1) / NB;               // 16-row tiles from jb
         // SBCE_CHOL_IMPL=u (A/B runs): update and factor of a panel of at most 16 row tiles in
@@ -1539,8 +1691,12 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
             if (upd_waves == 4) {
                 const int gpt = (rem + 3) / 4;
                 const long nblk = 8L * ((pb.B + 7) / 8) * gpt;
-                hipLaunchKernelGGL(panel_update_kernel<4>, dim3((unsigned)nblk), dim3(256), 0, s, a,
-                                   pb.L, jb, rem, gpt, skip);
+                if (g_debug.cplx3 && a.solve_mode == SBCE_SOLVE_CHOL)
+                    hipLaunchKernelGGL((panel_update_kernel<4, true>), dim3((unsigned)nblk), dim3(256), 0, s,
+                                       a, pb.L, jb, rem, gpt, skip);
+                else
+                    hipLaunchKernelGGL((panel_update_kernel<4, false>), dim3((unsigned)nblk), dim3(256), 0, s,
+                                       a, pb.L, jb, rem, gpt, skip);
             } else {
                 const int gpt = (rem + 7) / 8;
                 const long nblk = 8L * ((pb.B + 7) / 8) * gpt;
@@ -1548,8 +1704,12 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
                                    pb.L, jb, rem, gpt, skip);
             }
         }
-        hipLaunchKernelGGL(panel_factor_kernel, dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR, jb, rem,
-                           skip);
+        if (g_debug.cplx3 && a.solve_mode == SBCE_SOLVE_CHOL)
+            hipLaunchKernelGGL(panel_factor_kernel<true>, dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR, jb,
+                               rem, skip);
+        else
+            hipLaunchKernelGGL(panel_factor_kernel<false>, dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR, jb,
+                               rem, skip);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     // default: one-buffer one-barrier kernel (backsub4); SBCE_BACKSUB=3 the two-buffer one-barrier

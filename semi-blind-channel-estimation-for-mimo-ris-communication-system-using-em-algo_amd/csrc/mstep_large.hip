@@ -411,7 +411,7 @@ __global__ __launch_bounds__(64) void tile_inverse_kernel(MstepArgs a, int L, in
 //   TRSM (HERK = false): tile (i, k), C = A_ik W^H written in place (init 0);
 //   HERK (HERK = true):  tile (i, j), C = A_ij - L_ik L_jk^H.
 // 4 waves, wave w owns the 32 x 32 quadrant (w >> 1, w & 1) = 2 x 2 MFMA tiles.
-template <bool HERK>
+template <bool HERK, bool G3 = false>
 __global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int kb, int NR, TileExt ext) {
     __shared__ cd As[TB][KS + 1], Bs[TB][KS + 1];
     const int b = blockIdx.y;
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int 
     const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
     const int kmax = (L - k0) < TB ? (L - k0) : TB;
 
-    d4v cre[2][2], cim[2][2];
+    d4v cre[2][2], cim[2][2], c2[2][2];
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -459,8 +459,9 @@ __global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int 
                     }
                 }
             }
+            csub_init<G3>(cre[u][v], cim[u][v], c2[u][v]);
         }
-    const double sg = HERK ? -1.0 : 1.0;
+    const double sg = HERK ? 1.0 : -1.0;         // C -= (sg A) conj(B)^T
     // operand chunks (TB x KS of A and B) are loaded into registers one chunk ahead: the
     // global latency of chunk kc + KS overlaps the MFMAs of chunk kc
     constexpr int PF = TB * KS / 256;               // entries per thread and operand
@@ -493,15 +494,11 @@ __global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int 
 #pragma unroll
             for (int v = 0; v < 2; ++v) bv[v] = Bs[wc + 16 * v + li][4 * s + lk];
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+            for (int u = 0; u < 2; ++u) {
+                const cd va = cmk(sg * av[u].x, sg * av[u].y);
 #pragma unroll
-                for (int v = 0; v < 2; ++v) {
-                    // C += sg A conj(B)^T:  re += ar br + ai bi ; im += ai br - ar bi
-                    cre[u][v] = mfma4(sg * av[u].x, bv[v].x, cre[u][v]);
-                    cre[u][v] = mfma4(sg * av[u].y, bv[v].y, cre[u][v]);
-                    cim[u][v] = mfma4(sg * av[u].y, bv[v].x, cim[u][v]);
-                    cim[u][v] = mfma4(-sg * av[u].x, bv[v].y, cim[u][v]);
-                }
+                for (int v = 0; v < 2; ++v) csub_step<G3>(cre[u][v], cim[u][v], c2[u][v], va, bv[v]);
+            }
         }
     }
     __syncthreads();   // TRSM writes in place over its own A operand
@@ -513,7 +510,7 @@ __global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int 
             for (int q = 0; q < 4; ++q) {
                 const int r = r0 + wr + 16 * u + lk + 4 * q, c = c0 + wc + 16 * v + li;
                 if (r < L && c < L && (HERK || c < k0 + kmax))
-                    R[(size_t)r * L + c] = cmk(cre[u][v][q], cim[u][v][q]);
+                    R[(size_t)r * L + c] = csub_out<G3>(cre[u][v], cim[u][v], c2[u][v], q);
             }
     if (!HERK && ext.fwd) {
         // fused forward substitution: rows r0.. of y -= L_ik y_k (the tile just written)
@@ -538,6 +535,7 @@ __global__ __launch_bounds__(256) void tile_gemm_kernel(MstepArgs a, int L, int 
 // Blocks of one trial sit on one XCD (block id % 8) so the panel rows the trial's tiles share
 // are L2 hits.  ext.col: K and the tiles are clipped to the trial's active extent (min-norm
 // early exit: columns past it are dropped and never read again).
+template <bool G3 = false>
 __global__ __launch_bounds__(256) void tile_herk_kernel(MstepArgs a, int L, int kb_lo, int nkb,
                                                         int tj_lo, int tj_hi, int ntiles,
                                                         TileExt ext) {
@@ -578,11 +576,11 @@ __global__ __launch_bounds__(256) void tile_herk_kernel(MstepArgs a, int L, int 
     const int li = lane & 15, lk = lane >> 4;
     const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
 
-    d4v cre[2][2], cim[2][2];
+    d4v cre[2][2], cim[2][2], c2[2][2];
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int v = 0; v < 2; ++v)
+        for (int v = 0; v < 2; ++v) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int r = r0 + wr + 16 * u + lk + 4 * q, c = c0 + wc + 16 * v + li;
@@ -590,6 +588,8 @@ __global__ __launch_bounds__(256) void tile_herk_kernel(MstepArgs a, int L, int 
                 cre[u][v][q] = x.x;
                 cim[u][v][q] = x.y;
             }
+            csub_init<G3>(cre[u][v], cim[u][v], c2[u][v]);
+        }
     constexpr int PF = TB * KS / 256;               // entries per thread and operand
     cd pa[PF], pbv[PF];
     auto fetch = [&](int kc) {
@@ -622,13 +622,8 @@ __global__ __launch_bounds__(256) void tile_herk_kernel(MstepArgs a, int L, int 
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
-                for (int v = 0; v < 2; ++v) {
-                    // C -= A conj(B)^T:  re -= ar br + ai bi ; im -= ai br - ar bi
-                    cre[u][v] = mfma4(-av[u].x, bv[v].x, cre[u][v]);
-                    cre[u][v] = mfma4(-av[u].y, bv[v].y, cre[u][v]);
-                    cim[u][v] = mfma4(-av[u].y, bv[v].x, cim[u][v]);
-                    cim[u][v] = mfma4(av[u].x, bv[v].y, cim[u][v]);
-                }
+                for (int v = 0; v < 2; ++v)      // C -= A conj(B)^T
+                    csub_step<G3>(cre[u][v], cim[u][v], c2[u][v], av[u], bv[v]);
         }
     }
 #pragma unroll
@@ -638,7 +633,7 @@ __global__ __launch_bounds__(256) void tile_herk_kernel(MstepArgs a, int L, int 
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int r = r0 + wr + 16 * u + lk + 4 * q, c = c0 + wc + 16 * v + li;
-                if (r < L && c < L) R[(size_t)r * L + c] = cmk(cre[u][v][q], cim[u][v][q]);
+                if (r < L && c < L) R[(size_t)r * L + c] = csub_out<G3>(cre[u][v], cim[u][v], c2[u][v], q);
             }
 }
 
@@ -820,8 +815,12 @@ static hipError_t launch_herk(const Problem& pb, const MstepArgs& a, int kb_lo, 
     if (ntiles <= 0) return hipSuccess;
     const long nblk = 8L * ((pb.B + 7) / 8) * ntiles;
     if (nblk > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(tile_herk_kernel, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L, kb_lo, nkb,
-                       tj_lo, tj_hi, (int)ntiles, ex);
+    if (g_debug.cplx3 && a.solve_mode == SBCE_SOLVE_CHOL)
+        hipLaunchKernelGGL(tile_herk_kernel<true>, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L, kb_lo,
+                           nkb, tj_lo, tj_hi, (int)ntiles, ex);
+    else
+        hipLaunchKernelGGL(tile_herk_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L, kb_lo,
+                           nkb, tj_lo, tj_hi, (int)ntiles, ex);
     return hipGetLastError();
 }
 
@@ -835,8 +834,11 @@ hipError_t launch_tile_factor_step(const Problem& pb, const MstepArgs& a, int k,
     const size_t inv_lds = (size_t)TB * TB * sizeof(cd) + (size_t)TB * 8 * sizeof(cd);
     hipLaunchKernelGGL(tile_inverse_kernel, dim3(pb.B), dim3(64), inv_lds, s, a, pb.L, k0, w, pb.NR, ex);
     const int below = nb - k - 1;
-    if (below > 0)
-        hipLaunchKernelGGL(tile_gemm_kernel<false>, dim3(below, pb.B), dim3(256), 0, s, a, pb.L, k,
+    if (below > 0 && g_debug.cplx3 && a.solve_mode == SBCE_SOLVE_CHOL)
+        hipLaunchKernelGGL((tile_gemm_kernel<false, true>), dim3(below, pb.B), dim3(256), 0, s, a, pb.L, k,
+                           pb.NR, ex);
+    else if (below > 0)
+        hipLaunchKernelGGL((tile_gemm_kernel<false, false>), dim3(below, pb.B), dim3(256), 0, s, a, pb.L, k,
                            pb.NR, ex);
     return hipGetLastError();
 }

@@ -12,6 +12,41 @@ namespace sbce {
 // complex double, interleaved (numpy complex128 memory)
 typedef double2 cd;
 
+// C -= A conj(B)^T on a 16 x 16 complex MFMA tile, one k-step of 4 (lane values v = A, t = B,
+// v_mfma_f64_16x16x4f64 operand layout): four real MFMAs, or three with G3 (Gauss):  with
+// P1 = sum ar br, P2 = sum ai bi, P3 = sum (ar + ai)(br - bi) the update has
+//   re = C_re - P1 - P2,   im = C_im - (P3 - P1 + P2);
+// the accumulators X1 = C_re - P1 (cre), X2 = -P2 (c2), X3 = C_im + C_re - P3 (cim, csub_init)
+// give re = X1 + X2, im = X3 - X1 + X2 (csub_out).  Used for the CHOL solve only: the rounding
+// of the imaginary part grows (error ~ eps (|ar| + |ai|)(|br| + |bi|)), which the min-norm and
+// drop solves must not see -- their pivots past the numerical rank are that rounding noise.
+typedef double mf4 __attribute__((ext_vector_type(4)));
+template <bool G3>
+__device__ __forceinline__ void csub_init(mf4& cre, mf4& cim, mf4& c2) {
+    c2 = mf4{0.0, 0.0, 0.0, 0.0};
+    if constexpr (G3) cim += cre;
+}
+template <bool G3>
+__device__ __forceinline__ void csub_step(mf4& cre, mf4& cim, mf4& c2, cd v, cd t) {
+    if constexpr (G3) {
+        cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, c2, 0, 0, 0);
+        cim = __builtin_amdgcn_mfma_f64_16x16x4f64(-(v.x + v.y), t.x - t.y, cim, 0, 0, 0);
+    } else {
+        cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre, 0, 0, 0);
+        cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre, 0, 0, 0);
+        cim = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim, 0, 0, 0);
+        cim = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim, 0, 0, 0);
+    }
+}
+template <bool G3>
+__device__ __forceinline__ cd csub_out(const mf4& cre, const mf4& cim, const mf4& c2, int q) {
+    cd z;
+    z.x = G3 ? cre[q] + c2[q] : cre[q];
+    z.y = G3 ? cim[q] - cre[q] + c2[q] : cim[q];
+    return z;
+}
+
 __device__ __forceinline__ cd cmk(double r, double i) { cd z; z.x = r; z.y = i; return z; }
 __device__ __forceinline__ cd czero() { return cmk(0.0, 0.0); }
 __device__ __forceinline__ cd cadd(cd a, cd b) { return cmk(a.x + b.x, a.y + b.y); }
@@ -121,9 +156,10 @@ struct DebugConfig {
     bool rb_tc32;        // SBCE_RB_TC=32          32-symbol R-build chunks
     bool upd_waves8;     // SBCE_UPD_WAVES=8       eight-tile panel-update blocks
     int backsub;         // SBCE_BACKSUB           0 default, 1..3 older back substitutions
-    char chol_impl;      // SBCE_CHOL_IMPL         0 default, 'v' VALU, 'f' fused one-workgroup,
+    char chol_impl;      // SBCE_CHOL_IMPL         0 default, 'l' look-ahead panel steps, 'v' VALU, 'f' fused one-workgroup,
                          //                        'u' unified panel update + factor launch
     bool estep_nopair;   // SBCE_ESTEP_PAIR=0      no factorised-weight pass (estep_pair.hip)
+    bool cplx3;          // SBCE_CPLX3=0           four real MFMAs per complex product (default: three, Gauss)
 };
 extern DebugConfig g_debug;
 bool debug_nondefault();   // a result-affecting switch differs from its default

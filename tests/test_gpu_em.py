@@ -425,12 +425,15 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape):
     m = x
     S = x[..., :, None] * np.conj(x[..., None, :]) + 0.1 * np.eye(n_tx)
     out = {}
-    # default = batched panel launches; "fused" = one workgroup per trial; "valu"
+    # default = batched panel launches (complex tile products by three real MFMAs); "lookahead" =
+    # one launch per panel factoring it beside the next panel's update; "batched_c4" = four real
+    # MFMAs per complex product; "fused" = one workgroup per trial; "valu"
     # "batched_bs1": batched, with the one-step-prefetch back substitution instead of the
     # one-barrier kernel (default for L <= 272, n_rx <= 4), two-ahead three-barrier kernel
-    for impl in ("batched", "fused", "valu", "batched_bs1", "batched_bs2"):
+    for impl in ("batched", "lookahead", "batched_c4", "fused", "valu", "batched_bs1", "batched_bs2"):
         with sbce._lib.debug_env(SBCE_CHOL_IMPL=impl.split("_")[0],
-                                 SBCE_BACKSUB=impl[-1] if "_bs" in impl else "0"):
+                                 SBCE_BACKSUB=impl[-1] if "_bs" in impl else "0",
+                                 SBCE_CPLX3="0" if impl.endswith("_c4") else "1"):
             out[impl] = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], m, S,
                                          0.05)
     th_m, R, rhs, st = out["batched"]
@@ -440,6 +443,8 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape):
         ref = np.conj(X).reshape(-1)
         for impl in out:
             assert rel(out[impl][0][i], ref) < 1e-9, impl
+    assert rel(th_m, out["lookahead"][0]) < 1e-12
+    assert rel(th_m, out["batched_c4"][0]) < 1e-11
     assert rel(th_m, out["fused"][0]) < 1e-9
     assert rel(th_m, out["valu"][0]) < 1e-9
     assert rel(th_m, out["batched_bs1"][0]) < 1e-12
