@@ -257,6 +257,7 @@ __global__ __launch_bounds__(256) void act_kernel(MstepArgs a, int L, int k0) {
 // 2 x 2 MFMA tiles; 16-row chunks of both column strips staged in LDS.  The tiles of a trial run
 // back to back on one XCD (blocks are dealt round-robin over the 8 XCDs), so the strips shared
 // by the concurrently running tiles of a row or column are re-read from that XCD's L2.
+template <bool G3 = false>
 __global__ __launch_bounds__(256) void gram_kernel(MstepArgs a, int L, int ntiles) {
     __shared__ cd As[KS][TB + 1], Bs[KS][TB + 1];
     const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
@@ -278,13 +279,14 @@ __global__ __launch_bounds__(256) void gram_kernel(MstepArgs a, int L, int ntile
     const int li = lane & 15, lk = lane >> 4;
     const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
     const int nb = (L + TB - 1) / TB;
-    d4v cre[2][2], cim[2][2];
+    d4v cre[2][2], cim[2][2], c2[2][2];
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int v = 0; v < 2; ++v) {
             cre[u][v] = d4v{0.0, 0.0, 0.0, 0.0};
             cim[u][v] = d4v{0.0, 0.0, 0.0, 0.0};
+            csub_init<G3>(cre[u][v], cim[u][v], c2[u][v]);
         }
     for (int K = ti; K < nb; ++K) {
         const int k0 = K * TB;
@@ -306,16 +308,14 @@ __global__ __launch_bounds__(256) void gram_kernel(MstepArgs a, int L, int ntile
                 for (int u = 0; u < 2; ++u) av[u] = As[4 * s + lk][wr + 16 * u + li];
 #pragma unroll
                 for (int v = 0; v < 2; ++v) bv[v] = Bs[4 * s + lk][wc + 16 * v + li];
+                // C += conj(A) B  =  C - v conj(t)  with v = -conj(A), t = conj(B)
 #pragma unroll
-                for (int u = 0; u < 2; ++u)
+                for (int u = 0; u < 2; ++u) {
+                    const cd va = cmk(-av[u].x, av[u].y);
 #pragma unroll
-                    for (int v = 0; v < 2; ++v) {
-                        // C += conj(A) B:  re += ar br + ai bi ; im += ar bi - ai br
-                        cre[u][v] = mfma4(av[u].x, bv[v].x, cre[u][v]);
-                        cre[u][v] = mfma4(av[u].y, bv[v].y, cre[u][v]);
-                        cim[u][v] = mfma4(av[u].x, bv[v].y, cim[u][v]);
-                        cim[u][v] = mfma4(-av[u].y, bv[v].x, cim[u][v]);
-                    }
+                    for (int v = 0; v < 2; ++v)
+                        csub_step<G3>(cre[u][v], cim[u][v], c2[u][v], va, cmk(bv[v].x, -bv[v].y));
+                }
             }
         }
     }
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256) void gram_kernel(MstepArgs a, int L, int ntile
             for (int q = 0; q < 4; ++q) {
                 const int r = i0 + wr + 16 * u + lk + 4 * q, c = j0 + wc + 16 * v + li;
                 if (r < act && c < act) {
-                    cd val = cmk(cre[u][v][q], cim[u][v][q]);
+                    cd val = csub_out<G3>(cre[u][v], cim[u][v], c2[u][v], q);
                     // a dropped column of G is exactly zero: an uncoupled unit direction of C
                     if (r == c && val.x == 0.0) val = cmk(1.0, 0.0);
                     C[(size_t)r * L + c] = val;
@@ -550,7 +550,12 @@ hipError_t launch_minnorm(const Problem& pb, const MstepArgs& a, hipStream_t s) 
     {
         const int ntiles = nb * (nb + 1) / 2;
         const long nblk = (long)ntiles * ((pb.B + 7) / 8 * 8);
-        hipLaunchKernelGGL(gram_kernel, dim3((unsigned)nblk), dim3(256), 0, s, a, L, ntiles);
+        // three-MFMA products here too: C = G^H G is formed after the rank cut, so its rounding
+        // reaches theta (within lstsq's own) but no pivot decision
+        if (g_debug.cplx3)
+            hipLaunchKernelGGL(gram_kernel<true>, dim3((unsigned)nblk), dim3(256), 0, s, a, L, ntiles);
+        else
+            hipLaunchKernelGGL(gram_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, s, a, L, ntiles);
     }
     hipLaunchKernelGGL(ghb_kernel, dim3(nb, pb.B), dim3(256), 0, s, a, L, pb.NR);
     hipLaunchKernelGGL(gram_tol_kernel, dim3(pb.B), dim3(256), 0, s, a, L);
