@@ -542,10 +542,19 @@ class EMEngine:
     resident in HBM; ``run()`` resets theta from theta0 with a device copy and
     issues ONE sbce_em call on the current stream.  Nothing is allocated or
     synchronised inside ``run()``.
+
+    ``streams = K > 1``: ``run()`` issues the batch as K contiguous sub-batches, one sbce_em
+    call each on its own HIP stream (forked from and joined back into the current stream).
+    Trials are independent and every kernel treats them independently, so theta is bitwise
+    the same; the sub-batches' kernels overlap -- the latency-bound launches of one (the
+    Cholesky panel factors, the enumeration tail) run beside the MFMA-bound ones of another.
+    Each sub-batch has its own workspace (its work lists and counters are per call); the
+    inputs, theta and status are views of the whole-batch tensors.  ``estep()``, ``mstep()``
+    and ``mstep_phase()`` (kernel timing) stay whole-batch launches.
     """
 
     def __init__(self, batch, varn, mode="soft", solve="chol", x_d_true=None, h_true=None,
-                 partition_r=0, varx=1.0, x_sup=None):
+                 partition_r=0, varx=1.0, x_sup=None, streams=1):
         torch = _torch()
         self.torch = torch
         self.lib = _lib.load()
@@ -589,13 +598,38 @@ class EMEngine:
                               self.cons.data_ptr(), self.theta.data_ptr(), None, None, None, None,
                               self.status.data_ptr(), self.ws.data_ptr(), self.ws.numel(), None,
                               self.x_sup.data_ptr() if self.x_sup is not None else None)
+        self.subs = []
+        K = int(streams)
+        if K > 1 and B >= 2 * K and T_p and self.x_sup is None:
+            bounds = np.linspace(0, B, K + 1).astype(int)
+            for b0, b1 in zip(bounds[:-1], bounds[1:]):
+                dims = _lib.Dims(int(b1 - b0), self.n_tx, n_rx, P, T_p, T_d, self.M, int(partition_r),
+                                 self.varn, float(varx))
+                ws = torch.empty(max(_lib.workspace_bytes(dims), 16), dtype=torch.uint8, device="cuda")
+                ptrs = _lib.Ptrs(self.y_d[b0:b1].data_ptr(), self.y_p[b0:b1].data_ptr(),
+                                 self.psi_d[b0:b1].data_ptr(), self.u_p[b0:b1].data_ptr(),
+                                 self.cons.data_ptr(), self.theta[b0:b1].data_ptr(), None, None, None,
+                                 None, self.status[b0:b1].data_ptr(), ws.data_ptr(), ws.numel(), None,
+                                 None)
+                self.subs.append((dims, ptrs, ws, torch.cuda.Stream()))
 
     def run(self, itera):
         """One full EM (itera iterations) over the whole batch, stream-ordered."""
         self.theta.copy_(self.theta0)
-        rc = self.lib.sbce_em(self.dims, self.ptrs, int(itera), self.mode, self.solve,
-                              self.torch.cuda.current_stream().cuda_stream)
-        _lib.check(rc, "sbce_em")
+        cur = self.torch.cuda.current_stream()
+        if not self.subs:
+            rc = self.lib.sbce_em(self.dims, self.ptrs, int(itera), self.mode, self.solve,
+                                  cur.cuda_stream)
+            _lib.check(rc, "sbce_em")
+            return self.theta
+        ev = self.torch.cuda.Event()
+        ev.record(cur)
+        for dims, ptrs, _, st in self.subs:
+            st.wait_event(ev)
+            _lib.check(self.lib.sbce_em(dims, ptrs, int(itera), self.mode, self.solve, st.cuda_stream),
+                       "sbce_em")
+        for _, _, _, st in self.subs:
+            cur.wait_stream(st)
         return self.theta
 
     def estep(self):

@@ -661,6 +661,32 @@ def test_gaussian_sweep_entry_point(sbce):
 
 
 # ---------------------------------------------------------------- EMEngine (bench / sweeps)
+@pytest.mark.parametrize("mode,solve", [("soft", "chol"), ("hard", "chol"), ("pm_soft", "lstsq")])
+def test_engine_stream_subbatches_bitwise_equal(sbce, mode, solve):
+    """EMEngine(streams=K): the batch as K sub-batches on concurrent HIP streams (bench.py's cfg1
+    schedule) gives bitwise the theta and status of one whole-batch call, at the cfg1 geometry
+    (J = 65,536 soft E-step, L = 260 batched Cholesky) and on the PM / min-norm path."""
+    import torch
+    varn = float(sbce.signal_model.snr_to_varn(20.0))
+    if mode == "pm_soft":
+        b = sbce.signal_model.synthetic_batch(12, 3, 3, 40, 12, 40, 16, varn, seed=6)
+        kw = dict(partition_r=1)
+    else:
+        b = sbce.signal_model.synthetic_batch(12, 4, 4, 64, 16, 256, 16, varn, seed=6)
+        kw = {}
+    one = sbce.EMEngine(b, varn, mode=mode, solve=solve, **kw)
+    th1 = one.run(4).clone()
+    st1 = one.status.clone()
+    for k in (2, 4):
+        eng = sbce.EMEngine(b, varn, mode=mode, solve=solve, streams=k, **kw)
+        assert len(eng.subs) == k
+        thk = eng.run(4)
+        torch.cuda.synchronize()
+        assert torch.isfinite(torch.view_as_real(th1)).all()
+        assert torch.equal(thk, th1), k
+        assert torch.equal(eng.status, st1), k
+
+
 def test_engine_matches_em_batch_superimposed_and_gauss(sbce):
     """EMEngine (resident buffers, one sbce_em per run) equals em_batch for the modes that
     need more than the default arguments: T_p = 0 with superimposed pilots (placeholder

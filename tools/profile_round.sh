@@ -6,6 +6,9 @@
 #   (tools/pmc_summary.py; bench.py --pmc reads it for roofline.traffic),
 #   the bench line itself, and a kernel-trace --stats run of the same command.
 # Every GPU step has its own time limit; the script stops at the first failure.
+# The PMC passes run cfg1 with --streams 1 (whole-batch launches only: per-launch bytes of the
+# launches bench.py's roofline times); the bench line and the kernel trace use the default
+# schedule (four stream sub-batches at cfg1; tools/trace_summary.py keeps one row per grid).
 set -e
 TAG=${1:-r01}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -16,7 +19,7 @@ cd /tmp && export TMPDIR=/tmp
 C1="--config cfg1"
 C2="--config cfg2 --trials 256 --iters 2"
 for W in cfg1 cfg2; do
-    if [ $W = cfg1 ]; then C=$C1; PM="$C1 --steps 1 --warmup 0 --iters 2 --kernel-reps 2";
+    if [ $W = cfg1 ]; then C=$C1; PM="$C1 --steps 1 --warmup 0 --iters 2 --kernel-reps 2 --streams 1";
     else C=$C2; PM="--config cfg2 --trials 256 --iters 1 --steps 1 --warmup 0 --kernel-reps 1"; fi
     timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch_$W" -o run -- \
         python3 "$R/bench.py" $PM --no-cpu-baseline > "$O/pmc_fetch_$W.log" 2>&1
