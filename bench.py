@@ -261,14 +261,10 @@ def main():
                     help="PMC summary (default: profiles/pmc_<config>_latest.json)")
     args = ap.parse_args()
     nstreams = args.streams if args.streams is not None else (3 if args.config == "cfg1" else 1)
-    hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
-    if nstreams + 1 > hwq:
-        # one hardware queue per sub-batch stream (and the default stream): HIP maps streams onto
-        # GPU_MAX_HW_QUEUES queues (4 by default), and two sub-batches sharing a queue run one
-        # after the other (measured: 4 streams on 4 queues 276k EM-it/s, 3 streams 335k).  Read
-        # when HIP initialises, i.e. before torch touches the GPU.
-        os.environ["GPU_MAX_HW_QUEUES"] = str(min(2 * nstreams, 16))
-
+    # 3 sub-batch streams: with the default stream they fill HIP's 4 hardware queues per process
+    # (GPU_MAX_HW_QUEUES, the box's default).  Measured at cfg1: 1 stream 325k EM-it/s, 2 330k,
+    # 3 335k; 4 streams on 4 queues 276k (two sub-batches share a queue and run back to back), and
+    # with the queue count raised to 8 / 12 for 4 / 6 streams 294k / 280k.
     import torch
     import torch.distributed as dist
     import __graft_entry__ as ge
