@@ -256,11 +256,16 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
     ap.add_argument("--streams", type=int, default=None,
-                    help="sub-batches on concurrent HIP streams (default: 3 at cfg1, else 1)")
+                    help="sub-batches on concurrent HIP streams (default: 3 at cfg1 on one "
+                         "process, else 1)")
     ap.add_argument("--pmc", default=None,
                     help="PMC summary (default: profiles/pmc_<config>_latest.json)")
     args = ap.parse_args()
-    nstreams = args.streams if args.streams is not None else (3 if args.config == "cfg1" else 1)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    # multi-process runs keep one stream per rank: RCCL's own streams take hardware queues too,
+    # and the sub-batch schedule has not been measured beside them
+    nstreams = args.streams if args.streams is not None else (
+        3 if args.config == "cfg1" and world_env == 1 else 1)
     # 3 sub-batch streams: with the default stream they fill HIP's 4 hardware queues per process
     # (GPU_MAX_HW_QUEUES, the box's default).  Measured at cfg1: 1 stream 325k EM-it/s, 2 330k,
     # 3 335k; 4 streams on 4 queues 276k (two sub-batches share a queue and run back to back), and
