@@ -240,9 +240,49 @@ def cpu_baseline_reference_structured(cfg, varn, seed, budget_s=20.0):
                        f"BLAS threads={threads or 'default'}")}
 
 
-def main():
+def rank_envs(n, port, base=None):
+    """Environments of the N ranks of a single-node run (torchrun's variables): rank r drives
+    GPU r, rendezvous on 127.0.0.1:port."""
+    base = dict(os.environ if base is None else base)
+    return [dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            for r in range(n)]
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, timeout=None):
+    """`bench.py --gpus N` started without WORLD_SIZE: start N rank processes of this same
+    script as CHILDREN (one per GPU, torchrun's environment), wait for all, return the worst exit
+    code.  Called before this process touches the GPU; the parent never execs.  Rank 0 prints
+    the JSON line (children inherit stdout)."""
+    import subprocess
+    port = _free_port()
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env)
+             for env in rank_envs(n, port)]
+    codes = []
+    try:
+        for p in procs:
+            codes.append(p.wait(timeout=timeout))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node (one rank each).  Without WORLD_SIZE and N > 1 the "
+                         "ranks are started here; under torchrun it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="cfg1", choices=sorted(CONFIGS))
@@ -256,33 +296,139 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
     ap.add_argument("--streams", type=int, default=None,
-                    help="sub-batches on concurrent HIP streams (default: 3 at cfg1 on one "
-                         "process, else 1)")
+                    help="sub-batches on concurrent HIP streams per GPU (default: 3 at cfg1, else 1)")
+    ap.add_argument("--rccl-init", choices=["lazy", "eager"], default="lazy",
+                    help="multi-rank runs: create the RCCL communicator at its first collective "
+                         "(after the timed region; default) or at process-group init")
+    ap.add_argument("--dist-at-world1", action="store_true",
+                    help="initialise torch.distributed (RCCL) even for one rank (A/B of the "
+                         "multi-rank schedule on a one-GPU box)")
+    ap.add_argument("--selftest", action="store_true",
+                    help="CPU plumbing self-test (gloo, no GPU, no estimator work): the launcher, "
+                         "barriers, max-over-ranks timing and the accumulator all-reduce only")
     ap.add_argument("--pmc", default=None,
                     help="PMC summary (default: profiles/pmc_<config>_latest.json)")
-    args = ap.parse_args()
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    # multi-process runs keep one stream per rank: RCCL's own streams take hardware queues too,
-    # and the sub-batch schedule has not been measured beside them
-    nstreams = args.streams if args.streams is not None else (
-        3 if args.config == "cfg1" and world_env == 1 else 1)
+    return ap.parse_args(argv)
+
+
+def check_world(args, env=None):
+    """World size of this process and the --gpus consistency rule; raises SystemExit(2) when
+    --gpus disagrees with the launcher's WORLD_SIZE."""
+    env = os.environ if env is None else env
+    world = int(env.get("WORLD_SIZE", "1"))
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the run would not measure "
+              f"{args.gpus} GPUs", file=sys.stderr)
+        raise SystemExit(2)
+    return world
+
+
+class Ranks:
+    """Process-group plumbing of a run: host-side (gloo) barriers and the max-over-ranks clock,
+    so that nothing of RCCL exists while the timed region runs unless --rccl-init eager; the
+    Monte-Carlo accumulators go through ONE RCCL all-reduce afterwards."""
+
+    def __init__(self, args, world):
+        self.world = world
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        self.cpu = None
+        self.selftest = args.selftest
+        use_dist = world > 1 or args.dist_at_world1
+        if not args.selftest:
+            import torch
+            torch.cuda.set_device(self.local)
+        if use_dist:
+            import torch
+            import torch.distributed as dist
+            self.dist = dist
+            if args.selftest:
+                dist.init_process_group("gloo")
+                self.cpu = None
+            else:
+                kw = ({"device_id": torch.device("cuda", self.local)}
+                      if args.rccl_init == "eager" else {})
+                dist.init_process_group("nccl", **kw)
+                self.cpu = dist.new_group(backend="gloo")
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier(group=self.cpu)
+        if not self.selftest:
+            import torch
+            torch.cuda.synchronize()
+
+    def max_time(self, t):
+        if self.dist is None:
+            return t
+        import torch
+        v = torch.tensor([t], dtype=torch.float64)
+        self.dist.all_reduce(v, op=self.dist.ReduceOp.MAX, group=self.cpu)
+        return float(v.item())
+
+    def allreduce_sum(self, t):
+        """The Monte-Carlo accumulators: RCCL over xGMI (gloo in the self-test)."""
+        if self.dist is not None:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return t
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+def selftest(args, ranks):
+    """--selftest: the multi-rank code path with a fixed host-side step instead of the estimator
+    (CPU tests of the launcher; never a measurement)."""
+    import torch
+    B, iters = 8, 2
+    for _ in range(args.warmup):
+        time.sleep(0.01)
+    ranks.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.01)
+    ranks.barrier()
+    elapsed = ranks.max_time(time.perf_counter() - t0)
+    acc = ranks.allreduce_sum(torch.tensor([0.5 * B * (ranks.rank + 1), float(B)],
+                                           dtype=torch.float64))
+    if ranks.rank == 0:
+        print(json.dumps({"metric": "selftest (plumbing only, no estimator work)",
+                          "value": ranks.world * B * iters * args.steps / elapsed,
+                          "unit": "EM-iterations/s", "n_gpus": ranks.world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                          "dtype": "none", "data": "selftest",
+                          "config": {"workload": "selftest", "parallelism": f"trials-sharded x{ranks.world}"},
+                          "nmse_mean": float(acc[0] / acc[1]),
+                          "trials_total": int(acc[1].item())}), flush=True)
+    ranks.close()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus is not None and args.gpus > 1:
+        # no launcher: start one rank per GPU as child processes (nothing here has touched
+        # the GPU yet) and exit with their status
+        raise SystemExit(launch_ranks(args.gpus, argv))
+    world_env = check_world(args)
+    if args.selftest:
+        ranks = Ranks(args, world_env)
+        return selftest(args, ranks)
     # 3 sub-batch streams: with the default stream they fill HIP's 4 hardware queues per process
     # (GPU_MAX_HW_QUEUES, the box's default).  Measured at cfg1: 1 stream 325k EM-it/s, 2 330k,
     # 3 335k; 4 streams on 4 queues 276k (two sub-batches share a queue and run back to back), and
-    # with the queue count raised to 8 / 12 for 4 / 6 streams 294k / 280k.
+    # with the queue count raised to 8 / 12 for 4 / 6 streams 294k / 280k.  Multi-rank runs keep
+    # the same schedule: the RCCL communicator (and its streams) is created lazily at the
+    # accumulator all-reduce after the timed region (DESIGN.md §5).
+    nstreams = args.streams if args.streams is not None else (3 if args.config == "cfg1" else 1)
     import torch
-    import torch.distributed as dist
     import __graft_entry__ as ge
     pkg = ge.package()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+    ranks = Ranks(args, world_env)
+    world, rank = ranks.world, ranks.rank
 
     cfg = list(CONFIGS[args.config])
     if args.trials:
@@ -302,30 +448,20 @@ def main():
     del batch
     torch.cuda.synchronize()
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
     for _ in range(args.warmup):
         eng.run(iters)
-    barrier()
+    ranks.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.run(iters)
     torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+    ranks.barrier()
+    elapsed = ranks.max_time(time.perf_counter() - t0)
 
     # ---- the one collective: Monte-Carlo NMSE accumulators (sum NMSE, count) ----
     nm = eng.nmse()
     acc = torch.stack([nm.sum(), torch.tensor(float(B), dtype=torch.float64, device="cuda")])
-    if world > 1:
-        dist.all_reduce(acc, op=dist.ReduceOp.SUM)
+    ranks.allreduce_sum(acc)
     nmse_mean = float(acc[0] / acc[1])
     # SBCE_STATUS_NONHPD only: the PILOT / DETECTOR bits are informational
     nonhpd = int(((eng.status & pkg._lib.SBCE_STATUS_NONHPD) != 0).sum().item())
@@ -478,7 +614,8 @@ def main():
                    "T_d": T_d, "M": M, "trials_per_gpu": B, "em_iters": iters,
                    "snr_db": args.snr, "estep": mode, "partition_r": part_r, "solve": solve,
                    "parallelism": f"trials-sharded x{world}",
-                   "streams_per_gpu": len(eng.subs) or 1},
+                   "streams_per_gpu": len(eng.subs) or 1,
+                   "rccl_init": args.rccl_init if ranks.dist is not None else None},
         "schedule": (f"per GPU: {len(eng.subs)} contiguous sub-batches of the {B} trials, one sbce_em "
                      f"each on its own HIP stream (bitwise the same theta as one call); kernels_ms "
                      f"and the rooflines time whole-batch launches alone" if eng.subs else
@@ -504,8 +641,7 @@ def main():
             cfg, varn, args.seed)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    ranks.close()
 
 
 if __name__ == "__main__":

@@ -3,7 +3,8 @@ estimator with every trial of a sweep point batched into ONE sbce_em call.
 
   nmse_vs_tp   "Proposed method/Proposed_method_NMSEvsTp.py":133-176
   nmse_vs_td   "Proposed method/Proposed_method_NMSEvsTd.py":121-157
-  nmse_vs_snr  "Proposed method/SNR/all_Detectors.py":331-395 (exact and log-max EMs)
+  nmse_vs_snr  "Proposed method/SNR/all_Detectors.py":331-395 (its five EMs: PM r=1, log-max,
+               ZF, MMSE, exact)
   ser_vs_snr   "Proposed method/SER/log_max_SER.py":124-167 (log-max EM decisions)
   nmse_vs_tp_superimposed  "Parallel/ParallelProtocol_Tp.py":106-136 (superimposed pilots)
   nmse_vs_tp_gaussian      "Proposed method/MIMO_Gaussian_proposed.py":158-177 (Gaussian prior)
@@ -159,22 +160,57 @@ def gen_snr(SNR=(-5, 0, 5, 10, 15, 20), T_d=50, T_p=12, N=10, n_rx=2, n_tx=2, mo
     return points, varns
 
 
+# The five EMs of the NMSE-vs-SNR figure, PMd/SNR/all_Detectors.py:372-377, in the script's call
+# order: (E-step mode, reference EM, oracle early stop on the true h as THIS script has it, plot
+# label :396-401).  Unlike all_detectorsvsTd.py (DETECTORS below, every EM stops), only em_pm
+# stops here (:234-236); em_zf's stop is commented out (:125-127); em_mmse, em_ml, em have none.
+SNR_DETECTORS = {
+    "pm_soft": ("em_pm :170-240 (posterior-weighted list, partition_r_1 = 1)", True,
+                "Soft decision-PM r =1"),
+    "hard": ("em_ml :132-167 (log-max)", False, "log-max"),
+    "zf": ("em_zf :92-130", False, "Zero forcing"),
+    "mmse": ("em_mmse :53-90", False, "MMSE"),
+    "soft": ("em :242-274 (exact posterior)", False, "Exact"),
+}
+
+
 def nmse_vs_snr(SNR=(-5, 0, 5, 10, 15, 20), T_d=50, T_p=12, N=10, n_rx=2, n_tx=2, itera=5,
-                monte_iter=15, M=4, power=10.0, seed=0, replay=True, modes=("soft", "hard"),
-                varh=1.0):
-    """Mean NMSE per SNR for the exact ('soft', "Exact") and log-max ('hard') EMs
-    (PMd/SNR/all_Detectors.py:362-395; varn = power / 10^(SNR/10), :351-354)."""
+                monte_iter=15, M=4, power=10.0, seed=0, replay=True, modes=tuple(SNR_DETECTORS),
+                varh=1.0, partition_r=1, return_status=False):
+    """Mean NMSE per SNR of the five EMs of PMd/SNR/all_Detectors.py (driver :362-395; varn =
+    power / 10^(SNR/10), :351-354): em_pm (r = 1), em_ml, em_zf, em_mmse and the exact em, each
+    with that script's own early-stop pattern (SNR_DETECTORS) and np.linalg.solve M-step.
+
+    One batched sbce_em per (SNR point, detector) over this rank's trials; the accumulators of
+    every (detector, SNR) point are all-reduced ONCE at the end.  Returns (SNR, {mode: curve});
+    with return_status also {mode: (len(SNR),) count of trials whose status word is non-zero
+    (e.g. SBCE_STATUS_DETECTOR: the reference's nearest_symbol_ecul would raise IndexError)}."""
     dist, world, rank = _dist()
     mine = shard(monte_iter, world, rank).tolist()
     points, varns = gen_snr(SNR, T_d, T_p, N, n_rx, n_tx, monte_iter, M, power, seed, replay,
                             varh, keep=mine)
-    out = {}
-    for mode in modes:
-        acc = Accumulators(len(SNR))
-        _run_points(points, qam_constellation(M), list(varns), itera, mode, acc, dist)
-        acc.allreduce(dist)
-        out[mode] = acc.mean_nmse()
-    return np.asarray(SNR), out
+    cons = qam_constellation(M)
+    nm, ns = len(modes), len(SNR)
+    acc = Accumulators(nm * ns, n_extra=1)
+    for k, trials in enumerate(points):
+        if not trials:
+            continue
+        b = _pack(trials, None)
+        for mi, mode in enumerate(modes):
+            stop = SNR_DETECTORS[mode][1]
+            r = em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], cons, varns[k], itera,
+                         b["theta0"], mode=mode,
+                         partition_r=partition_r if mode.startswith("pm") else 0,
+                         h_true=b["h"] if stop else None)
+            acc.add(mi * ns + k, _nmse(r["theta"], b["h"]),
+                    extra_values=(r["status"] != 0).astype(float)[:, None])
+    acc.allreduce(dist)                   # the sweep's only collective
+    mean = acc.mean_nmse().reshape(nm, ns)
+    curves = {mode: mean[mi] for mi, mode in enumerate(modes)}
+    if return_status:
+        flagged = acc.extra[:, 0].reshape(nm, ns)
+        return np.asarray(SNR), curves, {mode: flagged[mi] for mi, mode in enumerate(modes)}
+    return np.asarray(SNR), curves
 
 
 def gen_ser(SNR=(-5, 0, 5, 10, 15, 20), T_d=50, T_p=20, N=30, n_rx=2, n_tx=2, monte_iter=75, M=4,

@@ -201,6 +201,90 @@ def case_kat2():
         N=N, n_tx=n_tx, n_rx=n_rx, T_d=T_d, T_p=T_p, M=M, itera=itera, seed=0)
 
 
+_SNR_DETS = ("pm", "ml", "zf", "mmse", "em")
+
+
+def _kat2_driver_job(job):
+    """One (trial, SNR point) of PMd/SNR/all_Detectors.py's driver: its five EMs in the order of
+    :372-377, each with the script's own early-stop pattern (em_pm stops on the true h, :234-236;
+    em_zf's stop is commented out, :125-127; em_mmse, em_ml and em have none)."""
+    i, k, d, varn, N, n_tx, M, T_d, T_p, itera, partition_r = job
+    ns = load_defs(os.path.join(PMD, "SNR", "all_Detectors.py"), N=N, n_tx=n_tx,
+                   beta_min=0.0, beta_max=2 * np.pi, qamCons=d["cons"])
+    common = (d["Y_d"], d["Y_p"], T_d, T_p, d["Z_p"], d["Ptd"])
+    out = {}
+    for det in _SNR_DETS:
+        try:
+            if det == "pm":
+                th = quiet(ns["em_pm"], *common, M, varn, itera, d["h0"], d["h"], n_tx, partition_r,
+                           d["X_d"], d["cons"])
+            elif det == "ml":
+                th = quiet(ns["em_ml"], *common, d["aps"], M, varn, itera, d["h0"])
+            elif det == "zf":
+                th = quiet(ns["em_zf"], *common, d["aps"], M, varn, itera, d["h0"], d["h"])
+            elif det == "mmse":
+                th = quiet(ns["em_mmse"], *common, d["aps"], M, varn, itera, d["h0"], d["h"])
+            else:
+                th = quiet(ns["em"], *common, d["aps"], M, varn, itera, d["h0"])
+            out[det] = np.asarray(th, dtype=complex).reshape(-1)
+        except IndexError:           # nearest_symbol_ecul's flat index past the table (:48-51)
+            out[det] = None
+    return i, k, out
+
+
+def case_kat2_driver(monte_iter=3, seed=0):
+    """PMd/SNR/all_Detectors.py's whole driver (:362-395) for `monte_iter` trials after
+    np.random.seed(seed), with the script's own helpers, constants (:331-354) and all FIVE EMs
+    of the NMSE-vs-SNR figure (em_pm r=1, em_ml, em_zf, em_mmse, em): per-trial thetas and
+    NMSE (the script's trace expression, :382-387) and the averaged curves (:390-395).  Data
+    are generated sequentially in the driver's draw order; the EM runs (mpmath, ~1 min each)
+    are spread over worker processes."""
+    N, n_tx, n_rx, T_d, T_p, M, itera, partition_r = 10, 2, 2, 50, 12, 4, 5, 1
+    SNR = [-5, 0, 5, 10, 15, 20]
+    varns = np.array([10 / np.power(10, s / 10) for s in SNR])
+    ns = load_defs(os.path.join(PMD, "SNR", "all_Detectors.py"), N=N, n_tx=n_tx,
+                   beta_min=0.0, beta_max=2 * np.pi)
+    np.random.seed(seed)
+    jobs, data = [], {}
+    for i in range(monte_iter):
+        h = quiet(ns["channelMatrix"], n_tx, n_rx, N, 1)
+        X_d, aps, cons = ns["symbols"](n_tx, M, T_d)
+        X_p = ns["pilotSymbols"](n_tx, M, T_p)
+        Ptp, Ptd = ns["irsMatrix"](T_p, T_d, N, 0, 1)
+        Ptd = np.insert(Ptd, 0, np.ones((1, T_d), dtype="complex128"), axis=0)
+        data[f"h{i}"], data[f"X_d{i}"] = h, np.stack(X_d)[..., 0]
+        data[f"X_p{i}"], data[f"Ptd{i}"] = np.stack(X_p)[..., 0], Ptd
+        Z_p = None
+        for k in range(len(SNR)):
+            Y_p, Y_d, Z_p, Z_d, h0 = ns["receivedSignals"](T_p, T_d, Ptp, Ptd, n_rx, n_tx, X_d,
+                                                            X_p, h, varns[k], M)
+            data[f"Y_p{i}_{k}"], data[f"Y_d{i}_{k}"] = np.stack(Y_p)[..., 0], np.stack(Y_d)[..., 0]
+            data[f"h0{i}_{k}"] = np.asarray(h0).reshape(-1)
+            data[f"Z_p{i}"] = np.stack(Z_p)
+            d = dict(Y_d=Y_d, Y_p=Y_p, Z_p=Z_p, Ptd=Ptd, h0=h0, h=h, X_d=X_d, aps=aps, cons=cons)
+            jobs.append((i, k, d, varns[k], N, n_tx, M, T_d, T_p, itera, partition_r))
+    import multiprocessing as mp_
+    if mp_.current_process().daemon:
+        results = [_kat2_driver_job(j) for j in jobs]
+    else:
+        with Pool(7) as pool:
+            results = pool.map(_kat2_driver_job, jobs)
+    nm = np.full((len(_SNR_DETS), monte_iter, len(SNR)), np.nan)
+    for i, k, out in results:
+        for di, det in enumerate(_SNR_DETS):
+            if out[det] is None:
+                continue
+            data[f"{det}_theta{i}_{k}"] = out[det]
+            e = out[det][:, None] - data[f"h{i}"][:, None]
+            nm[di, i, k] = (np.trace(np.abs(e.conj().T @ e)) /
+                            np.linalg.norm(data[f"h{i}"][:, None]) ** 2)
+    data.update(nmse=nm, curve=np.average(nm, axis=1), dets=np.array(_SNR_DETS), snr=np.array(SNR),
+                varn=varns, aps=aps, cons=cons, Ptp=Ptp, N=N, n_tx=n_tx,
+                n_rx=n_rx, T_d=T_d, T_p=T_p, M=M, itera=itera, partition_r=partition_r,
+                monte_iter=monte_iter, seed=seed)
+    return "kat2_driver", data
+
+
 def case_shape(name, N, n_tx, n_rx, T_d, T_p, M, varn, itera, seed):
     """Extra shapes through the north-star em (odd stream splits, 16/64-QAM)."""
     ns = load_defs(os.path.join(PMD, "Proposed_method_NMSEvsTp.py"),
@@ -457,6 +541,7 @@ CASES = {
     "kat1_s7": (case_kat1, (7,)),
     "kat1_s11": (case_kat1, (11,)),
     "kat2_snr": (case_kat2, ()),
+    "kat2_driver": (case_kat2_driver, ()),
     "root_tp": (case_root, ()),
     "nt4_m4": (case_shape, ("nt4_m4", 3, 4, 4, 16, 8, 4, 0.1, 2, 5)),
     "nt3_m4": (case_shape, ("nt3_m4", 3, 3, 2, 10, 8, 4, 0.2, 2, 9)),
@@ -476,6 +561,9 @@ def run(name):
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(CASES)
+    if len(names) == 1:                  # in-process: a case may use its own worker pool
+        print("%s: %.1fs" % run(names[0]), flush=True)
+        sys.exit(0)
     with Pool(min(len(names), 7)) as pool:
         for key, dt in pool.imap_unordered(run, names):
             print(f"{key}: {dt:.1f}s", flush=True)

@@ -121,3 +121,69 @@ def test_allreduce_uses_collective_device_by_default(sbce, monkeypatch):
     # an explicit device wins and skips the backend query
     acc.allreduce(_StubDist("nccl"), device="cpu")
     assert seen == ["nccl"]
+
+
+# ---------------------------------------------------------------- bench.py --gpus N launcher
+def _bench():
+    import importlib
+    import sys
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    return importlib.import_module("bench")
+
+
+def test_bench_rank_envs():
+    """bench.launch_ranks gives rank r of N torchrun's variables: RANK = LOCAL_RANK = r (GPU r),
+    WORLD_SIZE = N, rendezvous on 127.0.0.1."""
+    b = _bench()
+    envs = b.rank_envs(4, 29555, base={"PATH": "/usr/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    for e in envs:
+        assert e["WORLD_SIZE"] == "4" and e["LOCAL_WORLD_SIZE"] == "4"
+        assert e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29555"
+        assert e["PATH"] == "/usr/bin" and e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_bench_gpus_must_match_world_size():
+    b = _bench()
+    assert b.check_world(b.parse_args(["--gpus", "4"]), env={"WORLD_SIZE": "4"}) == 4
+    assert b.check_world(b.parse_args([]), env={"WORLD_SIZE": "2"}) == 2
+    assert b.check_world(b.parse_args([]), env={}) == 1
+    with pytest.raises(SystemExit) as e:
+        b.check_world(b.parse_args(["--gpus", "8"]), env={"WORLD_SIZE": "1"})
+    assert e.value.code == 2
+
+
+def _run_bench(args, env_extra=None):
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env,
+                       capture_output=True, text=True, timeout=300)
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    return r, lines
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_gpus_n_launches_n_ranks(n):
+    """`bench.py --gpus N` with no launcher starts N ranks (gloo self-test: the launcher, the
+    host barriers, the max-over-ranks clock and the accumulator all-reduce) and prints ONE line
+    with n_gpus = N whose accumulators cover every rank."""
+    r, lines = _run_bench(["--gpus", str(n), "--selftest", "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1
+    line = lines[0]
+    assert line["n_gpus"] == n and line["steps"] == 2 and line["scaling"] == "weak"
+    assert line["trials_total"] == 8 * n
+    assert line["nmse_mean"] == pytest.approx(0.5 * sum(range(1, n + 1)) / n)
+
+
+def test_bench_mismatched_launch_fails():
+    """Under a launcher (WORLD_SIZE set) a disagreeing --gpus exits non-zero before any work."""
+    r, lines = _run_bench(["--gpus", "4", "--selftest"], {"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode == 2 and not lines
+    assert "WORLD_SIZE=2" in r.stderr

@@ -32,6 +32,50 @@ def test_five_detector_ems_match_reference_fixture(sbce):
         assert abs(nmse(r["theta"][0], d["h"]) / float(d[f"{key}_nmse"]) - 1) < 1e-9, key
 
 
+SNR_MODES = {"pm": ("pm_soft", True), "ml": ("hard", False), "zf": ("zf", False),
+             "mmse": ("mmse", False), "em": ("soft", False)}
+
+
+def test_snr_figure_five_ems_match_reference_driver(sbce):
+    """The north-star figure's five EMs (PMd/SNR/all_Detectors.py:372-377), each with THAT
+    script's early-stop pattern (em_pm stops on h, :234-236; em_zf's stop is commented out,
+    :125-127; em_mmse / em_ml / em have none): device theta and NMSE of every (trial, SNR point)
+    of the reference's own driver run (kat2_driver: 3 trials x 6 SNR points) at 1e-9."""
+    k = golden("kat2_driver")
+    n_rx, itera, r = int(k["n_rx"]), int(k["itera"]), int(k["partition_r"])
+    dets = [str(x) for x in k["dets"]]
+    for i in range(int(k["monte_iter"])):
+        up = u_from_zp(k[f"Z_p{i}"], n_rx)[None]
+        for j in range(len(k["snr"])):
+            for key, (mode, stop) in SNR_MODES.items():
+                res = sbce.em_batch(k[f"Y_d{i}_{j}"][None], k[f"Y_p{i}_{j}"][None],
+                                    k[f"Ptd{i}"].T[None], up, k["cons"], float(k["varn"][j]), itera,
+                                    k[f"h0{i}_{j}"][None], mode=mode,
+                                    partition_r=r if key == "pm" else 0,
+                                    h_true=k[f"h{i}"][None] if stop else None)
+                assert rel(res["theta"][0], k[f"{key}_theta{i}_{j}"]) < 1e-9, (key, i, j)
+                nm = nmse(res["theta"][0], k[f"h{i}"])
+                assert abs(nm / k["nmse"][dets.index(key), i, j] - 1) < 1e-9, (key, i, j)
+                assert res["status"][0] == 0
+
+
+def test_snr_sweep_entry_point_five_curves_vs_reference(sbce):
+    """North-star parity through the sweep entry point: sweeps.nmse_vs_snr (seed-0 replay of the
+    script's draw order, every trial of an SNR point in one sbce_em call per detector, ONE
+    all-reduce) gives the reference driver's five averaged curves (:390-395).  Measured bar 1e-9;
+    the north-star bar is 1e-3."""
+    k = golden("kat2_driver")
+    snr, curves, flagged = sbce.sweeps.nmse_vs_snr(monte_iter=int(k["monte_iter"]), seed=0,
+                                                   return_status=True)
+    assert np.array_equal(snr, k["snr"])
+    dets = [str(x) for x in k["dets"]]
+    for key, (mode, _) in SNR_MODES.items():
+        ref = k["curve"][dets.index(key)]
+        assert np.allclose(curves[mode], ref, rtol=1e-9, atol=0), (mode, curves[mode], ref)
+        assert np.all(np.abs(curves[mode] / ref - 1) < 1e-3)
+        assert not flagged[mode].any()
+
+
 def test_detector_grid_driver_reproduces_reference_point(sbce):
     """sweeps.nmse_grid_detectors at the fixture's T_d point and seed: the five curves'
     values are the reference's."""

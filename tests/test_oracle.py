@@ -515,3 +515,110 @@ def test_oracle_matches_reference_at_cfg1_kernel_instantiation():
     for it in (1, int(d["itera"])):
         th = em_reduced(d["Y_d"], d["Y_p"], Up, d["Ptd"], d["aps"], float(d["varn"]), it, d["h0"])
         assert rel(th, d[f"theta_it{it}"]) < 1e-11, it
+
+
+# ------------------------------------------------- the five curves of PMd/SNR/all_Detectors.py
+_SNR_KEYS = {"pm_soft": "pm", "hard": "ml", "zf": "zf", "mmse": "mmse", "soft": "em"}
+
+
+def _oracle_snr_em(mode, y_d, y_p, psi, u_p, cons, varn, itera, theta0, h, partition_r):
+    """The oracle twin of one SNR-script EM (CPU), one trial."""
+    from oracle.pm import em_pm
+    from oracle.detectors import em_detector
+    n_rx = y_d.shape[1]
+    n_tx = u_p.shape[1] // psi.shape[0]
+    if mode == "pm_soft":
+        return em_pm(y_d, y_p, u_p, psi, varn, itera, theta0, n_tx, n_rx, partition_r, cons,
+                     soft=True, h=h)
+    aps = aps_from_cons(cons, n_tx)
+    if mode in ("zf", "mmse"):
+        return em_detector(y_d, y_p, u_p, psi, aps, varn, itera, theta0, n_tx, n_rx, mode, h=h)
+    return em_reduced(y_d, y_p, u_p, psi, aps, varn, itera, theta0, mode=mode)
+
+
+def test_kat2_driver_five_detectors_oracle_vs_reference():
+    """The oracle's five EMs (PM r=1 with the early stop, log-max, ZF, MMSE, exact; no early stop
+    for the last four, as PMd/SNR/all_Detectors.py has them) against the reference's own run of
+    the script's driver (tests/golden/kat2_driver.npz: 3 trials x 6 SNR points)."""
+    k = golden("kat2_driver")
+    n_rx, itera, r = int(k["n_rx"]), int(k["itera"]), int(k["partition_r"])
+    dets = [str(x) for x in k["dets"]]
+    for i in range(int(k["monte_iter"])):
+        Up = u_from_zp(k[f"Z_p{i}"], n_rx)
+        for j in range(len(k["snr"])):
+            for mode, key in _SNR_KEYS.items():
+                if f"{key}_theta{i}_{j}" not in k:
+                    continue
+                stop = mode == "pm_soft"
+                th = _oracle_snr_em(mode, k[f"Y_d{i}_{j}"], k[f"Y_p{i}_{j}"], k[f"Ptd{i}"], Up,
+                                    k["cons"], float(k["varn"][j]), itera, k[f"h0{i}_{j}"],
+                                    k[f"h{i}"] if stop else None, r)
+                assert rel(th, k[f"{key}_theta{i}_{j}"]) < 1e-11, (mode, i, j)
+                nm = nmse(th, k[f"h{i}"])
+                assert abs(nm / k["nmse"][dets.index(key), i, j] - 1) < 1e-9
+
+
+def test_snr_sweep_replays_reference_driver_data(sbce):
+    """sweeps.gen_snr (seed 0) reproduces the SNR script's draw order over several trials."""
+    k = golden("kat2_driver")
+    n = int(k["monte_iter"])
+    points, varns = sbce.sweeps.gen_snr(monte_iter=n, seed=0)
+    assert np.allclose(varns, k["varn"], rtol=1e-15, atol=0)
+    for j in range(len(k["snr"])):
+        for i in range(n):
+            t = points[j][i]
+            assert np.array_equal(t["h"], k[f"h{i}"])
+            assert rel(t["Y_d"], k[f"Y_d{i}_{j}"]) < 1e-14      # y = Z h + n, summation order
+            assert rel(t["Y_p"], k[f"Y_p{i}_{j}"]) < 1e-14
+            assert np.array_equal(t["Psi_d"], k[f"Ptd{i}"])
+            assert rel(t["h0"], k[f"h0{i}_{j}"]) < 1e-12
+
+
+def test_snr_sweep_five_detectors_one_collective(sbce, monkeypatch):
+    """Host logic of sweeps.nmse_vs_snr on the CPU: every detector with the script's early-stop
+    flag (h passed to em_pm only), partition_r = 1 for the PM list, and ONE all-reduce for all
+    (detector, SNR) accumulators.  em_batch is replaced by the oracle here (GPU: test_gpu_sweeps)."""
+    k = golden("kat2_driver")
+    seen = []
+
+    def fake_em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft",
+                      partition_r=0, h_true=None, **kw):
+        seen.append((mode, partition_r, h_true is not None))
+        th = np.stack([_oracle_snr_em(mode, y_d[b], y_p[b], psi_d[b].T, u_p[b], cons, varn, itera,
+                                      theta0[b], None if h_true is None else h_true[b],
+                                      partition_r) for b in range(len(y_d))])
+        return dict(theta=th, status=np.zeros(len(y_d), dtype=np.int32))
+
+    class Gloo:
+        class ReduceOp:
+            SUM = "sum"
+
+        def __init__(self):
+            self.calls = 0
+
+        def is_available(self):
+            return True
+
+        def is_initialized(self):
+            return True
+
+        def get_backend(self):
+            return "gloo"
+
+        def all_reduce(self, t, op=None):
+            self.calls += 1
+
+    stub = Gloo()
+    monkeypatch.setattr(sbce.sweeps, "em_batch", fake_em_batch)
+    monkeypatch.setattr(sbce.sweeps, "_dist", lambda: (stub, 1, 0))
+    snr, curves, flagged = sbce.sweeps.nmse_vs_snr(monte_iter=int(k["monte_iter"]), seed=0,
+                                                   return_status=True)
+    assert stub.calls == 1
+    assert {(m, r, s) for m, r, s in seen} == {("pm_soft", 1, True), ("hard", 0, False),
+                                              ("zf", 0, False), ("mmse", 0, False),
+                                              ("soft", 0, False)}
+    dets = [str(x) for x in k["dets"]]
+    for mode, key in _SNR_KEYS.items():
+        ref = k["curve"][dets.index(key)]
+        assert np.allclose(curves[mode], ref, rtol=1e-9, atol=0), mode
+        assert not flagged[mode].any()
