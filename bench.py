@@ -166,6 +166,25 @@ def phase_traffic(pmc, kernels, anchor):
             sum(e["write_bytes_total"] for e in ents) / anc["launches_write"])
 
 
+def host_threads():
+    """Threads a NumPy port can use here: the affinity set, capped by OMP_NUM_THREADS (BLAS;
+    16 on the GPU box).  NumPy's elementwise work itself is single-threaded."""
+    threads = os.environ.get("OMP_NUM_THREADS")
+    cores = len(os.sched_getaffinity(0))
+    if threads and threads.isdigit():
+        cores = min(cores, int(threads))
+    return cores
+
+
+def hypotheses_per_symbol(mode, n_tx, M, part_r=0):
+    """Hypotheses the reference's E-step loop visits per data symbol: every one of M^n_tx for the
+    exact / log-max EMs, the M^(p+1) list of the PM detectors (p = int(partition_r / log2 M),
+    PMd/PM.py:74-92)."""
+    if mode.startswith("pm"):
+        return float(M) ** (int(part_r / np.log2(M)) + 1)
+    return float(M) ** n_tx
+
+
 def cpu_baseline(cfg, varn, seed, iters=2, mode="soft", part_r=0):
     """Oracle port (vectorised float64 NumPy reduced form, or the PM list oracle) on
     1 trial x `iters` EM iterations of the same configuration: ~10-30 s of CPU work."""
@@ -186,24 +205,22 @@ def cpu_baseline(cfg, varn, seed, iters=2, mode="soft", part_r=0):
                    b["theta0"][0], mode=mode)
     dt = time.perf_counter() - t0
     threads = os.environ.get("OMP_NUM_THREADS")
-    # threads actually usable by the port: NumPy elementwise work is single-threaded,
-    # BLAS calls use up to OMP_NUM_THREADS (16 on the GPU box), never more than the affinity
-    cores = len(os.sched_getaffinity(0))
-    if threads and threads.isdigit():
-        cores = min(cores, int(threads))
-    return {"value": iters / dt, "unit": "EM-iterations/s", "cores": cores,
+    return {"value": iters / dt, "unit": "EM-iterations/s", "cores": host_threads(),
             "kind": "port",
             "sample": f"1 trial x {iters} EM iterations of the same config, "
                       f"{'oracle/pm.py' if mode.startswith('pm') else 'oracle/em_reduced.py'} "
                       f"(NumPy float64, BLAS threads={threads or 'default'}), {dt:.2f} s"}
 
 
-def cpu_baseline_reference_structured(cfg, varn, seed, budget_s=20.0):
+def cpu_baseline_reference_structured(cfg, varn, seed, budget_s=20.0, mode="soft", part_r=0):
     """the reference's own loop structure (oracle/em_loop.py: dense Kronecker
     regressor Z_{t,j} per hypothesis, K x K accumulation of every hypothesis, LAPACK solve on the
     K x K system -- PMd/Proposed_method_NMSEvsTp.py:50-83 in float64 instead of mpmath) timed at
     the plumbing shape (BASELINE configs[0]: 2x2, N_RIS = 16, T_p = 16, T_d = 50, 4-QAM), then
-    extrapolated to the bench workload with the loop's O(T_d J K^2) cost model."""
+    extrapolated to the bench workload with the loop's O(T_d J K^2) cost model, J = the
+    hypotheses the workload's E-step visits per symbol (hypotheses_per_symbol: M^n_tx exact,
+    the PM list M^(p+1) for the PM workloads, whose loop PMd/PM.py:79-104 accumulates every list
+    member the same way)."""
     import importlib
     from oracle.em_loop import em_loop
     pkg = importlib.import_module(
@@ -225,19 +242,22 @@ def cpu_baseline_reference_structured(cfg, varn, seed, budget_s=20.0):
             break
     t_plumb = (time.perf_counter() - t0) / n
 
-    def work(n_tx, n_rx, N, T_d, M):
-        return T_d * float(M) ** n_tx * ((N + 1) * n_tx * n_rx) ** 2
+    def work(n_tx, n_rx, N, T_d, J):
+        return T_d * J * ((N + 1) * n_tx * n_rx) ** 2
 
     n_tx, n_rx, N, T_p, T_d, M, _, _ = cfg
-    t_cfg = t_plumb * work(n_tx, n_rx, N, T_d, M) / work(pn_tx, pn_rx, pN, pT_d, pM)
+    J = hypotheses_per_symbol(mode, n_tx, M, part_r)
+    ratio = work(n_tx, n_rx, N, T_d, J) / work(pn_tx, pn_rx, pN, pT_d, float(pM) ** pn_tx)
+    t_cfg = t_plumb * ratio
     threads = os.environ.get("OMP_NUM_THREADS")
-    return {"value": 1.0 / t_cfg, "unit": "EM-iterations/s", "cores": 1, "kind": "port",
+    return {"value": 1.0 / t_cfg, "unit": "EM-iterations/s", "cores": host_threads(),
+            "kind": "port",
             "sample": (f"oracle/em_loop.py (reference loop structure, float64) at the plumbing "
                        f"shape 2x2 N_RIS=16 T_p=16 T_d=50 4-QAM: {t_plumb:.3f} s per "
-                       f"trial-iteration ({n} timed); extrapolated by T_d J K^2 "
-                       f"({work(n_tx, n_rx, N, T_d, M) / work(pn_tx, pn_rx, pN, pT_d, pM):.3g}x) "
-                       f"to this workload: {t_cfg:.3g} s per trial-iteration; "
-                       f"BLAS threads={threads or 'default'}")}
+                       f"trial-iteration ({n} timed); extrapolated by T_d J K^2 with J = {J:.6g} "
+                       f"hypotheses per symbol ({mode} E-step): {ratio:.3g}x, {t_cfg:.3g} s per "
+                       f"trial-iteration of this workload; NumPy elementwise work single-threaded, "
+                       f"BLAS threads={threads or 'default'} (cores = the BLAS thread cap)")}
 
 
 def rank_envs(n, port, base=None):
@@ -621,9 +641,10 @@ def main(argv=None):
                      f"and the rooflines time whole-batch launches alone" if eng.subs else
                      "one sbce_em call per GPU"),
         "nmse_mean": nmse_mean,
-        "nmse_note": ("the reference estimator's own fixed point: at cfg 1 / 20 dB EM moves the "
-                      "pilot-only theta_0 (NMSE ~0.93) to NMSE ~9 within ~4 iterations (pinned "
-                      "against the oracle's 20-iteration trajectories, tests/golden/cfg1_traj.npz)"
+        "nmse_note": ("at cfg 1 / 20 dB the EM moves the pilot-only theta_0 (NMSE ~0.93) to NMSE "
+                      "~9 within ~4 iterations; the 20-iteration trajectory is pinned to the float64 "
+                      "oracle (tests/golden/cfg1_traj.npz), which is validated against the reference "
+                      "em() itself at this kernel shape for 2 iterations (cfg1_kernel.npz)"
                       if args.config == "cfg1" else None),
         "nonhpd_trials": nonhpd,
         "status_trials": status_bits,
@@ -638,7 +659,7 @@ def main(argv=None):
                                             iters=2 if args.config in ("cfg1", "plumbing") else 1,
                                             mode=mode, part_r=part_r)
         line["cpu_baseline_reference_structured"] = cpu_baseline_reference_structured(
-            cfg, varn, args.seed)
+            cfg, varn, args.seed, mode=mode, part_r=part_r)
     if rank == 0:
         print(json.dumps(line), flush=True)
     ranks.close()

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define SBCE_ABI_VERSION 4
+#define SBCE_ABI_VERSION 5
 
 /* return codes */
 #define SBCE_OK 0
@@ -162,6 +162,12 @@ const char* sbce_strerror(int code);
 /* Device workspace needed by sbce_em / sbce_estep / sbce_mstep for `d` (every solve mode).
  * The size depends on the library version: re-query it after upgrading the library. */
 int sbce_workspace_bytes(const sbce_dims* d, size_t* bytes);
+
+/* Device workspace for `d` with ONE solve mode (SBCE_SOLVE_*): the min-norm Gram matrix
+ * ([B][L][L] complex) and the tiled factorisation's tile inverses are only carved when that solve
+ * needs them, so a SBCE_SOLVE_CHOL workspace at L <= 512 is about half the size.  sbce_em /
+ * sbce_mstep accept any workspace at least this large for their solve_mode (ABI 5). */
+int sbce_workspace_bytes_solve(const sbce_dims* d, int solve_mode, size_t* bytes);
 
 /* Full EM: `iters` iterations of E-step + M-step on every trial of the batch.
  * Replaces em() at Proposed_method_NMSEvsTp.py:50-83 (estep_mode SOFT) and the

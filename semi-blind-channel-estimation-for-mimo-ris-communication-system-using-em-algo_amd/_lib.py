@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsbce.so")
 
-SBCE_ABI_VERSION = 4
+SBCE_ABI_VERSION = 5
 SBCE_ESTEP_SOFT = 0
 SBCE_ESTEP_HARD = 1
 SBCE_ESTEP_PM = 2
@@ -28,7 +28,8 @@ SBCE_STATUS_DETECTOR = 4
 SBCE_STATUS_DEBUG = 8
 SBCE_STATUS_RANK = 16
 
-EXPORTED = ("sbce_abi_version", "sbce_strerror", "sbce_workspace_bytes", "sbce_em",
+EXPORTED = ("sbce_abi_version", "sbce_strerror", "sbce_workspace_bytes",
+            "sbce_workspace_bytes_solve", "sbce_em",
             "sbce_estep", "sbce_mstep", "sbce_ser", "sbce_gauss_expand", "sbce_nmse")
 
 
@@ -75,6 +76,9 @@ def load(path=None):
     lib.sbce_strerror.argtypes = [ctypes.c_int]
     lib.sbce_workspace_bytes.restype = ctypes.c_int
     lib.sbce_workspace_bytes.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(ctypes.c_size_t)]
+    lib.sbce_workspace_bytes_solve.restype = ctypes.c_int
+    lib.sbce_workspace_bytes_solve.argtypes = [ctypes.POINTER(Dims), ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_size_t)]
     lib.sbce_em.restype = ctypes.c_int
     lib.sbce_em.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(Ptrs), ctypes.c_int,
                             ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
@@ -134,7 +138,14 @@ def check(rc, what):
         raise SbceError(f"{what} failed: {msg} ({rc})")
 
 
-def workspace_bytes(dims):
+def workspace_bytes(dims, solve=None):
+    """Workspace of sbce_em / sbce_mstep for `dims`: for every solve mode (solve=None) or for
+    one SBCE_SOLVE_* mode (sbce_workspace_bytes_solve)."""
     n = ctypes.c_size_t(0)
-    check(load().sbce_workspace_bytes(ctypes.byref(dims), ctypes.byref(n)), "sbce_workspace_bytes")
+    if solve is None:
+        check(load().sbce_workspace_bytes(ctypes.byref(dims), ctypes.byref(n)),
+              "sbce_workspace_bytes")
+    else:
+        check(load().sbce_workspace_bytes_solve(ctypes.byref(dims), int(solve), ctypes.byref(n)),
+              "sbce_workspace_bytes_solve")
     return n.value

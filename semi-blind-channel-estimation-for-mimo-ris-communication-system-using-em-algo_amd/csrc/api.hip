@@ -71,8 +71,10 @@ size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 struct Carve {
     size_t mom, R, rhs, done, ysh, prep, list, tree, tol, winv, ppsi, pS, pflag, prhs, gram, grhs,
         act, tol2, dvec, total;
-    bool has_prep, has_prhs;
+    bool has_prep, has_prhs, has_winv, has_mn;
 };
+
+constexpr int kAnySolve = -1;            // carve for every solve mode (sbce_workspace_bytes)
 
 bool make_problem(const sbce_dims* d, Problem& pb) {
     if (!d) return false;
@@ -88,7 +90,11 @@ bool make_problem(const sbce_dims* d, Problem& pb) {
     return true;
 }
 
-Carve carve(const Problem& pb) {
+// Workspace layout for `solve` (SBCE_SOLVE_*, or kAnySolve): the regions only the tiled
+// factorisation (L > 512) or the min-norm solve use are appended last and carved only when that
+// solve can run, so a CHOL workspace at L <= 512 holds no Gram matrix.  Offsets of every region
+// that is carved do not depend on `solve`.
+Carve carve(const Problem& pb, int solve = kAnySolve) {
     Carve c;
     const size_t MS = (size_t)pb.NT + (size_t)pb.NT * pb.NT;
     c.mom = 0;
@@ -118,14 +124,21 @@ Carve carve(const Problem& pb) {
     if (c.has_prhs) c.total = align_up(c.prhs + (size_t)pb.B * pb.L * pb.NR * sizeof(cd));
     c.tol = c.total;                         // per-trial pivot threshold
     c.winv = align_up(c.tol + (size_t)pb.B * sizeof(double));
+    c.total = c.winv;
+    c.has_mn = solve == kAnySolve || solve == SBCE_SOLVE_MINNORM;
     // tiled factorisation (L > 512, and the min-norm solve at every L): diagonal-tile inverse
-    c.gram = align_up(c.winv + (size_t)pb.B * 64 * 64 * sizeof(cd));
-    // min-norm solve (minnorm.hip): Gram matrix C = G^H G, its right-hand sides, extents
-    c.grhs = align_up(c.gram + (size_t)pb.B * pb.L * pb.L * sizeof(cd));
-    c.act = align_up(c.grhs + (size_t)pb.B * pb.L * pb.NR * sizeof(cd));
-    c.tol2 = align_up(c.act + (size_t)pb.B * sizeof(int32_t));
-    c.dvec = align_up(c.tol2 + (size_t)pb.B * sizeof(double));
-    c.total = align_up(c.dvec + (size_t)pb.B * pb.L * sizeof(double));
+    c.has_winv = c.has_mn || pb.L > kLargeL;
+    c.gram = c.winv;
+    if (c.has_winv) c.total = c.gram = align_up(c.winv + (size_t)pb.B * 64 * 64 * sizeof(cd));
+    c.grhs = c.act = c.tol2 = c.dvec = c.total;
+    if (c.has_mn) {
+        // min-norm solve (minnorm.hip): Gram matrix C = G^H G, its right-hand sides, extents
+        c.grhs = align_up(c.gram + (size_t)pb.B * pb.L * pb.L * sizeof(cd));
+        c.act = align_up(c.grhs + (size_t)pb.B * pb.L * pb.NR * sizeof(cd));
+        c.tol2 = align_up(c.act + (size_t)pb.B * sizeof(int32_t));
+        c.dvec = align_up(c.tol2 + (size_t)pb.B * sizeof(double));
+        c.total = align_up(c.dvec + (size_t)pb.B * pb.L * sizeof(double));
+    }
     return c;
 }
 
@@ -133,17 +146,17 @@ int hip_rc(hipError_t e) { return e == hipSuccess ? SBCE_OK : SBCE_EHIP; }
 
 void set_large(MstepArgs& ma, char* ws, const Carve& c) {
     ma.tol = (double*)(ws + c.tol);
-    ma.winv = (cd*)(ws + c.winv);
+    ma.winv = c.has_winv ? (cd*)(ws + c.winv) : nullptr;
     ma.ppsi = (cd*)(ws + c.ppsi);
     ma.pS = (cd*)(ws + c.pS);
     ma.pflag = (int32_t*)(ws + c.pflag);
     ma.prhs = c.has_prhs ? (cd*)(ws + c.prhs) : nullptr;
     ma.gate = nullptr;
-    ma.gram = (cd*)(ws + c.gram);
-    ma.grhs = (cd*)(ws + c.grhs);
-    ma.act = (int32_t*)(ws + c.act);
-    ma.tol2 = (double*)(ws + c.tol2);
-    ma.dvec = (double*)(ws + c.dvec);
+    ma.gram = c.has_mn ? (cd*)(ws + c.gram) : nullptr;
+    ma.grhs = c.has_mn ? (cd*)(ws + c.grhs) : nullptr;
+    ma.act = c.has_mn ? (int32_t*)(ws + c.act) : nullptr;
+    ma.tol2 = c.has_mn ? (double*)(ws + c.tol2) : nullptr;
+    ma.dvec = c.has_mn ? (double*)(ws + c.dvec) : nullptr;
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -157,7 +170,7 @@ int status_init(int32_t* status, int B, hipStream_t s) {
                                                                                     : SBCE_EHIP;
 }
 
-int check_ptrs(const sbce_ptrs* p, const Problem& pb, bool need_ws) {
+int check_ptrs(const sbce_ptrs* p, const Problem& pb, bool need_ws, int solve = kAnySolve) {
     if (!p) return SBCE_EINVAL;
     const void* req[] = {p->y_d, p->y_p, p->psi_d, p->u_p, p->cons, p->theta};
     for (const void* q : req)
@@ -165,7 +178,7 @@ int check_ptrs(const sbce_ptrs* p, const Problem& pb, bool need_ws) {
     if (pb.Tp == 0) { /* pilots optional */ }
     if (need_ws) {
         if (!p->workspace || !aligned16(p->workspace)) return SBCE_EINVAL;
-        if (p->workspace_bytes < carve(pb).total) return SBCE_EWORKSPACE;
+        if (p->workspace_bytes < carve(pb, solve).total) return SBCE_EWORKSPACE;
     }
     return SBCE_OK;
 }
@@ -194,16 +207,26 @@ int sbce_workspace_bytes(const sbce_dims* d, size_t* bytes) {
     return SBCE_OK;
 }
 
+int sbce_workspace_bytes_solve(const sbce_dims* d, int solve_mode, size_t* bytes) {
+    Problem pb;
+    if (!bytes || !make_problem(d, pb)) return SBCE_EINVAL;
+    if (solve_mode != SBCE_SOLVE_CHOL && solve_mode != SBCE_SOLVE_CHOL_DROP &&
+        solve_mode != SBCE_SOLVE_MINNORM)
+        return SBCE_EINVAL;
+    *bytes = carve(pb, solve_mode).total;
+    return SBCE_OK;
+}
+
 int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, int solve_mode,
             void* hip_stream) {
     Problem pb;
     if (!make_problem(d, pb) || iters < 0) return SBCE_EINVAL;
     if (!estep_supported(pb, estep_mode) || !chol_supported(pb)) return SBCE_EUNSUPPORTED;
-    int rc = check_ptrs(p, pb, true);
-    if (rc) return rc;
     if (solve_mode != SBCE_SOLVE_CHOL && solve_mode != SBCE_SOLVE_CHOL_DROP &&
         solve_mode != SBCE_SOLVE_MINNORM)
         return SBCE_EINVAL;
+    int rc = check_ptrs(p, pb, true, solve_mode);
+    if (rc) return rc;
     if (p->llf && !p->x_d_true) return SBCE_EINVAL;
     const bool gauss = estep_mode == SBCE_ESTEP_GAUSS;
     if (gauss && !(pb.varx > 0.0)) return SBCE_EINVAL;
@@ -215,7 +238,7 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
         return SBCE_EINVAL;
     if (pb.B == 0 || iters == 0) return SBCE_OK;
     hipStream_t s = (hipStream_t)hip_stream;
-    const Carve c = carve(pb);
+    const Carve c = carve(pb, solve_mode);
     char* ws = (char*)p->workspace;
     int32_t* done = (int32_t*)(ws + c.done);
     if (hipMemsetAsync(done, 0, (size_t)pb.B * sizeof(int32_t), s) != hipSuccess) return SBCE_EHIP;
@@ -294,7 +317,7 @@ int sbce_estep(const sbce_dims* d, const sbce_ptrs* p, int estep_mode, void* mom
     ea.list = nullptr;
     ea.tree = nullptr;
     if (p->workspace && aligned16(p->workspace)) {
-        const Carve c = carve(pb);
+        const Carve c = carve(pb, SBCE_SOLVE_CHOL);      // the E-step regions come first
         if (c.has_prep && p->workspace_bytes >= c.total) {
             ea.prep = (double*)((char*)p->workspace + c.prep);
             ea.list = (int32_t*)((char*)p->workspace + c.list);
@@ -309,15 +332,15 @@ int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int 
     Problem pb;
     if (!make_problem(d, pb)) return SBCE_EINVAL;
     if (!chol_supported(pb)) return SBCE_EUNSUPPORTED;
-    int rc = check_ptrs(p, pb, true);
-    if (rc) return rc;
-    if (!moments) return SBCE_EINVAL;
     if (solve_mode != SBCE_SOLVE_CHOL && solve_mode != SBCE_SOLVE_CHOL_DROP &&
         solve_mode != SBCE_SOLVE_MINNORM)
         return SBCE_EINVAL;
+    int rc = check_ptrs(p, pb, true, solve_mode);
+    if (rc) return rc;
+    if (!moments) return SBCE_EINVAL;
     if (pb.B == 0) return SBCE_OK;
     hipStream_t s = (hipStream_t)hip_stream;
-    const Carve c = carve(pb);
+    const Carve c = carve(pb, solve_mode);
     char* ws = (char*)p->workspace;
     if ((rc = status_init(p->status, pb.B, s))) return rc;
     MstepArgs ma;
@@ -365,12 +388,12 @@ int sbce_debug_mstep_phase(const sbce_dims* d, const sbce_ptrs* p, const void* m
     Problem pb;
     if (!make_problem(d, pb)) return SBCE_EINVAL;
     if (!chol_supported(pb)) return SBCE_EUNSUPPORTED;
-    int rc = check_ptrs(p, pb, true);
+    int rc = check_ptrs(p, pb, true, SBCE_SOLVE_CHOL);
     if (rc) return rc;
     if (!moments || phase < 0 || phase > 2) return SBCE_EINVAL;
     if (pb.B == 0) return SBCE_OK;
     hipStream_t s = (hipStream_t)hip_stream;
-    const Carve c = carve(pb);
+    const Carve c = carve(pb, SBCE_SOLVE_CHOL);
     char* ws = (char*)p->workspace;
     MstepArgs ma;
     ma.yd = (const cd*)p->y_d; ma.yp = (const cd*)p->y_p; ma.psid = (const cd*)p->psi_d;
@@ -388,9 +411,9 @@ int sbce_debug_mstep_phase(const sbce_dims* d, const sbce_ptrs* p, const void* m
 int sbce_debug_minnorm_tol(const sbce_dims* d, const sbce_ptrs* p, double* tol_out, void* hip_stream) {
     Problem pb;
     if (!make_problem(d, pb) || !tol_out) return SBCE_EINVAL;
-    int rc = check_ptrs(p, pb, true);
+    int rc = check_ptrs(p, pb, true, SBCE_SOLVE_CHOL);
     if (rc) return rc;
-    const Carve c = carve(pb);
+    const Carve c = carve(pb, SBCE_SOLVE_CHOL);           // tol precedes the solve regions
     return hip_rc(hipMemcpyAsync(tol_out, (char*)p->workspace + c.tol, (size_t)pb.B * sizeof(double),
                                  hipMemcpyDefault, (hipStream_t)hip_stream));
 }

@@ -17,9 +17,12 @@ typedef double2 cd;
 // P1 = sum ar br, P2 = sum ai bi, P3 = sum (ar + ai)(br - bi) the update has
 //   re = C_re - P1 - P2,   im = C_im - (P3 - P1 + P2);
 // the accumulators X1 = C_re - P1 (cre), X2 = -P2 (c2), X3 = C_im + C_re - P3 (cim, csub_init)
-// give re = X1 + X2, im = X3 - X1 + X2 (csub_out).  Used for the CHOL solve only: the rounding
-// of the imaginary part grows (error ~ eps (|ar| + |ai|)(|br| + |bi|)), which the min-norm and
-// drop solves must not see -- their pivots past the numerical rank are that rounding noise.
+// give re = X1 + X2, im = X3 - X1 + X2 (csub_out).  The rounding of the imaginary part grows
+// (error ~ eps (|ar| + |ai|)(|br| + |bi|)), so G3 is used where no rank decision reads the
+// result: the CHOL solve, and in the min-norm solve AFTER the rank cut (the Gram build C = G^H G,
+// minnorm.hip gram_kernel, and C's own tiled factorisation).  Never for R's factorisation in the
+// drop or min-norm paths: its pivots past the numerical rank ARE the rounding noise, and the
+// pivot decisions must see four-MFMA rounding.
 typedef double mf4 __attribute__((ext_vector_type(4)));
 template <bool G3>
 __device__ __forceinline__ void csub_init(mf4& cre, mf4& cim, mf4& c2) {

@@ -110,7 +110,7 @@ def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_t
     if th.shape != (B, L * n_rx):
         raise ValueError(f"theta0 shape {tuple(th.shape)} != {(B, L * n_rx)}")
     dims = _lib.Dims(B, n_tx, n_rx, P, T_p, T_d, M, int(partition_r), float(varn), float(varx))
-    ws_bytes = _lib.workspace_bytes(dims)
+    ws_bytes = _lib.workspace_bytes(dims, _SOLVES[solve])
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device="cuda")
     status = torch.zeros(B, dtype=torch.int32, device="cuda")
     iters_done = torch.zeros(B, dtype=torch.int32, device="cuda")
@@ -582,10 +582,21 @@ class EMEngine:
             raise ValueError("superimposed pilots (x_sup) need the soft or hard E-step")
         self.dims = _lib.Dims(B, self.n_tx, n_rx, P, T_p, T_d, self.M, int(partition_r), self.varn,
                               float(varx))
-        self.ws = torch.empty(max(_lib.workspace_bytes(self.dims), 16), dtype=torch.uint8,
-                              device="cuda")
-        self.status = torch.zeros(B, dtype=torch.int32, device="cuda")
         self.mode, self.solve = _MODES[mode], _SOLVES[solve]
+        # ONE device buffer: the whole-batch workspace (estep / mstep / mstep_phase) and, when the
+        # batch runs as stream sub-batches, their workspaces as disjoint slices of the same memory
+        # (run() and the whole-batch diagnostics are never in flight together)
+        K = int(streams)
+        sub = K > 1 and B >= 2 * K and T_p and x_sup is None
+        bounds = np.linspace(0, B, K + 1).astype(int) if sub else np.array([0, B])
+        sub_dims = [_lib.Dims(int(b1 - b0), self.n_tx, n_rx, P, T_p, T_d, self.M, int(partition_r),
+                              self.varn, float(varx)) for b0, b1 in zip(bounds[:-1], bounds[1:])]
+        sub_bytes = [(_lib.workspace_bytes(d, self.solve) + 255) // 256 * 256 for d in sub_dims]
+        whole = _lib.workspace_bytes(self.dims, self.solve)
+        self.ws_all = torch.empty(max(whole, sum(sub_bytes) if sub else 0, 16), dtype=torch.uint8,
+                                  device="cuda")
+        self.ws = self.ws_all[:max(whole, 16)]
+        self.status = torch.zeros(B, dtype=torch.int32, device="cuda")
         self.x_d = dev(x_d_true)
         self.mom = torch.zeros((B, T_d, self.n_tx + self.n_tx ** 2), dtype=torch.complex128,
                                device="cuda")
@@ -599,13 +610,11 @@ class EMEngine:
                               self.status.data_ptr(), self.ws.data_ptr(), self.ws.numel(), None,
                               self.x_sup.data_ptr() if self.x_sup is not None else None)
         self.subs = []
-        K = int(streams)
-        if K > 1 and B >= 2 * K and T_p and self.x_sup is None:
-            bounds = np.linspace(0, B, K + 1).astype(int)
-            for b0, b1 in zip(bounds[:-1], bounds[1:]):
-                dims = _lib.Dims(int(b1 - b0), self.n_tx, n_rx, P, T_p, T_d, self.M, int(partition_r),
-                                 self.varn, float(varx))
-                ws = torch.empty(max(_lib.workspace_bytes(dims), 16), dtype=torch.uint8, device="cuda")
+        if sub:
+            off = 0
+            for (b0, b1), dims, nb in zip(zip(bounds[:-1], bounds[1:]), sub_dims, sub_bytes):
+                ws = self.ws_all[off:off + nb]
+                off += nb
                 ptrs = _lib.Ptrs(self.y_d[b0:b1].data_ptr(), self.y_p[b0:b1].data_ptr(),
                                  self.psi_d[b0:b1].data_ptr(), self.u_p[b0:b1].data_ptr(),
                                  self.cons.data_ptr(), self.theta[b0:b1].data_ptr(), None, None, None,

@@ -101,6 +101,20 @@ def test_workspace_and_validation_without_gpu(sbce):
               + 1000 * 4 + 1000 * 8                       # min-norm: extents, C's threshold
               + 1000 * Lw * 8)                            # min-norm: Schur-complement diagonal
     assert expect <= n <= expect + 14 * 256 + 4000
+    # one solve mode (ABI 5): CHOL at L <= 512 carves neither the tile inverses nor the min-norm
+    # regions; the min-norm solve needs all of them (= the any-mode size)
+    chol = L.workspace_bytes(d, L.SBCE_SOLVE_CHOL)
+    assert L.workspace_bytes(d, L.SBCE_SOLVE_CHOL_DROP) == chol
+    assert L.workspace_bytes(d, L.SBCE_SOLVE_MINNORM) == n
+    mn_only = (1000 * 64 * 64 * 16 + 1000 * Lw * Lw * 16 + 1000 * Lw * 4 * 16 + 1000 * 4
+               + 1000 * 8 + 1000 * Lw * 8)
+    assert 0 <= n - chol - mn_only <= 6 * 256
+    # L > 512 (tiled factorisation): CHOL keeps the tile inverses
+    big = L.Dims(4, 8, 8, 257, 32, 64, 16, 1, 0.1)
+    nbig, cbig = L.workspace_bytes(big), L.workspace_bytes(big, L.SBCE_SOLVE_CHOL)
+    Lb = 257 * 8
+    assert 0 <= nbig - cbig - (4 * Lb * Lb * 16 + 4 * Lb * 8 * 16 + 4 * 4 + 4 * 8 + 4 * Lb * 8) <= 5 * 256
+    assert lib.sbce_workspace_bytes_solve(ctypes.byref(d), 7, ctypes.byref(ctypes.c_size_t())) == -1
     bad = L.Dims(1, 9, 4, 65, 16, 256, 16, 0, 0.1)     # n_tx > 8
     nb = ctypes.c_size_t(0)
     assert lib.sbce_workspace_bytes(ctypes.byref(bad), ctypes.byref(nb)) == -1
@@ -109,6 +123,9 @@ def test_workspace_and_validation_without_gpu(sbce):
     # null pointers are rejected before any HIP call
     p = L.Ptrs()
     assert lib.sbce_em(ctypes.byref(d), ctypes.byref(p), 1, 0, 0, None) == -1
+    # a CHOL-sized workspace is too small for the min-norm solve (before any HIP call)
+    p = L.Ptrs(*([256] * 11), 256, chol)
+    assert lib.sbce_em(ctypes.byref(d), ctypes.byref(p), 1, 0, L.SBCE_SOLVE_MINNORM, None) == -4
 
 
 def test_product_path_fails_loudly_without_gpu(sbce):

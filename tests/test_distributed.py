@@ -187,3 +187,14 @@ def test_bench_mismatched_launch_fails():
     r, lines = _run_bench(["--gpus", "4", "--selftest"], {"WORLD_SIZE": "2", "RANK": "0"})
     assert r.returncode == 2 and not lines
     assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_bench_reference_structured_work_model_follows_estep():
+    """The reference-structured CPU baseline extrapolates by T_d J K^2 with J = the hypotheses the
+    workload's E-step visits: M^n_tx (exact / log-max), the PM list M^(p+1) (PMd/PM.py:74-92)."""
+    b = _bench()
+    assert b.hypotheses_per_symbol("soft", 4, 16) == 16 ** 4
+    assert b.hypotheses_per_symbol("hard", 2, 4) == 16
+    assert b.hypotheses_per_symbol("pm_soft", 8, 16, 1) == 16        # cfg2: p = int(1/4) = 0
+    assert b.hypotheses_per_symbol("pm", 4, 4, 2) == 16              # p = int(2/2) = 1
+    assert b.host_threads() >= 1
