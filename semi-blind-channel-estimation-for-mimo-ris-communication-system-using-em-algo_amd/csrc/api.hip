@@ -40,7 +40,7 @@ void read_debug_env(DebugConfig& c) {
     if ((v = env("SBCE_RB_TC"))) c.rb_tc32 = v[0] == '3';
     if ((v = env("SBCE_UPD_WAVES"))) c.upd_waves8 = v[0] == '8';
     if ((v = env("SBCE_BACKSUB"))) c.backsub = (v[0] >= '1' && v[0] <= '3') ? v[0] - '0' : 0;
-    if ((v = env("SBCE_CHOL_IMPL"))) c.chol_impl = (v[0] == 'v' || v[0] == 'f' || v[0] == 'u' || v[0] == 'l') ? v[0] : 0;
+    if ((v = env("SBCE_CHOL_IMPL"))) c.chol_impl = (v[0] == 'v' || v[0] == 'f' || v[0] == 'u' || v[0] == 'l' || v[0] == 'w') ? v[0] : 0;
     if ((v = env("SBCE_ESTEP_PAIR"))) c.estep_nopair = v[0] == '0';
     if ((v = env("SBCE_CPLX3"))) c.cplx3 = v[0] != '0';
 }
@@ -144,6 +144,12 @@ Carve carve(const Problem& pb, int solve = kAnySolve) {
 
 int hip_rc(hipError_t e) { return e == hipSuccess ? SBCE_OK : SBCE_EHIP; }
 
+// The launchers check their kernels with hipGetLastError(), which reports the last error of ANY
+// HIP call on this host thread until it is read.  A caller's earlier failed or "not ready" call
+// (e.g. an event query by the framework that owns the buffers) must not be reported as a failure
+// of this library's launches: every entry point that launches clears it first.
+void clear_stale_error() { (void)hipGetLastError(); }
+
 void set_large(MstepArgs& ma, char* ws, const Carve& c) {
     ma.tol = (double*)(ws + c.tol);
     ma.winv = c.has_winv ? (cd*)(ws + c.winv) : nullptr;
@@ -219,6 +225,7 @@ int sbce_workspace_bytes_solve(const sbce_dims* d, int solve_mode, size_t* bytes
 
 int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, int solve_mode,
             void* hip_stream) {
+    clear_stale_error();
     Problem pb;
     if (!make_problem(d, pb) || iters < 0) return SBCE_EINVAL;
     if (!estep_supported(pb, estep_mode) || !chol_supported(pb)) return SBCE_EUNSUPPORTED;
@@ -300,6 +307,7 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
 
 int sbce_estep(const sbce_dims* d, const sbce_ptrs* p, int estep_mode, void* moments,
                void* hip_stream) {
+    clear_stale_error();
     Problem pb;
     if (!make_problem(d, pb)) return SBCE_EINVAL;
     int rc = check_ptrs(p, pb, false);
@@ -329,6 +337,7 @@ int sbce_estep(const sbce_dims* d, const sbce_ptrs* p, int estep_mode, void* mom
 
 int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int solve_mode,
                void* r_out, void* rhs_out, void* hip_stream) {
+    clear_stale_error();
     Problem pb;
     if (!make_problem(d, pb)) return SBCE_EINVAL;
     if (!chol_supported(pb)) return SBCE_EUNSUPPORTED;
@@ -385,6 +394,7 @@ int sbce_debug_chol_skip(int mask) {
 // 8 -- phase 0 must have run -- else the VALU build with B^H), 2 = the whole build (R and B^H).
 int sbce_debug_mstep_phase(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int phase,
                            void* hip_stream) {
+    clear_stale_error();
     Problem pb;
     if (!make_problem(d, pb)) return SBCE_EINVAL;
     if (!chol_supported(pb)) return SBCE_EUNSUPPORTED;
@@ -450,6 +460,7 @@ int sbce_debug_estep_pair(unsigned long long* out, int reset) {
 
 int sbce_ser(const sbce_dims* d, const void* x_dest, const void* x_d_true, double* ser_out,
              void* hip_stream) {
+    clear_stale_error();
     Problem pb;
     if (!make_problem(d, pb) || !x_dest || !x_d_true || !ser_out) return SBCE_EINVAL;
     if (pb.B == 0) return SBCE_OK;
@@ -458,6 +469,7 @@ int sbce_ser(const sbce_dims* d, const void* x_dest, const void* x_d_true, doubl
 }
 
 int sbce_gauss_expand(const sbce_dims* d, const void* theta, void* h_out, void* hip_stream) {
+    clear_stale_error();
     Problem pb;
     if (!make_problem(d, pb) || !theta || !h_out || !aligned16(theta) || !aligned16(h_out))
         return SBCE_EINVAL;
@@ -467,6 +479,7 @@ int sbce_gauss_expand(const sbce_dims* d, const void* theta, void* h_out, void* 
 
 int sbce_nmse(const sbce_dims* d, const void* theta, const void* h_true, double* nmse_out,
               void* hip_stream) {
+    clear_stale_error();
     Problem pb;
     if (!make_problem(d, pb) || !theta || !h_true || !nmse_out) return SBCE_EINVAL;
     if (pb.B == 0) return SBCE_OK;

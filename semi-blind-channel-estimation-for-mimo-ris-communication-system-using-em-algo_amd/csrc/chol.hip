@@ -823,6 +823,26 @@ __global__ __launch_bounds__(64 * NWU) void panel_update_kernel(MstepArgs a, int
     panel_update_body<NWU, G3>(a, L, jb, jb, ntile, b, grp, skip, Bp);
 }
 
+// panel_update2_kernel (wide left-looking step): the updates of panels j AND j+1 by the columns
+// [0, jb) in one launch -- for every trial gpt0 four-tile groups of panel j's rows and gpt1 of
+// panel j+1's (rows from jb + 32, k < jb; the rank-32 remainder by panel j is the next factor
+// launch's pre-update).  A trial's blocks are adjacent on one XCD, so the two column halves read
+// each row segment of L[:, 0:jb] at about the same time: the second read is an L2 hit, and the
+// left-looking re-reads from HBM halve (a 64-column panel's traffic with the 32-column panels'
+// registers, occupancy and factor chain).
+template <bool G3 = false>
+__global__ __launch_bounds__(256) void panel_update2_kernel(MstepArgs a, int L, int jb, int ntile,
+                                                            int gpt0, int gpt1, int skip) {
+    __shared__ __attribute__((aligned(16))) cd Bp[PW * (KBU + 1)];
+    const int gpt = gpt0 + gpt1;
+    const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
+    const int b = (slot / gpt) * 8 + xcd, g = slot - (slot / gpt) * gpt;
+    if (b >= a.nbatch) return;
+    if (a.done && a.done[b]) return;
+    if (g < gpt0) panel_update_body<4, G3>(a, L, jb, jb, ntile, b, g, skip, Bp);
+    else panel_update_body<4, G3>(a, L, jb + PW, jb, ntile - 2, b, g - gpt0, skip, Bp);
+}
+
 // 16 x 16 tile of R (rows row0.., columns c0.., w valid columns) into per-lane registers:
 // lane holds entries e = lane + 64 h, row e >> 4, column e & 15
 __device__ __forceinline__ void load_tile16(const cd* R, int L, int row0, int c0, int w, int lane,
@@ -918,6 +938,8 @@ __device__ __forceinline__ void load_ycomp(const cd* y, int L, int NR, int row0,
 // LDS of the factor body (cd entries): Xs (4 waves' 16 x 16 scratch), DiA, DiB, XA1, ybA, ybB
 constexpr int kFacXs = 0, kFacDiA = 4 * NB * NB, kFacDiB = kFacDiA + NB * NB, kFacXA1 = kFacDiB + NB * NB,
               kFacYbA = kFacXA1 + NB * NB, kFacYbB = kFacYbA + NB * 8, kFacLds = kFacYbB + NB * 8;
+__device__ __forceinline__ void panel_preupdate(const MstepArgs& a, int L, int jb, int ntile, int b,
+                                                cd* Lp);
 template <bool G3 = false>
 __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int NR, int jb, int ntile,
                                                   int b, int skip, cd* sm, double* dinv, int& flag) {
@@ -1079,7 +1101,9 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
     if (tid == 0 && st && a.status) atomicOr(&a.status[b], st);
 }
 
-template <bool G3 = false>
+// PRE (wide schedule, odd panels): first the rank-32 update of the panel by the previous panel's
+// columns [jb-32, jb) (panel_preupdate: the part panel_update2_kernel left), then the factor.
+template <bool G3 = false, bool PRE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip) {
     __shared__ __attribute__((aligned(16))) cd sm[kFacLds];
@@ -1087,6 +1111,7 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
     __shared__ int flag;
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
+    if (PRE && !(skip & 1)) panel_preupdate(a, L, jb, ntile, b, sm);
     panel_factor_body<G3>(a, L, NR, jb, ntile, b, skip, sm, dinv, flag);
 }
 
@@ -1672,7 +1697,40 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
     }
-    for (int j = 0; j < npan && !lookahead; ++j) {
+    const bool wide = g_debug.chol_impl == 'w';
+    for (int j = 0; j < npan && wide; ++j) {
+        // wide schedule: even panels j >= 2 update panels j and j+1 by [0, jb) in one launch; odd
+        // panels are pre-updated by panel j-1 inside their factor launch
+        const int jb = j * PW;
+        const int rem = (pb.L - jb + NB - 1) / NB;
+        const bool g3 = g_debug.cplx3 && a.solve_mode == SBCE_SOLVE_CHOL;
+        if (j >= 2 && !(j & 1)) {
+            const int gpt0 = (rem + 3) / 4;
+            const int gpt1 = j + 1 < npan ? (rem - 2 + 3) / 4 : 0;
+            const long nblk = 8L * ((pb.B + 7) / 8) * (gpt0 + gpt1);
+            if (g3)
+                hipLaunchKernelGGL(panel_update2_kernel<true>, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L,
+                                   jb, rem, gpt0, gpt1, skip);
+            else
+                hipLaunchKernelGGL(panel_update2_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L,
+                                   jb, rem, gpt0, gpt1, skip);
+        }
+        const bool pre = (j & 1) != 0;
+        if (g3 && pre)
+            hipLaunchKernelGGL((panel_factor_kernel<true, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR,
+                               jb, rem, skip);
+        else if (g3)
+            hipLaunchKernelGGL((panel_factor_kernel<true, false>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
+                               pb.NR, jb, rem, skip);
+        else if (pre)
+            hipLaunchKernelGGL((panel_factor_kernel<false, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
+                               pb.NR, jb, rem, skip);
+        else
+            hipLaunchKernelGGL((panel_factor_kernel<false, false>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
+                               pb.NR, jb, rem, skip);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    for (int j = 0; j < npan && !lookahead && !wide; ++j) {
         const int jb = j * PW;
         const int rem = (pb.L - jb + NB - 1) / NB;               // 16-row tiles from jb
         // SBCE_CHOL_IMPL=u (A/B runs): update and factor of a panel of at most 16 row tiles in

@@ -164,3 +164,62 @@ def test_minnorm_cfg4_full_size(sbce):
     err = rel(th[0], th0)
     assert err < 1e-4, err
     assert abs(nmse(th[0], b["h"][0]) / nmse(th0, b["h"][0]) - 1) < 1e-3
+
+
+@pytest.mark.parametrize("decades", [3, 6, 9])
+def test_minnorm_graded_spectrum_vs_lstsq(sbce, decades):
+    """A rank-deficient R whose KEPT eigenvalues are graded over `decades` decades (cond_kept
+    10^decades, well above lstsq's cut): R = sum_p u_p u_p^H with u_p the rows of
+    diag(sqrt(lambda)) Q^H (pilots only; the moments are zero), so the minimum-norm solution's
+    conditioning is cond_kept.  theta vs numpy lstsq at max(1e-10, 1e-14 cond_kept)."""
+    rng = np.random.default_rng(decades)
+    n_tx, n_rx, N, T_p, T_d = 2, 2, 32, 40, 4
+    L = (N + 1) * n_tx
+    b = sbce.signal_model.synthetic_batch(2, n_tx, n_rx, N, T_p, T_d, 16, 0.05, seed=31)
+    Q, _ = np.linalg.qr(rng.standard_normal((L, L)) + 1j * rng.standard_normal((L, L)))
+    lam = np.logspace(0, -decades, T_p)
+    U = np.sqrt(lam)[:, None] * np.conj(Q[:, :T_p]).T             # (T_p, L)
+    u_p = np.stack([U, U])
+    zeros_m = np.zeros((2, T_d, n_tx), complex)
+    zeros_S = np.zeros((2, T_d, n_tx, n_tx), complex)
+    th, R, rhs, st = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], u_p, b["cons"], zeros_m,
+                                      zeros_S, 0.05, solve="lstsq")
+    for i in range(2):
+        R0 = U.T @ np.conj(U)                                     # sum_p u_p u_p^H (u_p rows)
+        assert rel(R[i], R0) < 1e-12
+        th0, rank = mstep_lstsq(R[i], rhs[i])
+        cond, rank2 = _cond_kept(R[i], L * n_rx)
+        assert rank == rank2 == T_p
+        err = rel(th[i], th0)
+        assert err < max(1e-10, 1e-14 * cond) or st[i] & sbce._lib.SBCE_STATUS_RANK, (err, cond)
+
+
+def test_minnorm_cfg2_rank_flagged_trials_vs_lstsq(sbce):
+    """The trials the min-norm solve flags SBCE_STATUS_RANK at full BASELINE cfg 2 size (8x8,
+    N_RIS = 256, L = 2056, PM_beta r = 1 E-step, 20 dB): trials 28 and 50 of the seed-0 64-trial
+    batch at their third M-step (tools/rank_study.py: 2 of 64 flagged after 2 iterations, none
+    after 3 or 4).  Each has ONE eigenvalue of R between the cut and the clean gap (311x / 648x
+    eps K lambda_max) that lstsq keeps (rank 1057 instead of 1056): the kept conditioning rises to
+    ~1e9 and theta agrees with numpy lstsq to 6.1e-5 / 1.1e-5 relative (the min-norm formula
+    G (G^H G)^-2 G^H b squares that conditioning), the NMSE to 9.9e-8 / 4.9e-9 relative -- four
+    orders inside the north-star bar (1e-3)."""
+    n_tx, n_rx, N, T_p, T_d = 8, 8, 256, 32, 1024
+    varn = float(sbce.signal_model.snr_to_varn(20.0))
+    b = sbce.signal_model.synthetic_batch(64, n_tx, n_rx, N, T_p, T_d, 16, varn, seed=0)
+    sel = [28, 50]
+    sub = {k: np.ascontiguousarray(b[k][sel]) for k in ("y_d", "y_p", "psi_d", "u_p", "theta0", "h")}
+    del b
+    r = sbce.em_batch(sub["y_d"], sub["y_p"], sub["psi_d"], sub["u_p"], sbce.qam.qam_constellation(16),
+                      varn, 2, sub["theta0"], mode="pm_soft", partition_r=1, solve="lstsq")
+    cons = sbce.qam.qam_constellation(16)
+    m, S = sbce.estep_batch(sub["y_d"], sub["psi_d"], cons, r["theta"], varn, n_tx, "pm_soft",
+                            partition_r=1)
+    th, R, rhs, st = sbce.mstep_batch(sub["y_d"], sub["y_p"], sub["psi_d"], sub["u_p"], cons, m, S,
+                                      varn, solve="lstsq")
+    for i in range(2):
+        assert st[i] & sbce._lib.SBCE_STATUS_RANK, st[i]
+        th0, rank = mstep_lstsq(R[i], rhs[i])
+        assert rank == T_p + T_d + 1
+        nm, nm0 = nmse(th[i], sub["h"][i]), nmse(th0, sub["h"][i])
+        assert abs(nm / nm0 - 1) < 1e-6, (nm, nm0)                # measured <= 1e-7
+        assert rel(th[i], th0) < 1e-3, rel(th[i], th0)           # measured <= 6.1e-5
