@@ -84,6 +84,24 @@ MSTEP_KERNELS_LARGE = ["pilot_factor_kernel", "pilot_rhs_kernel", "rbuild_herm_k
 # launched exactly once per M-step (the divisor of the phase's PMC totals; the pilot
 # factorisation runs once per EM run, so its bytes are spread over the run's M-steps)
 MSTEP_ANCHORS = ["rhs_dma_kernel", "rhs_lds_kernel", "rhs_kernel"]
+# the L <= 512 Cholesky solve's launches (csrc/chol.hip; diag_tol_kernel runs once per M-step)
+CHOL_KERNELS = ["diag_tol_kernel", "panel_update_kernel", "panel_update2_kernel", "panel_factor_kernel",
+                "backsub4_kernel", "backsub3_kernel", "backsub2_kernel", "backsub_kernel"]
+CHOL_ANCHORS = ["diag_tol_kernel"]
+
+
+def chol_flops_per_trial(L, n_rx, g3=True):
+    """Cholesky of the L x L Hermitian R plus the forward / back substitutions with n_rx
+    right-hand sides, as executed: (4/3) L^3 real flops of complex MACs (8 flops each), of which
+    the MFMA tile products run as three real MFMAs per complex product instead of four (G3: 3/4),
+    and 8 n_rx L^2 for the two triangular solves."""
+    return (4.0 / 3.0) * L ** 3 * (0.75 if g3 else 1.0) + 8.0 * n_rx * L * L
+
+
+def chol_bytes_per_trial(L, n_rx):
+    """Minimal HBM bytes of the solve: R's lower triangle read once and the factor written once
+    (16 B complex each), read once more by the back substitution, B^H read, theta written."""
+    return 16.0 * (3 * L * (L + 1) / 2 + 2 * L * n_rx)
 
 
 def rbuild_flops_per_trial_iter(n_tx, N, T_p, T_d):
@@ -546,6 +564,16 @@ def main(argv=None):
         torch.cuda.synchronize()
         rb_ms = e0.elapsed_time(e1) / args.kernel_reps
 
+    # ---- the Cholesky solve alone: whole M-step minus its build (R and B^H, phase 2) ----
+    build_ms = None
+    if n_tx * (N + 1) <= 512 and solve == "chol":
+        e0.record(stream)
+        for _ in range(args.kernel_reps):
+            eng.mstep_phase(2)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        build_ms = e0.elapsed_time(e1) / args.kernel_reps
+
     P = N + 1
     pmc = load_pmc_traffic(args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}_latest.json"))
     pmc_ok = bool(pmc and pmc.get("config") == args.config and pmc.get("trials") == B)
@@ -592,6 +620,23 @@ def main(argv=None):
                    "traffic_ratio": r_traffic / rbytes if r_traffic else None,
                    "measured_pipe_tflops": FP64_MFMA_MEASURED_TFLOPS,
                    "frac_of_measured_pipe": r_ach / FP64_MFMA_MEASURED_TFLOPS}
+    chol_roof = None
+    if build_ms is not None:
+        L_ = n_tx * P
+        c_ms = mstep_ms - build_ms
+        cflops = chol_flops_per_trial(L_, n_rx) * B
+        cbytes = chol_bytes_per_trial(L_, n_rx) * B
+        c_traffic = traffic_of(CHOL_KERNELS, CHOL_ANCHORS)
+        c_ach = cflops / (c_ms * 1e-3) / 1e12
+        chol_roof = {"bound": "mfma", "phase": "Cholesky solve (batched panels + back substitution)",
+                     "kernels": CHOL_KERNELS, "ms": c_ms, "how": "M-step minus its R / B^H build, "
+                     "both timed with HIP events on the launch stream",
+                     "achieved": c_ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": c_ach / FP64_PEAK_TFLOPS, "flops_per_launch": cflops,
+                     "traffic": c_traffic, "algorithmic_bytes": cbytes,
+                     "traffic_ratio": c_traffic / cbytes if c_traffic else None,
+                     "hbm_GBps_traffic": c_traffic / (c_ms * 1e-3) / 1e9 if c_traffic else None,
+                     "frac_of_measured_pipe": c_ach / FP64_MFMA_MEASURED_TFLOPS}
     if mode in ("soft", "hard"):
         flops = estep_flops_per_trial_iter(n_tx, n_rx, T_d, M) * B
         algo_bytes = estep_bytes_per_trial_iter(n_tx, n_rx, P, T_d) * B
@@ -652,6 +697,7 @@ def main(argv=None):
         "roofline": roofline,
         "rbuild_roofline": rb_roof,
         "mstep_roofline": mstep_roof,
+        "chol_roofline": chol_roof,
         "estep_roofline": estep_roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
