@@ -70,7 +70,7 @@ size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 struct Carve {
     size_t mom, R, rhs, done, ysh, prep, list, tree, tol, winv, ppsi, pS, pflag, prhs, gram, grhs,
-        act, tol2, dvec, total;
+        act, tol2, dvec, mnr, mnskip, total;
     bool has_prep, has_prhs, has_winv, has_mn;
 };
 
@@ -130,14 +130,17 @@ Carve carve(const Problem& pb, int solve = kAnySolve) {
     c.has_winv = c.has_mn || pb.L > kLargeL;
     c.gram = c.winv;
     if (c.has_winv) c.total = c.gram = align_up(c.winv + (size_t)pb.B * 64 * 64 * sizeof(cd));
-    c.grhs = c.act = c.tol2 = c.dvec = c.total;
+    c.grhs = c.act = c.tol2 = c.dvec = c.mnr = c.mnskip = c.total;
     if (c.has_mn) {
         // min-norm solve (minnorm.hip): Gram matrix C = G^H G, its right-hand sides, extents
         c.grhs = align_up(c.gram + (size_t)pb.B * pb.L * pb.L * sizeof(cd));
         c.act = align_up(c.grhs + (size_t)pb.B * pb.L * pb.NR * sizeof(cd));
         c.tol2 = align_up(c.act + (size_t)pb.B * sizeof(int32_t));
         c.dvec = align_up(c.tol2 + (size_t)pb.B * sizeof(double));
-        c.total = align_up(c.dvec + (size_t)pb.B * pb.L * sizeof(double));
+        // one refinement step on the kept subspace: residual and per-trial gate
+        c.mnr = align_up(c.dvec + (size_t)pb.B * pb.L * sizeof(double));
+        c.mnskip = align_up(c.mnr + (size_t)pb.B * pb.L * pb.NR * sizeof(cd));
+        c.total = align_up(c.mnskip + (size_t)pb.B * sizeof(int32_t));
     }
     return c;
 }
@@ -163,6 +166,8 @@ void set_large(MstepArgs& ma, char* ws, const Carve& c) {
     ma.act = c.has_mn ? (int32_t*)(ws + c.act) : nullptr;
     ma.tol2 = c.has_mn ? (double*)(ws + c.tol2) : nullptr;
     ma.dvec = c.has_mn ? (double*)(ws + c.dvec) : nullptr;
+    ma.mnr = c.has_mn ? (cd*)(ws + c.mnr) : nullptr;
+    ma.mnskip = c.has_mn ? (int32_t*)(ws + c.mnskip) : nullptr;
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }

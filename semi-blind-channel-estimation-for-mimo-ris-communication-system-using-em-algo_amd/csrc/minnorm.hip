@@ -352,12 +352,13 @@ __global__ __launch_bounds__(256) void gram_tol_kernel(MstepArgs a, int L) {
 // Block (column block J, trial): thread (column c, row phase q) sums conj(G[i][c]) b[i] over
 // rows i = J*64 + q (mod 4) (each row read by 64 lanes: one coalesced 1 KB segment); the four
 // phases are combined in a fixed order.  Rows past the active extent are written as 0.
-__global__ __launch_bounds__(256) void ghb_kernel(MstepArgs a, int L, int NR) {
+// b = bin ([B][L][NR]), or conj(bin) with cin (the refinement's G^H x0, x0 = conj(theta)).
+__global__ __launch_bounds__(256) void ghb_kernel(MstepArgs a, int L, int NR, const cd* bin, int cin) {
     const int J = blockIdx.x, b = blockIdx.y;
     if (a.done && a.done[b]) return;
     __shared__ cd part[4][TB][8];
     const cd* G = a.R + (size_t)b * L * L;
-    const cd* bv = a.rhs + (size_t)b * L * NR;
+    const cd* bv = bin + (size_t)b * L * NR;
     cd* out = a.grhs + (size_t)b * L * NR;
     const int tid = threadIdx.x, c = tid & 63, q = tid >> 6;
     const int col = J * TB + c;
@@ -370,7 +371,10 @@ __global__ __launch_bounds__(256) void ghb_kernel(MstepArgs a, int L, int NR) {
             const cd g = (col < act && i >= col) ? G[(size_t)i * L + col] : czero();
 #pragma unroll
             for (int r = 0; r < 8; ++r)
-                if (r < NR) acc[r] = cfmac(acc[r], bv[(size_t)i * NR + r], g);
+                if (r < NR) {
+                    const cd v = bv[(size_t)i * NR + r];
+                    acc[r] = cfmac(acc[r], cin ? cconj(v) : v, g);
+                }
         }
     }
 #pragma unroll
@@ -478,7 +482,10 @@ __global__ __launch_bounds__(256) void fwdupd_kernel(MstepArgs a, int L, int NR,
 // ---------------------------------------------------------------- x = G z, theta = conj(x)
 // Block (row block I, trial): tiles G_IJ (J <= I, columns below the active extent) staged in
 // LDS by coalesced row segments, z_J beside them; thread per (row, right-hand side).
-__global__ __launch_bounds__(256) void gz_kernel(MstepArgs a, int L, int NR) {
+// mode 0: out = conj(G z) (theta);  1: out = bref - G z (the refinement residual);
+// 2: out += conj(G z) (theta_1 = conj(x0 + dx)).
+__global__ __launch_bounds__(256) void gz_kernel(MstepArgs a, int L, int NR, int mode, cd* out,
+                                                 const cd* bref) {
     const int I = blockIdx.x, b = blockIdx.y;
     if (a.done && a.done[b]) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -486,7 +493,7 @@ __global__ __launch_bounds__(256) void gz_kernel(MstepArgs a, int L, int NR) {
     cd* zs = reinterpret_cast<cd*>(smem + (size_t)TB * (TB + 1) * sizeof(cd));
     const cd* G = a.R + (size_t)b * L * L;
     const cd* z = a.grhs + (size_t)b * L * NR;
-    cd* th = a.theta + (size_t)b * L * NR;
+    cd* th = out + (size_t)b * L * NR;
     const int act = a.act[b];
     const int tid = threadIdx.x, i0 = I * TB;
     const int h = (L - i0) < TB ? (L - i0) : TB;
@@ -516,8 +523,41 @@ __global__ __launch_bounds__(256) void gz_kernel(MstepArgs a, int L, int NR) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         const int e = tid + 256 * u;
-        if (e < h * NR) th[(size_t)i0 * NR + e] = cconj(acc[u]);
+        if (e < h * NR) {
+            const size_t o = (size_t)i0 * NR + e;
+            if (mode == 0) th[o] = cconj(acc[u]);
+            else if (mode == 1) th[o] = csub(bref[(size_t)b * L * NR + o], acc[u]);
+            else th[o] = cadd(th[o], cconj(acc[u]));
+        }
     }
+}
+
+// Refinement gate: C = F F^H's conditioning from F's diagonal over the kept columns of G.  The
+// first solve's relative error grows like eps cond(C) (times a modest factor: 6e-5 measured at
+// cond 9e8, tools/rank_study.py); trials with max/min F_kk^2 below 1e4 are already at the
+// rounding level and skip the refinement step (skip[b] = 1, also for trials already done).
+__global__ __launch_bounds__(256) void mn_gate_kernel(MstepArgs a, int L) {
+    const int b = blockIdx.x;
+    __shared__ double red[4];
+    if (a.done && a.done[b]) {
+        if (threadIdx.x == 0) a.mnskip[b] = 1;
+        return;
+    }
+    const cd* F = a.gram + (size_t)b * L * L;
+    const cd* G = a.R + (size_t)b * L * L;
+    const int act = a.act[b];
+    double mx = 0.0, mn = INFINITY;
+    for (int i = threadIdx.x; i < act; i += 256) {
+        if (G[(size_t)i * L + i].x == 0.0) continue;       // a dropped column: C's unit placeholder
+        const double d = F[(size_t)i * L + i].x;
+        const double p = d * d;
+        mx = fmax(mx, p);
+        mn = fmin(mn, p);
+    }
+    mx = block_max(mx, red);
+    __syncthreads();
+    mn = -block_max(-mn, red);
+    if (threadIdx.x == 0) a.mnskip[b] = (act == 0 || mn * 1e4 >= mx) ? 1 : 0;
 }
 
 hipError_t launch_act(const Problem& pb, const MstepArgs& a, int k0, hipStream_t s) {
@@ -528,7 +568,8 @@ hipError_t launch_act(const Problem& pb, const MstepArgs& a, int k0, hipStream_t
 }  // namespace
 
 hipError_t launch_minnorm(const Problem& pb, const MstepArgs& a, hipStream_t s) {
-    if (pb.NR > 8 || !a.gram || !a.grhs || !a.act || !a.tol2 || !a.winv || !a.tol || !a.dvec)
+    if (pb.NR > 8 || !a.gram || !a.grhs || !a.act || !a.tol2 || !a.winv || !a.tol || !a.dvec ||
+        !a.mnr || !a.mnskip)
         return hipErrorInvalidValue;
     const int L = pb.L, nb = (L + TB - 1) / TB;
     hipError_t e;
@@ -557,7 +598,7 @@ hipError_t launch_minnorm(const Problem& pb, const MstepArgs& a, hipStream_t s) 
         else
             hipLaunchKernelGGL(gram_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, s, a, L, ntiles);
     }
-    hipLaunchKernelGGL(ghb_kernel, dim3(nb, pb.B), dim3(256), 0, s, a, L, pb.NR);
+    hipLaunchKernelGGL(ghb_kernel, dim3(nb, pb.B), dim3(256), 0, s, a, L, pb.NR, (const cd*)a.rhs, 0);
     hipLaunchKernelGGL(gram_tol_kernel, dim3(pb.B), dim3(256), 0, s, a, L);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // z = C^-2 c:  C = F F^H with the fused F^-1, then F^-H, F^-1, F^-H
@@ -568,17 +609,47 @@ hipError_t launch_minnorm(const Problem& pb, const MstepArgs& a, hipStream_t s) 
     if ((e = launch_tile_factor(pb, c, exC, nullptr, s)) != hipSuccess) return e;
     if ((e = launch_tile_back(pb, c, a.act, s)) != hipSuccess) return e;
     const size_t upd_lds = (size_t)TB * (TB + 1) * sizeof(cd) + (size_t)TB * 8 * sizeof(cd);
-    for (int k = 0; k < nb; ++k) {
-        const int k0 = k * TB, w = (L - k0) < TB ? (L - k0) : TB;
-        hipLaunchKernelGGL(fwddiag_kernel, dim3(pb.B), dim3(256), 0, s, c, L, pb.NR, k0, w, a.act);
-        if (nb - k - 1 > 0)
-            hipLaunchKernelGGL(fwdupd_kernel, dim3(nb - k - 1, pb.B), dim3(256), upd_lds, s, c, L,
-                               pb.NR, k0, w, a.act);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
+    // forward solve F y = c on grhs (the factorisation fused the first one)
+    auto forward = [&](const MstepArgs& cc) -> hipError_t {
+        for (int k = 0; k < nb; ++k) {
+            const int k0 = k * TB, w = (L - k0) < TB ? (L - k0) : TB;
+            hipLaunchKernelGGL(fwddiag_kernel, dim3(pb.B), dim3(256), 0, s, cc, L, pb.NR, k0, w, a.act);
+            if (nb - k - 1 > 0)
+                hipLaunchKernelGGL(fwdupd_kernel, dim3(nb - k - 1, pb.B), dim3(256), upd_lds, s, cc, L,
+                                   pb.NR, k0, w, a.act);
+            hipError_t e2 = hipGetLastError();
+            if (e2 != hipSuccess) return e2;
+        }
+        return hipSuccess;
+    };
+    if ((e = forward(c)) != hipSuccess) return e;
     if ((e = launch_tile_back(pb, c, a.act, s)) != hipSuccess) return e;
     // theta = conj(G z)
-    hipLaunchKernelGGL(gz_kernel, dim3(nb, pb.B), dim3(256), upd_lds, s, a, L, pb.NR);
+    hipLaunchKernelGGL(gz_kernel, dim3(nb, pb.B), dim3(256), upd_lds, s, a, L, pb.NR, 0, a.theta,
+                       (const cd*)nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // One refinement step on the kept subspace, for the trials whose C is ill-conditioned:
+    //   x1 = x0 + G C^-2 G^H (b - G G^H x0).
+    // G G^H is R up to the dropped Schur complement (below the cut), and the residual is formed
+    // from G, not from C, so it is accurate to rounding; the step removes the first solve's error
+    // (which the squared conditioning of C^-2 amplifies) to second order.  Its fixed point is the
+    // minimum-norm solution of G G^H x = b on range(G) -- the same system, not a new answer.
+    hipLaunchKernelGGL(mn_gate_kernel, dim3(pb.B), dim3(256), 0, s, a, L);
+    MstepArgs r = a;                      // the refinement's launches skip the gated trials
+    r.done = a.mnskip;
+    MstepArgs cr = c;
+    cr.done = a.mnskip;
+    hipLaunchKernelGGL(ghb_kernel, dim3(nb, pb.B), dim3(256), 0, s, r, L, pb.NR, (const cd*)a.theta, 1);
+    hipLaunchKernelGGL(gz_kernel, dim3(nb, pb.B), dim3(256), upd_lds, s, r, L, pb.NR, 1, a.mnr,
+                       (const cd*)a.rhs);
+    hipLaunchKernelGGL(ghb_kernel, dim3(nb, pb.B), dim3(256), 0, s, r, L, pb.NR, (const cd*)a.mnr, 0);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = forward(cr)) != hipSuccess) return e;
+    if ((e = launch_tile_back(pb, cr, a.act, s)) != hipSuccess) return e;
+    if ((e = forward(cr)) != hipSuccess) return e;
+    if ((e = launch_tile_back(pb, cr, a.act, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(gz_kernel, dim3(nb, pb.B), dim3(256), upd_lds, s, r, L, pb.NR, 2, a.theta,
+                       (const cd*)nullptr);
     return hipGetLastError();
 }
 

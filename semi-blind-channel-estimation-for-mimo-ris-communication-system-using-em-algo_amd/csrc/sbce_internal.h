@@ -227,6 +227,8 @@ struct MstepArgs {
     int32_t* act;      // [B]  active extent: columns of G past act[b] are all dropped
     double* tol2;      // [B]  pivot threshold of C's Cholesky
     double* dvec;      // [B][L] diagonal of R's Schur complement (left-looking early exit)
+    cd* mnr;           // [B][L][NR] min-norm refinement: the residual b - G G^H x0
+    int32_t* mnskip;   // [B] min-norm refinement: 1 = the trial needs no refinement step
 };
 
 // Per-trial extents of one tiled-factorisation launch sequence (mstep_large.hip): column

@@ -171,7 +171,9 @@ def test_minnorm_graded_spectrum_vs_lstsq(sbce, decades):
     """A rank-deficient R whose KEPT eigenvalues are graded over `decades` decades (cond_kept
     10^decades, well above lstsq's cut): R = sum_p u_p u_p^H with u_p the rows of
     diag(sqrt(lambda)) Q^H (pilots only; the moments are zero), so the minimum-norm solution's
-    conditioning is cond_kept.  theta vs numpy lstsq at max(1e-10, 1e-14 cond_kept)."""
+    conditioning is cond_kept.  theta vs numpy lstsq at max(1e-10, 1e-14 cond_kept): the first
+    solve x0 = G (G^H G)^-2 G^H b loses ~eps cond_kept(C)-fold more than lstsq; the refinement
+    step the device takes for such trials (minnorm.hip mn_gate_kernel) restores lstsq's level."""
     rng = np.random.default_rng(decades)
     n_tx, n_rx, N, T_p, T_d = 2, 2, 32, 40, 4
     L = (N + 1) * n_tx
@@ -191,7 +193,8 @@ def test_minnorm_graded_spectrum_vs_lstsq(sbce, decades):
         cond, rank2 = _cond_kept(R[i], L * n_rx)
         assert rank == rank2 == T_p
         err = rel(th[i], th0)
-        assert err < max(1e-10, 1e-14 * cond) or st[i] & sbce._lib.SBCE_STATUS_RANK, (err, cond)
+        print(f"decades {decades} trial {i}: cond_kept {cond:.3g} theta rel err {err:.3g}")
+        assert err < max(1e-10, 1e-14 * cond), (err, cond)
 
 
 def test_minnorm_cfg2_rank_flagged_trials_vs_lstsq(sbce):
