@@ -98,6 +98,24 @@ def chol_flops_per_trial(L, n_rx, g3=True):
     return (4.0 / 3.0) * L ** 3 * (0.75 if g3 else 1.0) + 8.0 * n_rx * L * L
 
 
+def minnorm_flops_per_trial(L, n_rx, act, refined):
+    """The minimum-norm solve (csrc/minnorm.hip) as executed for a trial whose rank-cut
+    factorisation reached the active extent `act` (columns past it are never touched): Lanczos
+    (4 Hermitian mat-vecs, 8 L^2 each), the left-looking factorisation of act columns over L rows
+    (8 (L a^2/2 - a^3/3), four real MFMAs per complex product), C = G^H G on the active extent
+    and its Cholesky (three real MFMAs per complex product: x 3/4), G^H b and G z (8 n_rx (L a -
+    a^2/2) each), four triangular passes with C's factor (4 n_rx a^2 each); the refinement step
+    (refined = 1) adds two of each product with G and four more passes."""
+    a = float(act)
+    fac = 8.0 * (L * a * a / 2 - a ** 3 / 3)
+    gram = 0.75 * 8.0 * (L * a * a / 2 - a ** 3 / 3)
+    cfac = 0.75 * (4.0 / 3.0) * a ** 3
+    gmul = 8.0 * n_rx * (L * a - a * a / 2)
+    tri = 4.0 * n_rx * a * a
+    return (32.0 * L * L + fac + gram + cfac + 2 * gmul + 4 * tri
+            + refined * (4 * gmul + 4 * tri))
+
+
 def chol_bytes_per_trial(L, n_rx):
     """Minimal HBM bytes of the solve: R's lower triangle read once and the factor written once
     (16 B complex each), read once more by the back substitution, B^H read, theta written."""
@@ -582,11 +600,17 @@ def main(argv=None):
         return phase_traffic(pmc, kernels, anchor) if pmc_ok else None
 
     mflops = mstep_flops_per_trial_iter(n_tx, n_rx, N, T_p, T_d) * B
+    mn_stats = None
     if solve == "lstsq":
         # the min-norm factorisation stops at R's numerical rank (left-looking, minnorm.hip):
-        # its flops are rank dependent, so only the build (R and B^H) is counted
+        # priced per trial at the extent it reached (the last timed M-step's workspace)
         L_ = (N + 1) * n_tx
-        mflops = (rbuild_flops_per_trial_iter(n_tx, N, T_p, T_d) + 8 * n_rx * L_ * (T_d + T_p)) * B
+        rk = eng.minnorm_rank()
+        mn = sum(minnorm_flops_per_trial(L_, n_rx, int(a_), int(r_)) for a_, _, r_ in rk)
+        mflops = (rbuild_flops_per_trial_iter(n_tx, N, T_p, T_d) + 8 * n_rx * L_ * (T_d + T_p)) * B + mn
+        mn_stats = {"extent_mean": float(rk[:, 0].mean()), "rank_mean": float(rk[:, 1].mean()),
+                    "rank_min": int(rk[:, 1].min()), "rank_max": int(rk[:, 1].max()),
+                    "refined_trials": int(rk[:, 2].sum()), "minnorm_flops_per_launch": mn}
     mbytes = mstep_bytes_per_trial_iter(n_tx, n_rx, N, T_p, T_d) * B
     m_kern = MSTEP_KERNELS_LARGE if n_tx * P > 512 else MSTEP_KERNELS
     m_traffic = traffic_of(m_kern, MSTEP_ANCHORS)
@@ -603,9 +627,10 @@ def main(argv=None):
                   "measured_pipe_tflops": FP64_MFMA_MEASURED_TFLOPS,
                   "frac_of_measured_pipe": m_ach / FP64_MFMA_MEASURED_TFLOPS}
     if solve == "lstsq":
-        mstep_roof["note"] = ("flops count the R and B^H build only (the rank-cut factorisation, "
-                              "Lanczos, G^H G and its Cholesky are rank dependent): achieved is a "
-                              "lower bound")
+        mstep_roof["minnorm"] = mn_stats
+        mstep_roof["note"] = ("flops: the R and B^H build plus the min-norm solve priced per trial at "
+                              "the active extent its rank-cut factorisation reached "
+                              "(bench.minnorm_flops_per_trial, sbce_debug_minnorm_rank)")
     rb_roof = None
     if rb_ms is not None:
         rflops = rbuild_flops_per_trial_iter(n_tx, N, T_p, T_d) * B

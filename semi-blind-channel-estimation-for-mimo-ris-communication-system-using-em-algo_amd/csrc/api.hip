@@ -433,6 +433,25 @@ int sbce_debug_minnorm_tol(const sbce_dims* d, const sbce_ptrs* p, double* tol_o
                                  hipMemcpyDefault, (hipStream_t)hip_stream));
 }
 
+// Diagnostic, not part of include/sbce.h: per trial (active extent, rank, refinement ran) of the
+// last SBCE_SOLVE_MINNORM M-step whose workspace `p` holds (out3: [B][3] int32, device memory);
+// bench.py prices the min-norm solve at its executed flops from them.
+int sbce_debug_minnorm_rank(const sbce_dims* d, const sbce_ptrs* p, int32_t* out3, void* hip_stream) {
+    clear_stale_error();
+    Problem pb;
+    if (!make_problem(d, pb) || !out3) return SBCE_EINVAL;
+    int rc = check_ptrs(p, pb, true, SBCE_SOLVE_MINNORM);
+    if (rc) return rc;
+    if (pb.B == 0) return SBCE_OK;
+    const Carve c = carve(pb, SBCE_SOLVE_MINNORM);
+    MstepArgs ma;
+    ma.R = (cd*)((char*)p->workspace + c.R);
+    ma.done = nullptr;
+    ma.nbatch = pb.B;
+    set_large(ma, (char*)p->workspace, c);
+    return hip_rc(launch_minnorm_rank(pb, ma, out3, (hipStream_t)hip_stream));
+}
+
 // Diagnostic, not part of include/sbce.h: re-read the SBCE_* debug switches from the
 // environment (they are otherwise read once, when the library is loaded).  Returns 1 when a
 // result-affecting switch is now non-default (every trial is then flagged SBCE_STATUS_DEBUG).

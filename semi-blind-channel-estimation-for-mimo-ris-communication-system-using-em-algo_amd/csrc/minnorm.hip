@@ -560,12 +560,37 @@ __global__ __launch_bounds__(256) void mn_gate_kernel(MstepArgs a, int L) {
     if (threadIdx.x == 0) a.mnskip[b] = (act == 0 || mn * 1e4 >= mx) ? 1 : 0;
 }
 
+// DIAGNOSTIC (bench.py's executed-flop count): per trial the active extent act[b] the rank-cut
+// factorisation reached, the kept pivots of G (rank) and whether the refinement step ran.
+__global__ __launch_bounds__(256) void mn_rank_kernel(MstepArgs a, int L, int32_t* out) {
+    const int b = blockIdx.x;
+    __shared__ int cnt[4];
+    const cd* G = a.R + (size_t)b * L * L;
+    const int act = a.act[b];
+    int n = 0;
+    for (int i = threadIdx.x; i < act; i += 256) n += G[(size_t)i * L + i].x != 0.0 ? 1 : 0;
+    for (int off = 32; off >= 1; off >>= 1) n += __shfl_xor(n, off);
+    if ((threadIdx.x & 63) == 0) cnt[threadIdx.x >> 6] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        out[3 * b] = act;
+        out[3 * b + 1] = cnt[0] + cnt[1] + cnt[2] + cnt[3];
+        out[3 * b + 2] = a.mnskip[b] ? 0 : 1;
+    }
+}
+
 hipError_t launch_act(const Problem& pb, const MstepArgs& a, int k0, hipStream_t s) {
     hipLaunchKernelGGL(act_kernel, dim3(pb.B), dim3(256), 0, s, a, pb.L, k0);
     return hipGetLastError();
 }
 
 }  // namespace
+
+hipError_t launch_minnorm_rank(const Problem& pb, const MstepArgs& a, int32_t* out, hipStream_t s) {
+    if (!a.act || !a.mnskip) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(mn_rank_kernel, dim3(pb.B), dim3(256), 0, s, a, pb.L, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_minnorm(const Problem& pb, const MstepArgs& a, hipStream_t s) {
     if (pb.NR > 8 || !a.gram || !a.grhs || !a.act || !a.tol2 || !a.winv || !a.tol || !a.dvec ||

@@ -270,6 +270,8 @@ hipError_t launch_tile_factor(const Problem& pb, const MstepArgs& a, const TileE
                               hipError_t (*act_check)(const Problem&, const MstepArgs&, int, hipStream_t),
                               hipStream_t s);
 // L^H x = y on a.rhs by 64-column blocks (theta = conj(x) written when a.theta != null)
+// DIAGNOSTIC: out[3b..3b+2] = (active extent, rank of G, refinement ran) of the last min-norm solve
+hipError_t launch_minnorm_rank(const Problem& pb, const MstepArgs& a, int32_t* out, hipStream_t s);
 hipError_t launch_tile_back(const Problem& pb, const MstepArgs& a, const int32_t* ext, hipStream_t s);
 // minimum-norm solve (SBCE_SOLVE_MINNORM, minnorm.hip): R, rhs built; writes theta
 hipError_t launch_minnorm(const Problem& pb, const MstepArgs& a, hipStream_t s);

@@ -665,3 +665,14 @@ class EMEngine:
     def nmse(self):
         """Per-trial NMSE of the current theta against h (device, sbce_nmse)."""
         return nmse_batch(self.theta, self.h)
+
+    def minnorm_rank(self):
+        """(B, 3) int32: active extent, rank of G and whether the refinement step ran, of the
+        last whole-batch min-norm M-step (sbce_debug_minnorm_rank; solve='lstsq' only)."""
+        out = self.torch.zeros((self.B, 3), dtype=self.torch.int32, device="cuda")
+        fn = self.lib.sbce_debug_minnorm_rank
+        fn.restype = ctypes.c_int
+        rc = fn(ctypes.byref(self.dims), ctypes.byref(self.ptrs), ctypes.c_void_p(out.data_ptr()),
+                ctypes.c_void_p(self.torch.cuda.current_stream().cuda_stream))
+        _lib.check(rc, "sbce_debug_minnorm_rank")
+        return out.cpu().numpy()
