@@ -17,7 +17,7 @@ DebugConfig g_debug;
 
 namespace {
 constexpr DebugConfig kDebugDefault = {false, false, false, 4, false, false, false, false, 128,
-                                       0, false, false, 0, 0, false, true, false};
+                                       0, false, false, 0, 0, false, true};
 constexpr int kSphereBudgetMax = 256;      // estep.hip kBfsPmax
 
 void read_debug_env(DebugConfig& c) {
@@ -43,7 +43,6 @@ void read_debug_env(DebugConfig& c) {
     if ((v = env("SBCE_CHOL_IMPL"))) c.chol_impl = (v[0] == 'v' || v[0] == 'f' || v[0] == 'u' || v[0] == 'l' || v[0] == 'w') ? v[0] : 0;
     if ((v = env("SBCE_ESTEP_PAIR"))) c.estep_nopair = v[0] == '0';
     if ((v = env("SBCE_CPLX3"))) c.cplx3 = v[0] != '0';
-    if ((v = env("SBCE_HERK_TILE"))) c.herk128 = atoi(v) == 128;
 }
 
 __attribute__((constructor)) void load_debug_env() { read_debug_env(g_debug); }
@@ -58,7 +57,7 @@ bool debug_nondefault() {
            c.estep_nosphere != d.estep_nosphere || c.sphere_budget != d.sphere_budget ||
            c.rhs_impl != d.rhs_impl || c.rb_tc32 != d.rb_tc32 || c.upd_waves8 != d.upd_waves8 ||
            c.backsub != d.backsub || c.chol_impl != d.chol_impl || c.estep_nopair != d.estep_nopair ||
-           c.cplx3 != d.cplx3 || c.herk128 != d.herk128 ||
+           c.cplx3 != d.cplx3 ||
            (chol_debug_skip_mask() & 31);
 }
 

@@ -637,111 +637,6 @@ __global__ __launch_bounds__(256) void tile_herk_kernel(MstepArgs a, int L, int 
             }
 }
 
-// The same grouped update on 128 x 128 output tiles, 16 waves (1024 threads): every streamed
-// row of A (the tile's rows) and of B (the group's panel rows) now serves 128 outputs instead of
-// 64, halving the operand traffic of the K loop.  Wave w owns the 32 x 32 quadrant
-// (w >> 2, w & 3) -- the 64-tile kernel's per-wave work, element for element in the same k order,
-// so the results are bitwise those of tile_herk_kernel<false> (four real MFMAs per product).  Columns [c_lo, c_hi) of the group form
-// one or two 128-column tiles; a column tile's row tiles start at its first column; entries of
-// 64-blocks above the block diagonal are neither computed nor written (as in the 64-tile grid).
-constexpr int TB2 = 128;
-template <bool G3 = false>
-__global__ __launch_bounds__(1024) void tile_herk128_kernel(MstepArgs a, int L, int kb_lo, int nkb,
-                                                            int c_lo, int c_hi, int n0, int ntiles,
-                                                            TileExt ext) {
-    __shared__ cd As[TB2][KS + 1], Bs[TB2][KS + 1];
-    const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
-    const int b = (slot / ntiles) * 8 + xcd, tix = slot - (slot / ntiles) * ntiles;
-    if (b >= a.nbatch) return;
-    if (a.done && a.done[b]) return;
-    // column tile y (0: c_lo, 1: c_lo + 128), row tile x from that column
-    const int y = tix < n0 ? 0 : 1;
-    const int x = tix < n0 ? tix : tix - n0;
-    const int c0 = c_lo + TB2 * y, r0 = c0 + TB2 * x;
-    const int cend = (c0 + TB2) < c_hi ? (c0 + TB2) : c_hi;
-    const int k0 = kb_lo * TB;
-    int kend = (kb_lo + nkb) * TB < L ? (kb_lo + nkb) * TB : L;
-    if (ext.col) {
-        const int act = ext.col[b];
-        if (c0 >= act) return;              // dropped columns: never read again
-        kend = kend < act ? kend : act;
-    }
-    if (k0 >= kend) return;
-    if (ext.row && r0 >= ext.row[b]) return;
-    cd* R = a.R + (size_t)b * L * L;
-    const cd* Arow = R + (size_t)r0 * L;
-    const cd* Brow = R + (size_t)c0 * L;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int li = lane & 15, lk = lane >> 4;
-    const int wr = (wave >> 2) * 32, wc = (wave & 3) * 32;
-    // a quadrant wholly inside a 64-block above the block diagonal: nothing to compute
-    const bool live = (r0 + wr) / TB >= (c0 + wc) / TB && c0 + wc < cend;
-
-    d4v cre[2][2], cim[2][2], c2[2][2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int v = 0; v < 2; ++v) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int r = r0 + wr + 16 * u + lk + 4 * q, c = c0 + wc + 16 * v + li;
-                const cd xv = (live && r < L && c < cend) ? R[(size_t)r * L + c] : czero();
-                cre[u][v][q] = xv.x;
-                cim[u][v][q] = xv.y;
-            }
-            csub_init<G3>(cre[u][v], cim[u][v], c2[u][v]);
-        }
-    constexpr int PF = TB2 * KS / 1024;             // entries per thread and operand
-    cd pa[PF], pbv[PF];
-    auto fetch = [&](int kc) {
-#pragma unroll
-        for (int h = 0; h < PF; ++h) {
-            const int e = tid + 1024 * h, r = e / KS, k = e - r * KS;
-            const bool kin = kc + k < kend;
-            pa[h] = (kin && r0 + r < L) ? Arow[(size_t)r * L + kc + k] : czero();
-            pbv[h] = (kin && c0 + r < cend) ? Brow[(size_t)r * L + kc + k] : czero();
-        }
-    };
-    fetch(k0);
-    for (int kc = k0; kc < kend; kc += KS) {
-        __syncthreads();
-#pragma unroll
-        for (int h = 0; h < PF; ++h) {
-            const int e = tid + 1024 * h, r = e / KS, k = e - r * KS;
-            As[r][k] = pa[h];
-            Bs[r][k] = pbv[h];
-        }
-        __syncthreads();
-        if (kc + KS < kend) fetch(kc + KS);
-        if (live) {
-#pragma unroll
-            for (int s4 = 0; s4 < KS / 4; ++s4) {
-                cd av[2], bv[2];
-#pragma unroll
-                for (int u = 0; u < 2; ++u) av[u] = As[wr + 16 * u + li][4 * s4 + lk];
-#pragma unroll
-                for (int v = 0; v < 2; ++v) bv[v] = Bs[wc + 16 * v + li][4 * s4 + lk];
-#pragma unroll
-                for (int u = 0; u < 2; ++u)
-#pragma unroll
-                    for (int v = 0; v < 2; ++v)      // C -= A conj(B)^T
-                        csub_step<G3>(cre[u][v], cim[u][v], c2[u][v], av[u], bv[v]);
-            }
-        }
-    }
-    if (!live) return;
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int r = r0 + wr + 16 * u + lk + 4 * q, c = c0 + wc + 16 * v + li;
-                if (r < L && c < cend) R[(size_t)r * L + c] = csub_out<G3>(cre[u][v], cim[u][v], c2[u][v], q);
-            }
-}
-
 // dvec[b][j] -= sum_{m in [c0, c1)} |L[j][m]|^2 for rows j >= r0 = c1 (c1 clipped to the active
 // extent): the diagonal of the Schur complement after a group, for the min-norm early exit.
 // One wave per row (coalesced row segments), lanes reduced in a fixed order.
@@ -929,23 +824,6 @@ static hipError_t launch_herk(const Problem& pb, const MstepArgs& a, int kb_lo, 
     return hipGetLastError();
 }
 
-// the group update (every earlier column) on 128 x 128 tiles: columns [g0, g1) x 64
-static hipError_t launch_herk128(const Problem& pb, const MstepArgs& a, int g0, int g1, const TileExt& ex,
-                                 hipStream_t s) {
-    const int c_lo = g0 * TB, c_hi = (g1 * TB) < pb.L ? g1 * TB : pb.L;
-    const int n0 = (pb.L - c_lo + TB2 - 1) / TB2;
-    const int n1 = c_lo + TB2 < c_hi ? (pb.L - c_lo - TB2 + TB2 - 1) / TB2 : 0;
-    const int ntiles = n0 + n1;
-    const long nblk = 8L * ((pb.B + 7) / 8) * ntiles;
-    if (nblk > 0x7fffffffL) return hipErrorInvalidValue;
-    // four real MFMAs per complex product always: the three-MFMA form needs more than the 128
-    // VGPRs a 1024-thread block allows (the min-norm factorisation, the large-L default, uses
-    // four anyway)
-    hipLaunchKernelGGL(tile_herk128_kernel<false>, dim3((unsigned)nblk), dim3(1024), 0, s, a, pb.L, 0, g0,
-                       c_lo, c_hi, n0, ntiles, ex);
-    return hipGetLastError();
-}
-
 hipError_t launch_tile_factor_step(const Problem& pb, const MstepArgs& a, int k, const TileExt& ex,
                                    hipStream_t s) {
     const int nb = (pb.L + TB - 1) / TB;
@@ -982,9 +860,7 @@ hipError_t launch_tile_factor(const Problem& pb, const MstepArgs& a, const TileE
     for (int g0 = 0; g0 < nb; g0 += kTileGroup) {
         const int g1 = (g0 + kTileGroup) < nb ? (g0 + kTileGroup) : nb;
         if (act_check && (e = act_check(pb, a, g0 * TB, s)) != hipSuccess) return e;
-        if (g0 > 0 && (e = (g_debug.herk128 ? launch_herk128(pb, a, g0, g1, ex, s)
-                                            : launch_herk(pb, a, 0, g0, g0, g1, ex, s))) != hipSuccess)
-            return e;
+        if (g0 > 0 && (e = launch_herk(pb, a, 0, g0, g0, g1, ex, s)) != hipSuccess) return e;
         for (int k = g0; k < g1; ++k) {
             if ((e = launch_tile_factor_step(pb, a, k, ex, s)) != hipSuccess) return e;
             if (k + 1 < g1 && (e = launch_herk(pb, a, k, 1, k + 1, g1, ex, s)) != hipSuccess)

@@ -163,7 +163,6 @@ struct DebugConfig {
                          //                        'u' unified panel update + factor launch
     bool estep_nopair;   // SBCE_ESTEP_PAIR=0      no factorised-weight pass (estep_pair.hip)
     bool cplx3;          // SBCE_CPLX3=0           four real MFMAs per complex product (default: three, Gauss)
-    bool herk128;        // SBCE_HERK_TILE=128     large-L group updates on 128 x 128 tiles
 };
 extern DebugConfig g_debug;
 bool debug_nondefault();   // a result-affecting switch differs from its default

@@ -437,8 +437,11 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape):
         with sbce._lib.debug_env(SBCE_CHOL_IMPL=impl.split("_")[0],
                                  SBCE_BACKSUB=impl[-1] if "_bs" in impl else "0",
                                  SBCE_CPLX3="0" if impl.endswith("_c4") else "1"):
-            out[impl] = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], m, S,
-                                         0.05)
+            try:
+                out[impl] = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], m,
+                                             S, 0.05)
+            except sbce._lib.SbceError as e:
+                raise AssertionError(f"{impl}: {e}") from e
     th_m, R, rhs, st = out["batched"]
     assert not st.any()
     for i in range(2):

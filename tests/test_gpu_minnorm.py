@@ -226,19 +226,3 @@ def test_minnorm_cfg2_rank_flagged_trials_vs_lstsq(sbce):
         nm, nm0 = nmse(th[i], sub["h"][i]), nmse(th0, sub["h"][i])
         assert abs(nm / nm0 - 1) < 1e-6, (nm, nm0)                # measured <= 1e-7
         assert rel(th[i], th0) < 1e-3, rel(th[i], th0)           # measured <= 6.1e-5
-
-
-@pytest.mark.parametrize("shape", [(4, 4, 149, 16, 200), (8, 8, 80, 32, 100), (2, 2, 400, 12, 300)])
-def test_herk128_group_update_bitwise(sbce, shape):
-    """The large-L group update on 128 x 128 tiles (SBCE_HERK_TILE=128, tile_herk128_kernel) does
-    each element's work of the 64-tile kernel in the same order: the min-norm solve (four real
-    MFMAs per complex product) gives bitwise the same theta."""
-    n_tx, n_rx, N, T_p, T_d = shape
-    b = sbce.signal_model.synthetic_batch(3, n_tx, n_rx, N, T_p, T_d, 16, 0.05, seed=8)
-    m, S = _hard_moments(b["x_d"])
-    th0 = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], m, S, 0.05,
-                           solve="lstsq")[0]
-    with sbce._lib.debug_env(SBCE_HERK_TILE="128"):
-        th1 = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], m, S, 0.05,
-                               solve="lstsq")[0]
-    assert np.array_equal(th0, th1)
