@@ -62,13 +62,21 @@ _lib = None
 
 
 def load(path=None):
-    """Load libsbce.so (CPU-safe: loading does not touch the GPU)."""
+    """Load libsbce.so (CPU-safe: loading does not touch the GPU).
+
+    PyTorch is imported FIRST: its ROCm wheel ships its own HIP runtime (torch/lib/libamdhip64.so,
+    SONAME libamdhip64.so.7), and the device buffers and streams this library receives come from
+    that runtime.  Loaded after it, libsbce.so's NEEDED libamdhip64.so.7 resolves to the same
+    already-loaded runtime; loaded before it, the system /opt/rocm runtime would come in as well
+    and the process would run two HIP runtimes (the second to initialise finds no device:
+    hipErrorNoDevice on every launch)."""
     global _lib
     if _lib is not None and path is None:
         return _lib
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise SbceUnavailable(f"{p} not built: run __graft_entry__.build()")
+    import torch  # noqa: F401  (the HIP runtime this library must share; no GPU is touched)
     lib = ctypes.CDLL(p)
     lib.sbce_abi_version.restype = ctypes.c_int
     lib.sbce_abi_version.argtypes = []
