@@ -1697,10 +1697,12 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
     }
-    const bool wide = g_debug.chol_impl == 'w';
+    // default (round 4): the wide schedule -- even panels j >= 2 update panels j and j+1 by
+    // [0, jb) in one launch (panel_update2_kernel), odd panels are pre-updated by panel j-1 inside
+    // their factor launch: half the left-looking HBM re-reads (cfg1 M-step 2.32 -> 2.25 ms, EM
+    // +1.8 % at three streams).  SBCE_CHOL_IMPL=n: one update launch per 32-column panel (A/B).
+    const bool wide = g_debug.chol_impl == 0;
     for (int j = 0; j < npan && wide; ++j) {
-        // wide schedule: even panels j >= 2 update panels j and j+1 by [0, jb) in one launch; odd
-        // panels are pre-updated by panel j-1 inside their factor launch
         const int jb = j * PW;
         const int rem = (pb.L - jb + NB - 1) / NB;
         const bool g3 = g_debug.cplx3 && a.solve_mode == SBCE_SOLVE_CHOL;

@@ -430,9 +430,10 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape):
     # MFMAs per complex product; "fused" = one workgroup per trial; "valu"
     # "batched_bs1": batched, with the one-step-prefetch back substitution instead of the
     # one-barrier kernel (default for L <= 272, n_rx <= 4), two-ahead three-barrier kernel
-    # "wide": even panels update panels j and j+1 by [0, jb) in one launch, odd panels are pre-updated
-    # by their predecessor inside the factor launch
-    for impl in ("batched", "wide", "lookahead", "batched_c4", "fused", "valu", "batched_bs1",
+    # "batched" (default) is the wide schedule: even panels update panels j and j+1 by [0, jb) in
+    # one launch, odd panels are pre-updated by their predecessor inside the factor launch;
+    # "narrow" = one update launch per 32-column panel
+    for impl in ("batched", "narrow", "lookahead", "batched_c4", "fused", "valu", "batched_bs1",
                  "batched_bs2"):
         with sbce._lib.debug_env(SBCE_CHOL_IMPL=impl.split("_")[0],
                                  SBCE_BACKSUB=impl[-1] if "_bs" in impl else "0",
@@ -449,7 +450,7 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape):
         ref = np.conj(X).reshape(-1)
         for impl in out:
             assert rel(out[impl][0][i], ref) < 1e-9, impl
-    assert rel(th_m, out["wide"][0]) < 1e-12
+    assert rel(th_m, out["narrow"][0]) < 1e-12
     assert rel(th_m, out["lookahead"][0]) < 1e-12
     assert rel(th_m, out["batched_c4"][0]) < 1e-11
     assert rel(th_m, out["fused"][0]) < 1e-9

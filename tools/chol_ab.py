@@ -2,7 +2,8 @@
 """A/B of the L <= 512 Cholesky schedules on the bench workload (cfg1, 1000 trials): the M-step
 alone (sbce_mstep from fixed moments, HIP events on the launch stream) and the whole bench step,
 per SBCE_CHOL_IMPL arm, same process.
-  python tools/chol_ab.py [arm ...]      arms: default t (team) l (look-ahead)
+  python tools/chol_ab.py [arm ...]      arms: default (wide schedule) n (one update per panel)
+                                          l (look-ahead)
 """
 import json
 import os
@@ -14,7 +15,7 @@ sys.path.insert(0, ROOT)
 
 
 def main():
-    arms = sys.argv[1:] or ["default", "t"]
+    arms = sys.argv[1:] or ["default", "n"]
     import numpy as np
     import torch
     import __graft_entry__ as ge
