@@ -70,7 +70,8 @@ def metric_name(n_tx, N, T_p, T_d):
 ESTEP_KERNELS = ["estep_tree_kernel", "estep_bfs_kernel", "estep_pair_kernel", "estep_bounds_kernel", "estep_prep_kernel",
                  "estep_mfma_kernel_occ3", "estep_mfma_kernel"]
 MSTEP_KERNELS = ["pilot_factor_kernel", "pilot_rhs_kernel", "rbuild_herm_kernel", "rbuild_kernel", "rhs_lds_kernel",
-                 "rhs_dma_kernel", "rhs_kernel", "diag_tol_kernel", "panel_update_kernel", "panel_factor_kernel",
+                 "rhs_dma_kernel", "rhs_kernel", "diag_tol_kernel", "panel_update_kernel",
+                 "panel_update2_kernel", "panel_factor_kernel",
                  "backsub_kernel", "backsub2_kernel", "backsub3_kernel",
                  "backsub4_kernel", "chol_mfma_kernel"]
 MSTEP_KERNELS_LARGE = ["pilot_factor_kernel", "pilot_rhs_kernel", "rbuild_herm_kernel",
@@ -80,10 +81,11 @@ MSTEP_KERNELS_LARGE = ["pilot_factor_kernel", "pilot_rhs_kernel", "rbuild_herm_k
                        "backdiag_kernel", "backupd_kernel",
                        # the minimum-norm solve (csrc/minnorm.hip)
                        "lanczos_tol_kernel", "gram_kernel", "gram_tol_kernel", "ghb_kernel",
-                       "fwddiag_kernel", "fwdupd_kernel", "gz_kernel"]
-# launched exactly once per M-step (the divisor of the phase's PMC totals; the pilot
-# factorisation runs once per EM run, so its bytes are spread over the run's M-steps)
-MSTEP_ANCHORS = ["rhs_dma_kernel", "rhs_lds_kernel", "rhs_kernel"]
+                       "fwddiag_kernel", "fwdupd_kernel", "gz_kernel", "mn_gate_kernel"]
+# launched exactly once per full M-step (the divisor of the phase's PMC totals for kernels launched
+# several times per M-step; the pilot factorisation runs once per EM run, so its bytes are spread
+# over the run's M-steps)
+MSTEP_ANCHORS = ["diag_tol_kernel", "lanczos_tol_kernel"]   # once per full M-step solve
 # the L <= 512 Cholesky solve's launches (csrc/chol.hip; diag_tol_kernel runs once per M-step)
 CHOL_KERNELS = ["diag_tol_kernel", "panel_update_kernel", "panel_update2_kernel", "panel_factor_kernel",
                 "backsub4_kernel", "backsub3_kernel", "backsub2_kernel", "backsub_kernel"]
@@ -189,17 +191,36 @@ def kernel_traffic(pmc, kernel):
     return k["fetch_bytes_total"] / k["launches_fetch"] + k["write_bytes_total"] / k["launches_write"]
 
 
+# kernels launched exactly once per phase execution: their bytes are taken per launch (the bench
+# also launches the build kernels alone for its phase timings, so their launch counts exceed the
+# phase's); every other kernel of a phase is averaged over the phase's anchor launches
+ONCE_PER_PHASE = {"rbuild_herm_kernel", "rbuild_kernel", "rbuild_wide_kernel", "rhs_dma_kernel",
+                  "rhs_lds_kernel", "rhs_kernel", "diag_tol_kernel", "backsub4_kernel",
+                  "backsub3_kernel", "backsub2_kernel", "backsub_kernel", "lanczos_tol_kernel",
+                  "gram_kernel", "gram_tol_kernel", "mn_gate_kernel"}
+
+
 def phase_traffic(pmc, kernels, anchor):
-    """HBM bytes of ONE phase execution from a PMC summary (tools/pmc_summary.py): total
-    FETCH / WRITE bytes of the phase's kernels divided by the launches of its once-per-phase
-    anchor kernel (the first name in `anchor` the summary holds); None without an anchor."""
+    """HBM bytes of ONE phase execution from a PMC summary (tools/pmc_summary.py): for a kernel
+    launched once per phase (ONCE_PER_PHASE) its average FETCH / WRITE bytes per launch, for the
+    others (the panel and tile launches, several per phase) their totals divided by the launches
+    of the phase's once-per-phase anchor kernel (the first name in `anchor` the summary holds);
+    None without an anchor."""
     ks = (pmc or {}).get("kernels", {})
     anc = next((ks[a] for a in anchor if a in ks), None)
     if not anc or not anc["launches_fetch"] or not anc["launches_write"]:
         return None
-    ents = [v for k, v in ks.items() if k in kernels]
-    return (sum(e["fetch_bytes_total"] for e in ents) / anc["launches_fetch"] +
-            sum(e["write_bytes_total"] for e in ents) / anc["launches_write"])
+    tot = 0.0
+    for k, e in ks.items():
+        if k not in kernels:
+            continue
+        if k in ONCE_PER_PHASE:
+            tot += e["fetch_bytes_total"] / max(e["launches_fetch"], 1)
+            tot += e["write_bytes_total"] / max(e["launches_write"], 1)
+        else:
+            tot += e["fetch_bytes_total"] / anc["launches_fetch"]
+            tot += e["write_bytes_total"] / anc["launches_write"]
+    return tot
 
 
 def host_threads():
