@@ -722,7 +722,7 @@ constexpr int PW = 32;    // panel width: two 16-column sub-panels
 // G3: the complex products by three real MFMAs instead of four (csub_step, sbce_internal.h).
 template <int NWU, bool G3 = false>
 __device__ __forceinline__ void panel_update_body(const MstepArgs& a, int L, int jb, int kend, int ntile,
-                                                  int b, int grp, int skip, cd* Bp) {
+                                                  int b, int grp, int skip, cd* Bp, int kbeg = 0) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
@@ -755,7 +755,7 @@ __device__ __forceinline__ void panel_update_body(const MstepArgs& a, int L, int
         }
         csub_init<G3>(cre[v], cim[v], c2[v]);
     }
-    for (int kb0 = 0; kb0 < ((skip & 1) ? 0 : kend); kb0 += KBU) {
+    for (int kb0 = kbeg; kb0 < ((skip & 1) ? 0 : kend); kb0 += KBU) {
         const int kbs = (kend - kb0) < KBU ? (kend - kb0) : KBU;    // multiple of 16
         cd av[4];
         if (active) {
@@ -841,6 +841,21 @@ __global__ __launch_bounds__(256) void panel_update2_kernel(MstepArgs a, int L, 
     if (a.done && a.done[b]) return;
     if (g < gpt0) panel_update_body<4, G3>(a, L, jb, jb, ntile, b, g, skip, Bp);
     else panel_update_body<4, G3>(a, L, jb + PW, jb, ntile - 2, b, g - gpt0, skip, Bp);
+}
+
+// panel_preupd_kernel (wide schedule, odd panels): the rank-32 update of panel jb by the previous
+// panel's columns [jb - 32, jb) -- the part panel_update2_kernel left -- as a launch of its own over
+// every trial's four-tile groups, instead of by the four waves of the trial's factor workgroup
+// ahead of its diagonal chain (SBCE_CHOL_IMPL=q keeps that in-factor pre-update, A/B).
+template <bool G3 = false>
+__global__ __launch_bounds__(256) void panel_preupd_kernel(MstepArgs a, int L, int jb, int ntile, int gpt,
+                                                           int skip) {
+    __shared__ __attribute__((aligned(16))) cd Bp[PW * (KBU + 1)];
+    const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
+    const int b = (slot / gpt) * 8 + xcd, grp = slot - (slot / gpt) * gpt;
+    if (b >= a.nbatch) return;
+    if (a.done && a.done[b]) return;
+    panel_update_body<4, G3>(a, L, jb, jb, ntile, b, grp, skip, Bp, jb - PW);
 }
 
 // 16 x 16 tile of R (rows row0.., columns c0.., w valid columns) into per-lane registers:
@@ -1701,7 +1716,7 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
     // [0, jb) in one launch (panel_update2_kernel), odd panels are pre-updated by panel j-1 inside
     // their factor launch: half the left-looking HBM re-reads (cfg1 M-step 2.32 -> 2.25 ms, EM
     // +1.8 % at three streams).  SBCE_CHOL_IMPL=n: one update launch per 32-column panel (A/B).
-    const bool wide = g_debug.chol_impl == 0;
+    const bool wide = g_debug.chol_impl == 0 || g_debug.chol_impl == 'q';
     for (int j = 0; j < npan && wide; ++j) {
         const int jb = j * PW;
         const int rem = (pb.L - jb + NB - 1) / NB;
@@ -1717,7 +1732,17 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
                 hipLaunchKernelGGL(panel_update2_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L,
                                    jb, rem, gpt0, gpt1, skip);
         }
-        const bool pre = (j & 1) != 0;
+        const bool pre = (j & 1) != 0 && g_debug.chol_impl == 'q';
+        if ((j & 1) && !pre) {
+            const int gpt = (rem + 3) / 4;
+            const long nblk = 8L * ((pb.B + 7) / 8) * gpt;
+            if (g3)
+                hipLaunchKernelGGL(panel_preupd_kernel<true>, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L,
+                                   jb, rem, gpt, skip);
+            else
+                hipLaunchKernelGGL(panel_preupd_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L,
+                                   jb, rem, gpt, skip);
+        }
         if (g3 && pre)
             hipLaunchKernelGGL((panel_factor_kernel<true, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR,
                                jb, rem, skip);
