@@ -1715,8 +1715,10 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
     // default (round 4): the wide schedule -- even panels j >= 2 update panels j and j+1 by
     // [0, jb) in one launch (panel_update2_kernel), odd panels are pre-updated by panel j-1 inside
     // their factor launch: half the left-looking HBM re-reads (cfg1 M-step 2.32 -> 2.25 ms, EM
-    // +1.8 % at three streams).  SBCE_CHOL_IMPL=n: one update launch per 32-column panel (A/B).
-    const bool wide = g_debug.chol_impl == 0 || g_debug.chol_impl == 'q';
+    // +1.8 % at three streams).  SBCE_CHOL_IMPL=n: one update launch per 32-column panel;
+    // SBCE_CHOL_IMPL=s: the odd pre-update as a launch of its own (panel_preupd_kernel; measured
+    // M-step 2.32 vs 2.30 ms in-factor) -- both A/B only.
+    const bool wide = g_debug.chol_impl == 0 || g_debug.chol_impl == 's';
     for (int j = 0; j < npan && wide; ++j) {
         const int jb = j * PW;
         const int rem = (pb.L - jb + NB - 1) / NB;
@@ -1732,7 +1734,7 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
                 hipLaunchKernelGGL(panel_update2_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L,
                                    jb, rem, gpt0, gpt1, skip);
         }
-        const bool pre = (j & 1) != 0 && g_debug.chol_impl == 'q';
+        const bool pre = (j & 1) != 0 && g_debug.chol_impl != 's';
         if ((j & 1) && !pre) {
             const int gpt = (rem + 3) / 4;
             const long nblk = 8L * ((pb.B + 7) / 8) * gpt;

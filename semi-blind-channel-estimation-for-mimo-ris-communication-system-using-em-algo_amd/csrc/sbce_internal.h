@@ -159,7 +159,8 @@ struct DebugConfig {
     bool rb_tc32;        // SBCE_RB_TC=32          32-symbol R-build chunks
     bool upd_waves8;     // SBCE_UPD_WAVES=8       eight-tile panel-update blocks
     int backsub;         // SBCE_BACKSUB           0 default, 1..3 older back substitutions
-    char chol_impl;      // SBCE_CHOL_IMPL         0 default (wide update schedule), 'n' one update launch per
+    char chol_impl;      // SBCE_CHOL_IMPL         0 default (wide update schedule), 's' wide with the odd
+                         //                        pre-update launched separately, 'n' one update launch per
                          //                        panel, 'l' look-ahead panel steps, 'v' VALU, 'f' fused
                          //                        one-workgroup, 'u' unified panel update + factor launch
     bool estep_nopair;   // SBCE_ESTEP_PAIR=0      no factorised-weight pass (estep_pair.hip)

@@ -432,9 +432,9 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape):
     # one-barrier kernel (default for L <= 272, n_rx <= 4), two-ahead three-barrier kernel
     # "batched" (default) is the wide schedule: even panels update panels j and j+1 by [0, jb) in
     # one launch, odd panels are pre-updated by their predecessor inside the factor launch;
-    # "narrow" = one update launch per 32-column panel; "qpre" = the wide schedule with the odd
-    # panels' rank-32 pre-update inside their factor launch instead of a launch of its own
-    for impl in ("batched", "narrow", "qpre", "lookahead", "batched_c4", "fused", "valu",
+    # "narrow" = one update launch per 32-column panel; "spre" = the wide schedule with the odd
+    # panels' rank-32 pre-update as a launch of its own instead of inside their factor launch
+    for impl in ("batched", "narrow", "spre", "lookahead", "batched_c4", "fused", "valu",
                  "batched_bs1", "batched_bs2"):
         with sbce._lib.debug_env(SBCE_CHOL_IMPL=impl.split("_")[0],
                                  SBCE_BACKSUB=impl[-1] if "_bs" in impl else "0",
@@ -452,7 +452,7 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape):
         for impl in out:
             assert rel(out[impl][0][i], ref) < 1e-9, impl
     assert rel(th_m, out["narrow"][0]) < 1e-12
-    assert rel(th_m, out["qpre"][0]) < 1e-12
+    assert rel(th_m, out["spre"][0]) < 1e-12
     assert rel(th_m, out["lookahead"][0]) < 1e-12
     assert rel(th_m, out["batched_c4"][0]) < 1e-11
     assert rel(th_m, out["fused"][0]) < 1e-9
