@@ -504,12 +504,17 @@ __device__ double candidate_distance(const cd* H, const cd* yg, const cd* s_cons
 
 constexpr int kMfmaWaves = 2;
 constexpr int kChunk = 256;
+constexpr int kScreenD = 256;   // per-wave LDS doubles of the V16 FP32 screen tables
+
+typedef float f4v __attribute__((ext_vector_type(4)));
 
 // Per-wave LDS doubles of the MFMA sweep: heff | alpha | U | V | Q2 | lb | scratch (128) |
-// 2 x staged record (DMA double buffer: 128 + 32 done words, or the record itself)
+// 2 x staged record (DMA double buffer: 128 + 32 done words, or the record itself) |
+// FP32 screen tables (V16: alpha and U as floats, kScreenD doubles)
+constexpr int mfma_rec_d(int rec_words) { return 2 * (rec_words <= 128 ? 160 : (rec_words + 1) / 2 * 2 + 32); }
 constexpr int mfma_tab_d(int NO, int chunk, int steps, int M, int nkt_pad, int rec_words) {
-    return (2 * NO + chunk + 3 * (4 * steps) * M + nkt_pad + 128 + 1) / 2 * 2 +
-           2 * (rec_words <= 128 ? 160 : (rec_words + 1) / 2 * 2 + 32);
+    return (2 * NO + chunk + 3 * (4 * steps) * M + nkt_pad + 128 + 1) / 2 * 2 + mfma_rec_d(rec_words) +
+           kScreenD;
 }
 
 struct MfmaConst {
@@ -526,6 +531,7 @@ struct MfmaConst {
     int rowb;                  // row-tile bounds on (NT = 4 with a prep record)
     int rec_words;             // prep record + y_t, doubles (staged per symbol in LDS)
     int spw;                   // symbols per wave (consecutive; the next record prefetched)
+    int screen;                // V16 FP32 screen of the tile groups (SBCE_ESTEP_F32=0 disables)
 };
 
 // V16 (M == 16, NA == 2): the A operand's V term, V[kk][i & 15] = V[kk][lane & 15], is the
@@ -664,6 +670,10 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     double* s_lb = s_Q2 + 4 * STEPS * k_M;                     // [nkt] column-tile bounds
     double* s_tab = s_lb + k_nkt_pad;                          // scratch: 64 cd
     double* s_recb = s_tab + 128;                  // 2 x [prep record | y_t (128) | done (32)]
+    // V16 FP32 screen: alpha (row order: the f32 MFMA's C/D row of value q is 4 (lane >> 4) + q,
+    // not the f64 form's (lane >> 4) + 4 q) and U (s_U's layout) as floats
+    float* s_al32 = reinterpret_cast<float*>(s_recb + mfma_rec_d(k_rec_words));
+    float* s_U32 = s_al32 + 256;
 
     for (int i = threadIdx.x; i < k_M; i += blockDim.x) s_cons[i] = a.cons[i];
     __syncthreads();
@@ -861,7 +871,10 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
             }
             s_U[e] = u;
             if (NA == 2) s_V[e] = v;
-            if (V16) s_Q2[e] = q2;
+            if (V16) {
+                s_Q2[e] = q2;
+                s_U32[e] = (float)u;
+            }
         }
         wave_sync();
     }
@@ -870,10 +883,12 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     // V16: hoisted A-operand V term, and the B operand q_k = h_NA x_kt + h_NA+1 x_col split
     // into a per-kt LDS row (s_Q2) plus a lane constant (q3reg)
     double vreg[STEPS], q3reg[STEPS];
+    float vreg32[STEPS];
 #pragma unroll
     for (int s = 0; s < STEPS; ++s) {
         const int kk = 4 * s + rq;
         vreg[s] = V16 ? s_V[kk * 16 + col] : 0.0;
+        vreg32[s] = (float)vreg[s];
         double q3 = 0.0;
         if (V16 && kk < K2) {
             const cd hx = cmul(H[(NA + 1) * NR + (kk >> 1)], s_cons[col]);
@@ -885,6 +900,16 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     const int nktile = k_JB >> 4;
     const int ntile_chunk = k_chunk >> 4;
     bool table_ready = false;
+    // FP32 screen (V16): a tile group's distances first by FP32 MFMAs (v_mfma_f32_16x16x4f32,
+    // a third of the FP64 instruction's cycles); the FP64 group runs only if some entry can be
+    // within the skip bound.  |d32 - d| <= 2^-17 (2 max_i alpha_i + gamma_k) (rounding of the
+    // operands and of K2 + 1 f32 sums, |sum_kk P' Q| <= 2 |p_i||q_k| <= alpha_i + gamma_k), so
+    // a screened-out group is one the FP64 test below would discard too: results are bitwise
+    // those of the unscreened sweep.  A symbol whose groups mostly pass (wide posterior) stops
+    // screening after 16 groups.
+    double amax = 0.0;               // max_i alpha_i (set with the alpha table)
+    bool scr_on = V16 && c.screen;   // wave-uniform
+    int scr_n = 0, scr_pass = 0;
 
     const double hard_bound = d0 + 1e-10 * cscale_d + 1e-300;
     unsigned groups = 0;             // wave-uniform count of issued tile groups
@@ -921,6 +946,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb) xb[bb] = s_cons[(k >> (k_lm * (NB - 1 - bb))) & mask];
         double bop[STEPS];
+        float bop32[STEPS];
         double gam = 0.0;
         if constexpr (V16) {
             // gamma_k = ||q_k||^2 = sum over the 4 lanes of column k of their bop^2
@@ -931,6 +957,8 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
             }
             gam += bperm_d(gam, xaddr16);
             gam += bperm_d(gam, xaddr32);
+#pragma unroll
+            for (int s = 0; s < STEPS; ++s) bop32[s] = (float)bop[s];
         } else {
             cd qv[NR];
 #pragma unroll
@@ -958,6 +986,13 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
 #pragma unroll
         for (int q = 0; q < NA; ++q) mu[q] = czero();
         bool touched = false;       // wave-uniform: an exp was taken in this column tile
+        // V16 (NA = 2): hypothesis i = 16 s0 + s1 with s0 = the tile (wave-uniform per tile) and
+        // s1 = rq + 4 j (the lane's row j), so the per-column-tile sums factor: R1[j] = sum over
+        // tiles of w (-> ck, mu_1, nu_1), Q[j] = sum of w x_s0 (-> mu_0, and kappa through
+        // conj(x_s1)), N0 = sum of w |x_s0|^2 (-> nu_0); 4 VALU ops per weight instead of 21,
+        // the x_s1 products once per column tile
+        double R1[4] = {0.0, 0.0, 0.0, 0.0}, N0 = 0.0;
+        cd Q[4] = {czero(), czero(), czero(), czero()};
 
         for (int i0 = 0; i0 < k_JA; i0 += k_chunk) {
             if (!table_ready && V16) {
@@ -982,11 +1017,17 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                                                               cx, 0, 0, 0);
                 wave_sync();
                 const double nvv = s_tab[16 + col];
+                double am = 0.0;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int s0 = rq + 4 * j;
-                    s_al[s0 * 16 + (col & 3) * 4 + (col >> 2)] = 0.25 * (s_tab[s0] + nvv) + 0.5 * cx[j];
+                    const double al = 0.25 * (s_tab[s0] + nvv) + 0.5 * cx[j];
+                    s_al[s0 * 16 + (col & 3) * 4 + (col >> 2)] = al;
+                    s_al32[s0 * 16 + col] = (float)al;     // natural order: f32 C/D rows 4 rq + q
+                    am = fmax(am, al);
                 }
+                for (int off = 32; off >= 1; off >>= 1) am = fmax(am, shfl_xor_d(am, off));
+                amax = am;
                 wave_sync();
                 table_ready = true;
             }
@@ -1013,6 +1054,30 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                 // TU independent 16x16 tiles in flight: STEPS*TU MFMAs per group;
                 // accumulators start at alpha_i, gamma_k (lane constant) stays outside
                 if (V16 && !((rowmask >> tg) & ((1u << TU) - 1u))) continue;
+                if (V16 && scr_on) {
+                    f4v s32[TU];
+#pragma unroll
+                    for (int u = 0; u < TU; ++u)
+                        s32[u] = *reinterpret_cast<const f4v*>(s_al32 + (tg + u) * 16 + rq * 4);
+#pragma unroll
+                    for (int s = 0; s < STEPS; ++s)
+#pragma unroll
+                        for (int u = 0; u < TU; ++u) {
+                            const float av = s_U32[(4 * s + rq) * 16 + (i0 >> 4) + tg + u] + vreg32[s];
+                            s32[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bop32[s], s32[u], 0, 0, 0);
+                        }
+                    float m32 = fminf(fminf(s32[0][0], s32[0][1]), fminf(s32[0][2], s32[0][3]));
+#pragma unroll
+                    for (int u = 1; u < TU; ++u)
+                        m32 = fminf(m32, fminf(fminf(s32[u][0], s32[u][1]), fminf(s32[u][2], s32[u][3])));
+                    const double lim = ((MODE == SBCE_ESTEP_HARD) ? best_d : mshift + c.thr_d) - gam +
+                                       0x1p-17 * (2.0 * amax + gam);
+                    ++scr_n;
+                    const bool pass = __any((double)m32 <= lim);
+                    scr_pass += pass;
+                    if (scr_n >= 16 && 2 * scr_pass > scr_n) scr_on = false;
+                    if (!pass) continue;
+                }
                 ++groups;
                 d4v acc[TU];
 #pragma unroll
@@ -1073,15 +1138,25 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                     for (int off = 32; off >= 1; off >>= 1) mn = fmin(mn, shfl_xor_d(mn, off));
                     const double f = fexp_neg((mn - mshift) * inv_s2);
                     mshift = mn;
-                    tot_c *= f; ck *= f; kap = cscale(kap, f); tot_kB = cscale(tot_kB, f);
+                    // V16: ck, mu are formed at the column tile's end; the stream-3 totals
+                    // (x_3 = cons[col], a lane constant) are formed after the sweep
+                    constexpr int NBS = V16 ? 1 : NB;
+                    tot_c *= f; kap = cscale(kap, f);
+                    if constexpr (!V16) { ck *= f; tot_kB = cscale(tot_kB, f); }
 #pragma unroll
                     for (int q = 0; q < NA; ++q) {
-                        tot_muA[q] = cscale(tot_muA[q], f); nu[q] *= f; mu[q] = cscale(mu[q], f);
+                        tot_muA[q] = cscale(tot_muA[q], f); nu[q] *= f;
+                        if constexpr (!V16) mu[q] = cscale(mu[q], f);
 #pragma unroll
-                        for (int bb = 0; bb < NB; ++bb) tot_X[q][bb] = cscale(tot_X[q][bb], f);
+                        for (int bb = 0; bb < NBS; ++bb) tot_X[q][bb] = cscale(tot_X[q][bb], f);
                     }
 #pragma unroll
-                    for (int bb = 0; bb < NB; ++bb) { tot_mB[bb] = cscale(tot_mB[bb], f); tot_nB[bb] *= f; }
+                    for (int bb = 0; bb < NBS; ++bb) { tot_mB[bb] = cscale(tot_mB[bb], f); tot_nB[bb] *= f; }
+                    if constexpr (V16) {
+                        N0 *= f;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) { R1[j] *= f; Q[j] = cscale(Q[j], f); }
+                    }
                 }
                 if (!__any(cm <= mshift + c.thr_d)) continue;
                 touched = true;
@@ -1090,6 +1165,21 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                     const double cmu =
                         fmin(fmin(acc[u][0], acc[u][1]), fmin(acc[u][2], acc[u][3])) + gam;
                     if (!__any(cmu <= mshift + c.thr_d)) continue;
+                    if constexpr (V16) {
+                        const cd x0 = s_cons[tg + u];          // stream 0 of the tile (i0 = 0)
+                        const double n0 = cabs2(x0);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const double dj = acc[u][j] + gam;
+                            // rows with no lane inside the bound: weights < e^-50 of the maximum
+                            if (!__any(dj <= mshift + c.thr_d)) continue;
+                            const double w = fexp_neg((mshift - dj) * inv_s2);
+                            R1[j] += w;
+                            Q[j] = caxpy(Q[j], w, x0);
+                            N0 = fma(w, n0, N0);
+                        }
+                        continue;
+                    }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int i = i0 + (tg + u) * 16 + rq + 4 * j;
@@ -1109,20 +1199,45 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
             }
         }
         if (MODE == SBCE_ESTEP_SOFT && touched) {
+            if constexpr (V16) {
+                // the lane's row streams x_s1 = cons[rq + 4 j]
+                ck = (R1[0] + R1[1]) + (R1[2] + R1[3]);
+                mu[0] = cadd(cadd(Q[0], Q[1]), cadd(Q[2], Q[3]));
+                mu[1] = czero();
+                nu[0] += N0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const cd x1 = s_cons[rq + 4 * j];
+                    mu[1] = caxpy(mu[1], R1[j], x1);
+                    nu[1] = fma(R1[j], cabs2(x1), nu[1]);
+                    kap = cadd(kap, cmulc(Q[j], x1));
+                }
+            }
+            constexpr int NBS = V16 ? 1 : NB;
             tot_c += ck;
 #pragma unroll
-            for (int bb = 0; bb < NB; ++bb) {
+            for (int bb = 0; bb < NBS; ++bb) {
                 tot_mB[bb] = caxpy(tot_mB[bb], ck, xb[bb]);
                 tot_nB[bb] = fma(ck, cabs2(xb[bb]), tot_nB[bb]);
             }
-            if (NPB) tot_kB = caxpy(tot_kB, ck, cmulc(xb[0], xb[NB > 1 ? 1 : 0]));
+            if (NPB && !V16) tot_kB = caxpy(tot_kB, ck, cmulc(xb[0], xb[NB > 1 ? 1 : 0]));
 #pragma unroll
             for (int q = 0; q < NA; ++q) {
                 tot_muA[q] = cadd(tot_muA[q], mu[q]);
 #pragma unroll
-                for (int bb = 0; bb < NB; ++bb) tot_X[q][bb] = cfmac(tot_X[q][bb], mu[q], xb[bb]);
+                for (int bb = 0; bb < NBS; ++bb) tot_X[q][bb] = cfmac(tot_X[q][bb], mu[q], xb[bb]);
             }
         }
+    }
+    if constexpr (V16) {
+        // stream 3 is the lane constant x_3 = cons[col] (k = 16 kt + col): its sums are the
+        // lane's totals times x_3
+        const cd x3 = s_cons[col];
+        tot_mB[1] = cscale(x3, tot_c);
+        tot_nB[1] = tot_c * cabs2(x3);
+        tot_kB = cmulc(tot_mB[0], x3);
+#pragma unroll
+        for (int q = 0; q < NA; ++q) tot_X[q][1] = cmulc(tot_muA[q], x3);
     }
 
     if (c.count && lane == 0) atomicAdd(&g_estep_mfma, (unsigned long long)groups * STEPS * TU);
@@ -2101,6 +2216,7 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     c.rec_words = c.prep_stride + 2 * pb.NR;
     c.tab_d = mfma_tab_d(NO, c.chunk, steps, pb.M, c.nkt_pad, c.rec_words);
     c.spw = g_debug.estep_spw;                           // symbols per wave (A/B runs)
+    c.screen = !g_debug.estep_nof32;                     // FP32 tile-group screen (V16)
     c.rowb = pb.NT == 4 && c.prune && !g_debug.estep_norowb;
     lds = 64 * sizeof(cd) + (size_t)kMfmaWaves * c.tab_d * sizeof(double);
     const long nsym = (long)pb.B * pb.Td;

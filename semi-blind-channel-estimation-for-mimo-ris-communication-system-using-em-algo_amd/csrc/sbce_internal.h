@@ -151,6 +151,7 @@ struct DebugConfig {
     bool estep_count;    // SBCE_ESTEP_COUNT=1     device counters (results unchanged)
     int estep_spw;       // SBCE_ESTEP_SPW         symbols per sweep wave (default 4)
     bool estep_norowb;   // SBCE_ESTEP_ROWB=0      no row-tile bounds
+    bool estep_nof32;    // SBCE_ESTEP_F32=0       no FP32 screen of the sweep's tile groups
     bool estep_occ2;     // SBCE_ESTEP_OCC=2       sweep without the VGPR cap
     bool prep_nouni;     // SBCE_PREP_UNI=0
     bool estep_nosphere; // SBCE_ESTEP_SPHERE=0    tile sweep only

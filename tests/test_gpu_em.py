@@ -296,6 +296,25 @@ def test_sphere_estep_cfg1_geometry(sbce, snr):
         assert np.array_equal(mh1, mh0)
 
 
+@pytest.mark.parametrize("snr", [30, 20, 10, 0, -5])
+def test_estep_fp32_screen_is_bitwise_neutral(sbce, snr):
+    """The sweep's FP32 screen of its tile groups (V16 geometry: n_tx = 4, 16-QAM) only skips
+    groups the FP64 test discards too: soft moments and hard decisions are BITWISE those of the
+    unscreened sweep (SBCE_ESTEP_F32=0), at theta_0 (the wide iteration-0 posteriors) and near
+    the true channel, with and without the sphere pass (which lists fewer symbols)."""
+    varn = float(sbce.signal_model.snr_to_varn(snr))
+    b = sbce.signal_model.synthetic_batch(4, 4, 4, 64, 16, 64, 16, varn, seed=40 + snr)
+    for th in (b["theta0"], b["h"] + 0.05 * b["theta0"] / np.abs(b["theta0"]).max()):
+        for sph in ("1", "0"):
+            res = {}
+            for f32 in ("1", "0"):
+                with sbce._lib.debug_env(SBCE_ESTEP_F32=f32, SBCE_ESTEP_SPHERE=sph):
+                    res[f32] = [sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], th, varn, 4, m)
+                                for m in ("soft", "hard")]
+            for (x1, y1), (x0, y0) in zip(res["1"], res["0"]):
+                assert np.array_equal(x1, x0) and np.array_equal(y1, y0), (snr, sph)
+
+
 def test_snr_sweep_entry_point_reproduces_reference_curve(sbce):
     """North-star parity through the sweep entry point: sweeps.nmse_vs_snr with the
     reference's own RNG replay (seed 0, one trial) gives the reference's NMSE-vs-SNR
