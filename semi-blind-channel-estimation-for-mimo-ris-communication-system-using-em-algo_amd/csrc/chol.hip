@@ -299,7 +299,7 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
     cd* th = a.theta + (size_t)b * L * NR;
     for (int e = tid; e < L * NR; e += nth) th[e] = cconj(y[e]);
     if (tid == 0 && a.status)
-        a.status[b] |= ((*flag & 1) ? SBCE_STATUS_NONHPD : 0) | ((*flag & 2) ? SBCE_STATUS_RANK : 0) |
+        a.status[b] |= ((*flag & 1) ? a.clamp_status : 0) | ((*flag & 2) ? SBCE_STATUS_RANK : 0) |
                        ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
 }
 
@@ -697,7 +697,7 @@ void chol_mfma_kernel(MstepArgs a, int L, int NR, int skip, CholGeom g) {
     }
 #undef SBCE_CLK
     if (tid == 0 && a.status)
-        a.status[b] |= ((*flag & 1) ? SBCE_STATUS_NONHPD : 0) | ((*flag & 2) ? SBCE_STATUS_RANK : 0) |
+        a.status[b] |= ((*flag & 1) ? a.clamp_status : 0) | ((*flag & 2) ? SBCE_STATUS_RANK : 0) |
                        ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
 }
 
@@ -1111,7 +1111,7 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
             wave_sync();
         }
     }
-    const int st = ((flag & 1) ? SBCE_STATUS_NONHPD : 0) | ((flag & 2) ? SBCE_STATUS_RANK : 0) |
+    const int st = ((flag & 1) ? a.clamp_status : 0) | ((flag & 2) ? SBCE_STATUS_RANK : 0) |
                    ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
     if (tid == 0 && st && a.status) atomicOr(&a.status[b], st);
 }
@@ -1429,7 +1429,7 @@ void panel_fused_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip)
             wave_sync();
         }
     }
-    const int st = ((flag & 1) ? SBCE_STATUS_NONHPD : 0) | ((flag & 2) ? SBCE_STATUS_RANK : 0) |
+    const int st = ((flag & 1) ? a.clamp_status : 0) | ((flag & 2) ? SBCE_STATUS_RANK : 0) |
                    ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
     if (tid == 0 && st && a.status) atomicOr(&a.status[b], st);
 }

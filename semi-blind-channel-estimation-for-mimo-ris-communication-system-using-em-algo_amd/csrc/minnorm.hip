@@ -628,7 +628,8 @@ hipError_t launch_minnorm(const Problem& pb, const MstepArgs& a, hipStream_t s) 
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // z = C^-2 c:  C = F F^H with the fused F^-1, then F^-H, F^-1, F^-H
     MstepArgs c = a;
-    c.R = a.gram; c.rhs = a.grhs; c.theta = nullptr; c.tol = a.tol2; c.status = nullptr;
+    c.R = a.gram; c.rhs = a.grhs; c.theta = nullptr; c.tol = a.tol2;
+    c.clamp_status = SBCE_STATUS_RANK;     // a clamped pivot of C: flagged, the refinement below runs
     c.solve_mode = SBCE_SOLVE_CHOL;
     const TileExt exC{a.act, a.act, 1};
     if ((e = launch_tile_factor(pb, c, exC, nullptr, s)) != hipSuccess) return e;

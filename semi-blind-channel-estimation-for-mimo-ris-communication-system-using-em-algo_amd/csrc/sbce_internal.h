@@ -232,6 +232,10 @@ struct MstepArgs {
     double* dvec;      // [B][L] diagonal of R's Schur complement (left-looking early exit)
     cd* mnr;           // [B][L][NR] min-norm refinement: the residual b - G G^H x0
     int32_t* mnskip;   // [B] min-norm refinement: 1 = the trial needs no refinement step
+    // status bit a clamped pivot sets: NONHPD for R; RANK for the min-norm solve's C = G^H G
+    // (HPD by construction: a clamp there means the kept subspace is too ill-conditioned for
+    // the normal equations to hold lstsq's accuracy)
+    int clamp_status = SBCE_STATUS_NONHPD;
 };
 
 // Per-trial extents of one tiled-factorisation launch sequence (mstep_large.hip): column
