@@ -309,6 +309,57 @@ __global__ __launch_bounds__(512) void chol_solve_kernel(MstepArgs a, int L, int
 // C/D value q at row (l>>4) + 4q, column l&15.
 constexpr int KCM = 16;                // k-chunk of the A-operand register pipeline
 
+// Di = L^-1 of a factored 16 x 16 diagonal block (A: L's lower part, pivots on the diagonal;
+// dinv: 1 / pivot, 0 for dropped / absent directions) by recursive doubling: Di[k][k] = dinv[k],
+// then for s = 1, 2, 4, 8 the off-diagonal block of every 2s x 2s diagonal block,
+//   Di21 = -D22 (L21 D11),
+// from the two s x s blocks inverted at the level before -- two lane-parallel products per level
+// (one output entry per lane) instead of 16 dependent row steps with cross-lane reductions.
+// A dropped direction (dinv = 0) zeroes its row and column of Di, as the row recurrence does.
+// P (L21 D11) is staged in Di's upper-right 8 x 8 quarter (strictly upper: no block of the
+// recursion touches it), zeroed at the end.
+__device__ __forceinline__ void diag_inverse_rd(const cd* A, cd* Di, const double* dinv, int w, int lane) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const int e = lane + 64 * h, r = e >> 4, c = e & 15;
+        Di[e] = (r == c && r < w) ? cmk(dinv[r], 0.0) : czero();
+    }
+    wave_sync();
+    cd* P = Di + 8;                                          // P[e] at Di[(e >> 3) * 16 + 8 + (e & 7)]
+#pragma unroll
+    for (int ls = 0; ls < 4; ++ls) {
+        const int s = 1 << ls;
+        const bool on = lane < 8 * s;                        // 8 s entries at this level
+        const int bi = lane >> (2 * ls), rem = lane & (s * s - 1);
+        const int i = rem >> ls, j = rem & (s - 1);
+        const int b0 = bi * 2 * s;
+        if (on) {                                            // P = L21 D11 (D11 lower: m >= j)
+            const cd* Lr = A + (b0 + s + i) * NB + b0;
+            cd acc = czero();
+#pragma unroll
+            for (int m = 0; m < s; ++m)
+                if (m >= j) acc = cfma(acc, Lr[m], Di[(b0 + m) * NB + b0 + j]);
+            P[(lane >> 3) * NB + (lane & 7)] = acc;
+        }
+        wave_sync();
+        if (on) {                                            // Di21 = -D22 P (D22 lower: m <= i)
+            const cd* Dr = Di + (b0 + s + i) * NB + b0 + s;
+            cd acc = czero();
+#pragma unroll
+            for (int m = 0; m < s; ++m) {
+                if (m <= i) {
+                    const int pe = bi * s * s + m * s + j;
+                    acc = cfma(acc, Dr[m], P[(pe >> 3) * NB + (pe & 7)]);
+                }
+            }
+            Di[(b0 + s + i) * NB + b0 + j] = (b0 + s + i < w) ? cmk(-acc.x, -acc.y) : czero();
+        }
+        wave_sync();
+    }
+    P[(lane >> 3) * NB + (lane & 7)] = czero();
+    wave_sync();
+}
+
 // One-wave factorisation of the w x w diagonal block held in LDS A[16][16] (lower part
 // valid).  Lane l owns entries (row (l>>4) + 4h, col l&15), h < 4.  Column c costs ONE
 // LDS round trip: every lane reads the pivot and the column entries it needs, then
@@ -318,6 +369,7 @@ constexpr int KCM = 16;                // k-chunk of the A-operand register pipe
 // sum over m (reduced by two xor-shuffles): 16 dependent steps of one round trip each.
 // Few registers, so the MFMA update loop keeps its occupancy.  Writes Di to LDS and the
 // factor rows + conj(Di) (strict upper) into R's diagonal block.
+template <bool RD = true, bool COLS2 = RD>
 __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double tol,
                                                 int solve_mode, cd* Di, double* dinv, int* flag,
                                                 cd* Rdiag, int L,
@@ -353,6 +405,31 @@ __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double t
         if (clk && lane == 0) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); clk[9] += t2 - tc; tc = t2; }
         wave_sync();                                         // all reads of column c done
         dinv[c] = inv;                                       // same value from every lane
+        if constexpr (COLS2) {
+            // every entry as new = base + A[r][c] f: trailing (col > c, r >= col): base = A[r][col],
+            // f = -conj(A[col][c]) / p^2; column c (r >= c, the pivot included): base = 0, f = 1/sqrt(p);
+            // others: base = A[r][col], f = 0 -- 4 FMAs and 7 selects per entry instead of the three
+            // candidate values and their selects.  The pivot's imaginary part is set to 0, and a
+            // clamped / dropped pivot (wave-uniform, rare) takes its value from piv as before.
+            const bool cgt = col > c && col < w, ceq = col == c;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const int r = r0 + 4 * h;
+                const bool trail = cgt && r >= col && r < w;
+                const bool iscol = ceq && r >= c && r < w;
+                const double fx = trail ? -lcs.x : (iscol ? inv : 0.0);
+                const double fy = trail ? -lcs.y : 0.0;
+                const double bx = iscol ? 0.0 : arx[h].x, by = iscol ? 0.0 : arx[h].y;
+                // A[r][c] enters only where it is read (r >= c: the lower part); the strict upper
+                // part of the block may hold anything (the workspace's previous contents)
+                const cd ac = csel(trail || iscol, arc[h], czero());
+                cd v = cmk(fma(ac.x, fx, fma(-ac.y, fy, bx)), fma(ac.x, fy, fma(ac.y, fx, by)));
+                const bool isdiag = ceq && r == c;
+                v.y = isdiag ? 0.0 : v.y;
+                if (bad) v.x = isdiag ? piv : v.x;           // wave-uniform branch
+                A[r * NB + col] = v;
+            }
+        } else {
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
             const int r = r0 + 4 * h;
@@ -366,14 +443,17 @@ __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double t
             v = csel(isdiag, cmk(piv, 0.0), v);
             A[r * NB + col] = v;
         }
+        }
         wave_sync();
         if (clk && lane == 0) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); clk[10] += t2 - tc; tc = t2; }
     }
     if (bad_any) *flag |= 1;
     if (near_any) *flag |= 2;
     if (clk && lane == 0) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); clk[0] += t2 - tc; tc = t2; }
+    if constexpr (RD) {
+        diag_inverse_rd(A, Di, dinv, w, lane);
+    } else {
     // Di[k][j] = (delta_kj - sum_{j<=m<k} L[k][m] Di[m][j]) / L[k][k]; lane = (j, part)
-    {
         const int j = lane & 15, part = lane >> 4;
 #pragma unroll 1
         for (int k = 0; k < NB; ++k) {
@@ -955,7 +1035,7 @@ constexpr int kFacXs = 0, kFacDiA = 4 * NB * NB, kFacDiB = kFacDiA + NB * NB, kF
               kFacYbA = kFacXA1 + NB * NB, kFacYbB = kFacYbA + NB * 8, kFacLds = kFacYbB + NB * 8;
 __device__ __forceinline__ void panel_preupdate(const MstepArgs& a, int L, int jb, int ntile, int b,
                                                 cd* Lp);
-template <bool G3 = false>
+template <bool G3 = false, bool RD = true>
 __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int NR, int jb, int ntile,
                                                   int b, int skip, cd* sm, double* dinv, int& flag) {
     // skip: DIAGNOSTIC phase mask (timing only, results invalid): 2 diag factors, 8 trsm tiles
@@ -1013,7 +1093,7 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
         }
         wave_sync();
         if (!(skip & 2)) {
-            factor_diag_lds(X, wA, lane, tol, a.solve_mode, DiA, dinv, &flag,
+            factor_diag_lds<RD>(X, wA, lane, tol, a.solve_mode, DiA, dinv, &flag,
                             R + (size_t)jb * L + jb, L);
             forward_y_lds(DiA, ybA, y + jb * NR, wA, NR, lane);
         }
@@ -1051,7 +1131,7 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
             for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = csub_out<G3>(cre, cim, c2, q);
             wave_sync();
             if (!(skip & 2)) {
-                factor_diag_lds(X, wB, lane, tol, a.solve_mode, DiB, dinv, &flag,
+                factor_diag_lds<RD>(X, wB, lane, tol, a.solve_mode, DiB, dinv, &flag,
                                 R + (size_t)jbB * L + jbB, L);
                 forward_y_lds(DiB, ybB, y + jbB * NR, wB, NR, lane);
             }
@@ -1118,7 +1198,7 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
 
 // PRE (wide schedule, odd panels): first the rank-32 update of the panel by the previous panel's
 // columns [jb-32, jb) (panel_preupdate: the part panel_update2_kernel left), then the factor.
-template <bool G3 = false, bool PRE = false>
+template <bool G3 = false, bool PRE = false, bool RD = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip) {
     __shared__ __attribute__((aligned(16))) cd sm[kFacLds];
@@ -1127,7 +1207,7 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
     if (PRE && !(skip & 1)) panel_preupdate(a, L, jb, ntile, b, sm);
-    panel_factor_body<G3>(a, L, NR, jb, ntile, b, skip, sm, dinv, flag);
+    panel_factor_body<G3, RD>(a, L, NR, jb, ntile, b, skip, sm, dinv, flag);
 }
 
 // ---------------------------------------------------------------- look-ahead panel step
@@ -1745,7 +1825,13 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
                 hipLaunchKernelGGL(panel_preupd_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L,
                                    jb, rem, gpt, skip);
         }
-        if (g3 && pre)
+        if (g3 && pre && g_debug.chol_inv_loop)     // SBCE_CHOL_INV=loop: the row-recurrence inverse (A/B)
+            hipLaunchKernelGGL((panel_factor_kernel<true, true, false>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
+                               pb.NR, jb, rem, skip);
+        else if (g3 && g_debug.chol_inv_loop)
+            hipLaunchKernelGGL((panel_factor_kernel<true, false, false>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
+                               pb.NR, jb, rem, skip);
+        else if (g3 && pre)
             hipLaunchKernelGGL((panel_factor_kernel<true, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR,
                                jb, rem, skip);
         else if (g3)

@@ -5,7 +5,7 @@
 
 namespace sbce {
 __global__ void ubench_kernel(cd* Rg, unsigned long long* out, int reps, int mode,
-                              unsigned long long* clk) {
+                              unsigned long long* clk, cd* Dout, cd* Aout) {
     __shared__ cd A[256], Di[256];
     __shared__ int flag;
     __shared__ double dinv[16];
@@ -18,12 +18,18 @@ __global__ void ubench_kernel(cd* Rg, unsigned long long* out, int reps, int mod
         }
         wave_sync();
         const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-        if (mode == 0) factor_diag_lds(A, 16, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16);
-        if (mode == 2) factor_diag_lds(A, 16, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16, clk);
+        if (mode == 0) factor_diag_lds<false>(A, 16, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16);
+        if (mode == 2) factor_diag_lds<false>(A, 16, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16, clk);
+        if (mode == 3) factor_diag_lds<true, false>(A, 16, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16);
+        if (mode == 6) factor_diag_lds<true, true>(A, 16, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16);
+        if (mode == 7) factor_diag_lds<true, true>(A, 13, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16);
+        if (mode == 4) factor_diag_lds<false>(A, 13, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16);
+        if (mode == 5) factor_diag_lds<true, false>(A, 13, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16);
         wave_sync();
         acc += __builtin_amdgcn_s_memtime() - t0;
     }
     if (lane == 0) out[0] = acc / reps;
+    for (int e = lane; e < 256; e += 64) { Dout[e] = Di[e]; Aout[e] = A[e]; }
 }
 }  // namespace sbce
 
@@ -35,11 +41,32 @@ int main() {
     unsigned long long* clk;
     hipMalloc(&clk, 32 * 8);
     hipMemset(clk, 0, 32 * 8);
-    for (int mode = 0; mode < 3; ++mode) {
-        hipLaunchKernelGGL(sbce::ubench_kernel, dim3(1), dim3(64), 0, 0, R, o, 50, mode, clk);
+    sbce::cd *Dd, *Ad;
+    hipMalloc(&Dd, 256 * sizeof(sbce::cd));
+    hipMalloc(&Ad, 256 * sizeof(sbce::cd));
+    sbce::cd Dh[8][256], Ah[8][256];
+    for (int mode = 0; mode < 8; ++mode) {
+        hipLaunchKernelGGL(sbce::ubench_kernel, dim3(1), dim3(64), 0, 0, R, o, 50, mode, clk, Dd, Ad);
         unsigned long long h = 0;
         hipMemcpy(&h, o, 8, hipMemcpyDeviceToHost);
+        hipMemcpy(Dh[mode], Dd, sizeof(Dh[mode]), hipMemcpyDeviceToHost);
+        hipMemcpy(Ah[mode], Ad, sizeof(Ah[mode]), hipMemcpyDeviceToHost);
         printf("mode %d: %llu cycles per call\n", mode, h);
+    }
+    // the recursive-doubling inverse (modes 3, 5) against the row recurrence (0, 4): max |diff|
+    for (int pr = 0; pr < 4; ++pr) {
+        const int m0 = (pr & 1) ? 4 : 0, m1 = pr == 0 ? 3 : pr == 1 ? 5 : pr == 2 ? 6 : 7;
+        double mx = 0, mag = 0;
+        for (int e = 0; e < 256; ++e) {
+            const double dx = Dh[m0][e].x - Dh[m1][e].x, dy = Dh[m0][e].y - Dh[m1][e].y;
+            mx = fmax(mx, fabs(dx) + fabs(dy));
+            mag = fmax(mag, fabs(Dh[m0][e].x) + fabs(Dh[m0][e].y));
+        }
+        double ma = 0;
+        for (int e = 0; e < 256; ++e)
+            if ((e & 15) <= (e >> 4)) ma = fmax(ma, fabs(Ah[m0][e].x - Ah[m1][e].x) + fabs(Ah[m0][e].y - Ah[m1][e].y));
+        printf("modes %d vs %d (w=%d): max |Di diff| = %.3g (max |Di| %.3g), max |L diff| = %.3g\n", m0, m1,
+               (pr & 1) ? 13 : 16, mx, mag, ma);
     }
     unsigned long long hc[32];
     hipMemcpy(hc, clk, sizeof(hc), hipMemcpyDeviceToHost);
