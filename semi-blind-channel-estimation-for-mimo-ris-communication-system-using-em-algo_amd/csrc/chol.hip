@@ -114,14 +114,17 @@ __device__ __forceinline__ void forward_y_lds(const cd* Di, cd* yb, cd* yglob, i
                                               int lane) {
     const int e0 = lane, e1 = lane + 64;
     cd t0 = czero(), t1 = czero();
-    if (e0 < w * NR) {
-        const int c = e0 / NR, r = e0 - c * NR;
-        for (int c2 = 0; c2 <= c; ++c2) t0 = cfma(t0, Di[c * NB + c2], yb[c2 * NR + r]);
-    }
-    if (e1 < w * NR) {
-        const int c = e1 / NR, r = e1 - c * NR;
-        for (int c2 = 0; c2 <= c; ++c2) t1 = cfma(t1, Di[c * NB + c2], yb[c2 * NR + r]);
-    }
+    // all 16 terms with every load issued up front (Di's strict upper part is zero, so the terms
+    // past the row's diagonal add nothing), four partial sums: a dependent chain of 4, not 16
+    auto row = [&](int e) {
+        const int c = e / NR, r = e - c * NR;
+        cd p[4] = {czero(), czero(), czero(), czero()};
+#pragma unroll
+        for (int c2 = 0; c2 < NB; ++c2) p[c2 & 3] = cfma(p[c2 & 3], Di[c * NB + c2], yb[c2 * NR + r]);
+        return cadd(cadd(p[0], p[1]), cadd(p[2], p[3]));
+    };
+    if (e0 < w * NR) t0 = row(e0);
+    if (e1 < w * NR) t1 = row(e1);
     wave_sync();
     if (e0 < NB * NR) yb[e0] = t0;
     if (e1 < NB * NR) yb[e1] = t1;
@@ -398,7 +401,7 @@ __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double t
         near_any |= solve_mode == SBCE_SOLVE_MINNORM && dia > tol * (1.0 / 8) && dia < tol * 64;
         const bool drop = bad && solve_mode != SBCE_SOLVE_CHOL;
         const double pv = bad ? tol : dia;
-        const double rs = fast_rsqrt(pv);
+        const double rs = COLS2 ? fast_rsqrt64(pv) : fast_rsqrt(pv);
         const double piv = drop ? 0.0 : pv * rs;
         const double inv = drop ? 0.0 : rs;
         const cd lcs = cscale(cconj(lc), inv * inv);
@@ -406,28 +409,27 @@ __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double t
         wave_sync();                                         // all reads of column c done
         dinv[c] = inv;                                       // same value from every lane
         if constexpr (COLS2) {
-            // every entry as new = base + A[r][c] f: trailing (col > c, r >= col): base = A[r][col],
-            // f = -conj(A[col][c]) / p^2; column c (r >= c, the pivot included): base = 0, f = 1/sqrt(p);
-            // others: base = A[r][col], f = 0 -- 4 FMAs and 7 selects per entry instead of the three
-            // candidate values and their selects.  The pivot's imaginary part is set to 0, and a
-            // clamped / dropped pivot (wave-uniform, rare) takes its value from piv as before.
-            const bool cgt = col > c && col < w, ceq = col == c;
+            // Per lane, the role in column step c depends only on its column (lane-uniform over
+            // the 4 entries): col > c trailing, new = A[r][col] - A[r][c] conj(A[col][c]) / p;
+            // col == c the column, new = A[r][c] / sqrt(p); col < c final (not stored).  So every
+            // entry is new = m A[r][col] + A[r][c] f with (m, f) per lane, and the rows above the
+            // diagonal are not excluded: they are the strict upper part (never read as L; its
+            // values, the workspace's old contents included, only pass through or become other
+            // garbage there).  Rows and columns past w are zero and stay zero.  The pivot entry is
+            // then stored as (piv, 0) by its owner.  6 FP64 ops per entry, no per-entry selects.
+            const bool gt = col > c, eq = col == c;
+            const double m = eq ? 0.0 : 1.0;
+            const double fx = gt ? -lcs.x : (eq ? inv : 0.0);
+            const double fy = gt ? -lcs.y : 0.0;
+            if (col >= c) {
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                const int r = r0 + 4 * h;
-                const bool trail = cgt && r >= col && r < w;
-                const bool iscol = ceq && r >= c && r < w;
-                const double fx = trail ? -lcs.x : (iscol ? inv : 0.0);
-                const double fy = trail ? -lcs.y : 0.0;
-                const double bx = iscol ? 0.0 : arx[h].x, by = iscol ? 0.0 : arx[h].y;
-                // A[r][c] enters only where it is read (r >= c: the lower part); the strict upper
-                // part of the block may hold anything (the workspace's previous contents)
-                const cd ac = csel(trail || iscol, arc[h], czero());
-                cd v = cmk(fma(ac.x, fx, fma(-ac.y, fy, bx)), fma(ac.x, fy, fma(ac.y, fx, by)));
-                const bool isdiag = ceq && r == c;
-                v.y = isdiag ? 0.0 : v.y;
-                if (bad) v.x = isdiag ? piv : v.x;           // wave-uniform branch
-                A[r * NB + col] = v;
+                for (int h = 0; h < 4; ++h) {
+                    const int r = r0 + 4 * h;
+                    const cd v = cmk(fma(arc[h].x, fx, fma(-arc[h].y, fy, m * arx[h].x)),
+                                     fma(arc[h].x, fy, fma(arc[h].y, fx, m * arx[h].y)));
+                    A[r * NB + col] = v;
+                }
+                if (eq && r0 == (c & 3)) A[c * NB + c] = cmk(piv, 0.0);
             }
         } else {
 #pragma unroll
@@ -988,14 +990,16 @@ __device__ __forceinline__ void trsm_tile16(cd* R, cd* y, const cd* Di, const cd
     }
     const bool isre = li < NR, on = li < 2 * NR;
     const int r = isre ? li : li - NR;
-    d4v u = {0.0, 0.0, 0.0, 0.0};
+    // two accumulation chains of four MFMAs (Re X and Im X parts) instead of one of eight
+    d4v u = {0.0, 0.0, 0.0, 0.0}, u2 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int s2 = 0; s2 < NB / 4; ++s2) {
         const cd v = on ? yb[(4 * s2 + lk) * NR + r] : czero();     // Y_blk[4s+lk][r]
         const double b1 = isre ? v.x : v.y, b2 = isre ? -v.y : v.x;
         u = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[s2].x, b1, u, 0, 0, 0);
-        u = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[s2].y, b2, u, 0, 0, 0);
+        u2 = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[s2].y, b2, u2, 0, 0, 0);
     }
+    u += u2;
     if (on) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {

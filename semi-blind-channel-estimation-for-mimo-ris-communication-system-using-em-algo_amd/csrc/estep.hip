@@ -2120,8 +2120,18 @@ __global__ __launch_bounds__(64 * kBfsWaves) void estep_bfs_kernel(EstepArgs a, 
                 const int ib = NT & 1;
                 const double* lb = s_pb[wave][ib];
                 const int* li = s_pi[wave][ib];
+                // the minimum and every leaf's weight lane-parallel (the weights go to the free
+                // half of the path-bound buffer); the output lanes then only accumulate
                 double dmin = INFINITY;
-                for (int k = 0; k < n_in; ++k) dmin = fmin(dmin, lb[k]);
+                for (int k = lane; k < n_in; k += 64) dmin = fmin(dmin, lb[k]);
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) dmin = fmin(dmin, shfl_xor_d(dmin, off));
+                double* lw = s_pb[wave][ib ^ 1];
+                for (int k = lane; k < n_in; k += 64) {
+                    const double d = lb[k];
+                    lw[k] = d <= dmin + c.thr_d ? fexp_neg((dmin - d) * c.inv_s2) : 0.0;
+                }
+                wave_sync();
                 if (lane < MS) {
                     const int sp_ = lane < NT ? lane : (lane - NT) / NT;   // output stream pair
                     const int sq_ = lane < NT ? 0 : (lane - NT) % NT;
@@ -2135,9 +2145,8 @@ __global__ __launch_bounds__(64 * kBfsWaves) void estep_bfs_kernel(EstepArgs a, 
                     double z = 0.0;
                     cd v = czero();
                     for (int k = 0; k < n_in; ++k) {
-                        const double d = lb[k];
-                        if (d <= dmin + c.thr_d) {
-                            const double w = fexp_neg((dmin - d) * c.inv_s2);
+                        const double w = lw[k];             // > 0 exactly for the leaves within
+                        if (w != 0.0) {                     // 50 varn^2 of the minimum
                             const int id = li[k];
                             const cd xp = s_cons[(id >> (lm * lp)) & mask];
                             const cd xq = s_cons[(id >> (lm * lq)) & mask];

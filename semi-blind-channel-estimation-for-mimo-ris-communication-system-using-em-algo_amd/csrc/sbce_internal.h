@@ -138,6 +138,15 @@ __device__ __forceinline__ double fast_rsqrt(double x) {
     y = fma(0.5 * y, r, y);
     return __builtin_amdgcn_ldexp(y, -h);
 }
+// The same from the FP64 hardware seed (v_rsq_f64, no exponent split or f32 round trip): five
+// dependent ops instead of ten on the Cholesky pivot chain; two Newton steps as above.
+__device__ __forceinline__ double fast_rsqrt64(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    double r = fma(-x * y, y, 1.0);
+    y = fma(0.5 * y, r, y);
+    r = fma(-x * y, y, 1.0);
+    return fma(0.5 * y, r, y);
+}
 
 
 // ------------------------------------------------------------------ debug configuration

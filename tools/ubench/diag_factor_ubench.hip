@@ -64,7 +64,8 @@ int main() {
         }
         double ma = 0;
         for (int e = 0; e < 256; ++e)
-            if ((e & 15) <= (e >> 4)) ma = fmax(ma, fabs(Ah[m0][e].x - Ah[m1][e].x) + fabs(Ah[m0][e].y - Ah[m1][e].y));
+            if ((e & 15) <= (e >> 4) && (e >> 4) < ((pr & 1) ? 13 : 16))     // L's rows < w
+                ma = fmax(ma, fabs(Ah[m0][e].x - Ah[m1][e].x) + fabs(Ah[m0][e].y - Ah[m1][e].y));
         printf("modes %d vs %d (w=%d): max |Di diff| = %.3g (max |Di| %.3g), max |L diff| = %.3g\n", m0, m1,
                (pr & 1) ? 13 : 16, mx, mag, ma);
     }
