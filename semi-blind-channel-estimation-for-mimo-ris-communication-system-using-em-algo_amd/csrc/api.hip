@@ -17,7 +17,7 @@ DebugConfig g_debug;
 
 namespace {
 constexpr DebugConfig kDebugDefault = {false, false, false, 4, false, false, false, false, false, 128,
-                                       0, false, false, 0, 0, false, false, true};
+                                       0, false, false, 0, 0, 0, false, true};
 constexpr int kSphereBudgetMax = 256;      // estep.hip kBfsPmax
 
 void read_debug_env(DebugConfig& c) {
@@ -30,7 +30,7 @@ void read_debug_env(DebugConfig& c) {
     if ((v = env("SBCE_ESTEP_SPW"))) c.estep_spw = atoi(v) < 1 ? 1 : atoi(v);
     if ((v = env("SBCE_ESTEP_ROWB"))) c.estep_norowb = v[0] == '0';
     if ((v = env("SBCE_ESTEP_F32"))) c.estep_nof32 = v[0] == '0';
-    if ((v = env("SBCE_CHOL_INV"))) c.chol_inv_loop = v[0] == 'l';
+    if ((v = env("SBCE_CHOL_INV"))) c.chol_inv = (v[0] == 'l' || v[0] == 'p') ? v[0] : 0;
     if ((v = env("SBCE_ESTEP_OCC"))) c.estep_occ2 = v[0] == '2';
     if ((v = env("SBCE_PREP_UNI"))) c.prep_nouni = v[0] == '0';
     if ((v = env("SBCE_ESTEP_SPHERE"))) c.estep_nosphere = v[0] == '0';
@@ -55,7 +55,7 @@ bool debug_nondefault() {
     const DebugConfig& d = kDebugDefault;
     return c.estep_valu != d.estep_valu || c.estep_noprune != d.estep_noprune ||
            c.estep_spw != d.estep_spw || c.estep_norowb != d.estep_norowb || c.estep_nof32 != d.estep_nof32 ||
-           c.chol_inv_loop != d.chol_inv_loop ||
+           c.chol_inv != d.chol_inv ||
            c.estep_occ2 != d.estep_occ2 || c.prep_nouni != d.prep_nouni ||
            c.estep_nosphere != d.estep_nosphere || c.sphere_budget != d.sphere_budget ||
            c.rhs_impl != d.rhs_impl || c.rb_tc32 != d.rb_tc32 || c.upd_waves8 != d.upd_waves8 ||

@@ -372,7 +372,7 @@ __device__ __forceinline__ void diag_inverse_rd(const cd* A, cd* Di, const doubl
 // sum over m (reduced by two xor-shuffles): 16 dependent steps of one round trip each.
 // Few registers, so the MFMA update loop keeps its occupancy.  Writes Di to LDS and the
 // factor rows + conj(Di) (strict upper) into R's diagonal block.
-template <bool RD = true, bool COLS2 = RD>
+template <bool RD = true, bool COLS2 = RD, bool PAIR = false>
 __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double tol,
                                                 int solve_mode, cd* Di, double* dinv, int* flag,
                                                 cd* Rdiag, int L,
@@ -380,11 +380,74 @@ __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double t
     const int col = lane & 15, r0 = lane >> 4;
     unsigned long long tc = clk ? __builtin_amdgcn_s_memtime() : 0;
     bool bad_any = false, near_any = false;
+    if constexpr (PAIR) {
+        // Two columns per LDS round trip: column c1 = c + 1 is updated by column c in registers
+        // (A'[x][c1] = A[x][c1] - A[x][c] g, g = conj(A[c1][c]) / p0), its pivot follows from
+        // p1 = A[c1][c1] - |A[c1][c]|^2 / p0, and every entry takes both rank-1 steps at once:
+        //   col > c1: m = 1, f0 = -conj(A[col][c]) / p0, f1 = -conj(A'[col][c1]) / p1
+        //   col == c1: A'[r][c1] / sqrt(p1);   col == c: A[r][c] / sqrt(p0);   col < c: final.
+        // Garbage in the strict upper part meets only zero factors of entries that are upper
+        // themselves, except (c, c) (A[c][c1] is upper), which its owner then stores as (p0, 0).
+#pragma unroll 1
+        for (int c = 0; c < w; c += 2) {
+            const int c1 = c + 1;
+            const bool two = c1 < w;
+            const double dia0 = A[c * NB + c].x, dia1 = A[c1 * NB + c1].x;
+            const cd a10 = A[c1 * NB + c];
+            const cd lc0 = A[col * NB + c], lc1 = A[col * NB + c1];
+            cd arc0[4], arc1[4], arx[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const int r = r0 + 4 * h;
+                arc0[h] = A[r * NB + c];
+                arc1[h] = A[r * NB + c1];
+                arx[h] = A[r * NB + col];
+            }
+            const bool bad0 = !(dia0 > tol);
+            const bool drop0 = bad0 && solve_mode != SBCE_SOLVE_CHOL;
+            const double pv0 = bad0 ? tol : dia0;
+            const double rs0 = fast_rsqrt64(pv0);
+            const double piv0 = drop0 ? 0.0 : pv0 * rs0, inv0 = drop0 ? 0.0 : rs0;
+            const double q0 = inv0 * inv0;
+            const cd g = cmk(a10.x * q0, -a10.y * q0);                   // conj(a10) / p0
+            const double d1 = dia1 - fma(a10.x, g.x, -a10.y * g.y);      // A'[c1][c1]
+            const bool bad1 = two && !(d1 > tol);
+            const bool drop1 = bad1 && solve_mode != SBCE_SOLVE_CHOL;
+            const double pv1 = bad1 ? tol : d1;
+            const double rs1 = two ? fast_rsqrt64(pv1) : 0.0;
+            const double piv1 = (drop1 || !two) ? 0.0 : pv1 * rs1, inv1 = (drop1 || !two) ? 0.0 : rs1;
+            bad_any |= bad0 || bad1;
+            near_any |= solve_mode == SBCE_SOLVE_MINNORM &&
+                        ((dia0 > tol * (1.0 / 8) && dia0 < tol * 64) || (two && d1 > tol * (1.0 / 8) && d1 < tol * 64));
+            const cd t1 = csub(lc1, cmul(lc0, g));                       // A'[col][c1]
+            const double q1 = inv1 * inv1;
+            wave_sync();                                                 // all reads done
+            dinv[c] = inv0;
+            if (two) dinv[c1] = inv1;
+            const bool gt = col > c1, eq0 = col == c, eq1 = col == c1;
+            const double m = gt ? 1.0 : 0.0;
+            const double f0x = gt ? -lc0.x * q0 : (eq0 ? inv0 : 0.0), f0y = gt ? lc0.y * q0 : 0.0;
+            const double f1x = gt ? -t1.x * q1 : (eq1 ? inv1 : 0.0), f1y = gt ? t1.y * q1 : 0.0;
+            if (col >= c) {
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    const int r = r0 + 4 * h;
+                    const cd a1 = csub(arc1[h], cmul(arc0[h], g));       // A'[r][c1]
+                    const double vx = fma(a1.x, f1x, fma(-a1.y, f1y, fma(arc0[h].x, f0x, fma(-arc0[h].y, f0y, m * arx[h].x))));
+                    const double vy = fma(a1.x, f1y, fma(a1.y, f1x, fma(arc0[h].x, f0y, fma(arc0[h].y, f0x, m * arx[h].y))));
+                    A[r * NB + col] = cmk(vx, vy);
+                }
+                if (eq0 && r0 == (c & 3)) A[c * NB + c] = cmk(piv0, 0.0);
+                if (eq1 && two && r0 == (c1 & 3)) A[c1 * NB + c1] = cmk(piv1, 0.0);
+            }
+            wave_sync();
+        }
+    }
     // Branch-free: every entry (r, col) has exactly one owner lane, which rewrites it each
     // column (unchanged entries get their old value back); divergent branches in this
     // single-wave dependent chain cost more than the arithmetic.
 #pragma unroll 1
-    for (int c = 0; c < w; ++c) {
+    for (int c = 0; c < (PAIR ? 0 : w); ++c) {
         const double dia = A[c * NB + c].x;
         const cd lc = A[col * NB + c];                      // A[col][c] (unscaled)
         cd arc[4], arx[4];
@@ -1039,7 +1102,7 @@ constexpr int kFacXs = 0, kFacDiA = 4 * NB * NB, kFacDiB = kFacDiA + NB * NB, kF
               kFacYbA = kFacXA1 + NB * NB, kFacYbB = kFacYbA + NB * 8, kFacLds = kFacYbB + NB * 8;
 __device__ __forceinline__ void panel_preupdate(const MstepArgs& a, int L, int jb, int ntile, int b,
                                                 cd* Lp);
-template <bool G3 = false, bool RD = true>
+template <bool G3 = false, int DM = 1>   // diagonal blocks: 0 row-recurrence inverse, 1 recursive doubling, 2 + two columns per step
 __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int NR, int jb, int ntile,
                                                   int b, int skip, cd* sm, double* dinv, int& flag) {
     // skip: DIAGNOSTIC phase mask (timing only, results invalid): 2 diag factors, 8 trsm tiles
@@ -1097,7 +1160,7 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
         }
         wave_sync();
         if (!(skip & 2)) {
-            factor_diag_lds<RD>(X, wA, lane, tol, a.solve_mode, DiA, dinv, &flag,
+            factor_diag_lds<DM != 0, DM != 0, DM == 2>(X, wA, lane, tol, a.solve_mode, DiA, dinv, &flag,
                             R + (size_t)jb * L + jb, L);
             forward_y_lds(DiA, ybA, y + jb * NR, wA, NR, lane);
         }
@@ -1135,7 +1198,7 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
             for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = csub_out<G3>(cre, cim, c2, q);
             wave_sync();
             if (!(skip & 2)) {
-                factor_diag_lds<RD>(X, wB, lane, tol, a.solve_mode, DiB, dinv, &flag,
+                factor_diag_lds<DM != 0, DM != 0, DM == 2>(X, wB, lane, tol, a.solve_mode, DiB, dinv, &flag,
                                 R + (size_t)jbB * L + jbB, L);
                 forward_y_lds(DiB, ybB, y + jbB * NR, wB, NR, lane);
             }
@@ -1202,7 +1265,7 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
 
 // PRE (wide schedule, odd panels): first the rank-32 update of the panel by the previous panel's
 // columns [jb-32, jb) (panel_preupdate: the part panel_update2_kernel left), then the factor.
-template <bool G3 = false, bool PRE = false, bool RD = true>
+template <bool G3 = false, bool PRE = false, int DM = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip) {
     __shared__ __attribute__((aligned(16))) cd sm[kFacLds];
@@ -1211,7 +1274,7 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
     if (PRE && !(skip & 1)) panel_preupdate(a, L, jb, ntile, b, sm);
-    panel_factor_body<G3, RD>(a, L, NR, jb, ntile, b, skip, sm, dinv, flag);
+    panel_factor_body<G3, DM>(a, L, NR, jb, ntile, b, skip, sm, dinv, flag);
 }
 
 // ---------------------------------------------------------------- look-ahead panel step
@@ -1829,11 +1892,18 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
                 hipLaunchKernelGGL(panel_preupd_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L,
                                    jb, rem, gpt, skip);
         }
-        if (g3 && pre && g_debug.chol_inv_loop)     // SBCE_CHOL_INV=loop: the row-recurrence inverse (A/B)
-            hipLaunchKernelGGL((panel_factor_kernel<true, true, false>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
+        // SBCE_CHOL_INV=loop: the row-recurrence inverse, =pair: two columns per step (A/B)
+        if (g3 && pre && g_debug.chol_inv == 'l')
+            hipLaunchKernelGGL((panel_factor_kernel<true, true, 0>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
                                pb.NR, jb, rem, skip);
-        else if (g3 && g_debug.chol_inv_loop)
-            hipLaunchKernelGGL((panel_factor_kernel<true, false, false>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
+        else if (g3 && g_debug.chol_inv == 'l')
+            hipLaunchKernelGGL((panel_factor_kernel<true, false, 0>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
+                               pb.NR, jb, rem, skip);
+        else if (g3 && pre && g_debug.chol_inv == 'p')
+            hipLaunchKernelGGL((panel_factor_kernel<true, true, 2>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
+                               pb.NR, jb, rem, skip);
+        else if (g3 && g_debug.chol_inv == 'p')
+            hipLaunchKernelGGL((panel_factor_kernel<true, false, 2>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
                                pb.NR, jb, rem, skip);
         else if (g3 && pre)
             hipLaunchKernelGGL((panel_factor_kernel<true, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR,

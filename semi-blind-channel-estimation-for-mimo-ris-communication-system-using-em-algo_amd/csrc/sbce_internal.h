@@ -173,7 +173,8 @@ struct DebugConfig {
                          //                        pre-update launched separately, 'n' one update launch per
                          //                        panel, 'l' look-ahead panel steps, 'v' VALU, 'f' fused
                          //                        one-workgroup, 'u' unified panel update + factor launch
-    bool chol_inv_loop;  // SBCE_CHOL_INV=loop     diagonal-block inverse by the 16-step row recurrence
+    char chol_inv;       // SBCE_CHOL_INV          0 default (recursive-doubling inverse), 'l' (loop) the
+                         //                        16-step row recurrence, 'p' (pair) two columns per step
     bool estep_nopair;   // SBCE_ESTEP_PAIR=0      no factorised-weight pass (estep_pair.hip)
     bool cplx3;          // SBCE_CPLX3=0           four real MFMAs per complex product (default: three, Gauss)
 };

@@ -456,11 +456,12 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape):
     # "batched_il": the diagonal-block inverse by the 16-step row recurrence instead of the
     # recursive doubling (SBCE_CHOL_INV=loop)
     for impl in ("batched", "narrow", "spre", "lookahead", "batched_c4", "fused", "valu",
-                 "batched_bs1", "batched_bs2", "batched_il"):
+                 "batched_bs1", "batched_bs2", "batched_il", "batched_pair"):
         with sbce._lib.debug_env(SBCE_CHOL_IMPL=impl.split("_")[0],
                                  SBCE_BACKSUB=impl[-1] if "_bs" in impl else "0",
                                  SBCE_CPLX3="0" if impl.endswith("_c4") else "1",
-                                 SBCE_CHOL_INV="loop" if impl.endswith("_il") else "rd"):
+                                 SBCE_CHOL_INV="loop" if impl.endswith("_il") else
+                                 "pair" if impl.endswith("_pair") else "rd"):
             try:
                 out[impl] = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], m,
                                              S, 0.05)
@@ -476,6 +477,7 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape):
     assert rel(th_m, out["narrow"][0]) < 1e-12
     assert rel(th_m, out["spre"][0]) < 1e-12
     assert rel(th_m, out["batched_il"][0]) < 1e-12
+    assert rel(th_m, out["batched_pair"][0]) < 1e-12
     assert rel(th_m, out["lookahead"][0]) < 1e-12
     assert rel(th_m, out["batched_c4"][0]) < 1e-11
     assert rel(th_m, out["fused"][0]) < 1e-9

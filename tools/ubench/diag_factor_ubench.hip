@@ -23,6 +23,8 @@ __global__ void ubench_kernel(cd* Rg, unsigned long long* out, int reps, int mod
         if (mode == 3) factor_diag_lds<true, false>(A, 16, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16);
         if (mode == 6) factor_diag_lds<true, true>(A, 16, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16);
         if (mode == 7) factor_diag_lds<true, true>(A, 13, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16);
+        if (mode == 8) factor_diag_lds<true, true, true>(A, 16, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16);
+        if (mode == 9) factor_diag_lds<true, true, true>(A, 13, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16);
         if (mode == 4) factor_diag_lds<false>(A, 13, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16);
         if (mode == 5) factor_diag_lds<true, false>(A, 13, lane, 1e-14, 0, Di, dinv, &flag, Rg, 16);
         wave_sync();
@@ -44,8 +46,8 @@ int main() {
     sbce::cd *Dd, *Ad;
     hipMalloc(&Dd, 256 * sizeof(sbce::cd));
     hipMalloc(&Ad, 256 * sizeof(sbce::cd));
-    sbce::cd Dh[8][256], Ah[8][256];
-    for (int mode = 0; mode < 8; ++mode) {
+    sbce::cd Dh[10][256], Ah[10][256];
+    for (int mode = 0; mode < 10; ++mode) {
         hipLaunchKernelGGL(sbce::ubench_kernel, dim3(1), dim3(64), 0, 0, R, o, 50, mode, clk, Dd, Ad);
         unsigned long long h = 0;
         hipMemcpy(&h, o, 8, hipMemcpyDeviceToHost);
@@ -54,8 +56,9 @@ int main() {
         printf("mode %d: %llu cycles per call\n", mode, h);
     }
     // the recursive-doubling inverse (modes 3, 5) against the row recurrence (0, 4): max |diff|
-    for (int pr = 0; pr < 4; ++pr) {
-        const int m0 = (pr & 1) ? 4 : 0, m1 = pr == 0 ? 3 : pr == 1 ? 5 : pr == 2 ? 6 : 7;
+    for (int pr = 0; pr < 6; ++pr) {
+        const int m1s[6] = {3, 5, 6, 7, 8, 9};
+        const int m0 = (pr & 1) ? 4 : 0, m1 = m1s[pr];
         double mx = 0, mag = 0;
         for (int e = 0; e < 256; ++e) {
             const double dx = Dh[m0][e].x - Dh[m1][e].x, dy = Dh[m0][e].y - Dh[m1][e].y;
