@@ -2120,12 +2120,12 @@ __global__ __launch_bounds__(64 * kBfsWaves) void estep_bfs_kernel(EstepArgs a, 
                 const int ib = NT & 1;
                 const double* lb = s_pb[wave][ib];
                 const int* li = s_pi[wave][ib];
-                // the minimum and every leaf's weight lane-parallel (the weights go to the free
-                // half of the path-bound buffer); the output lanes then only accumulate
+                // every leaf's weight lane-parallel (to the free half of the path-bound buffer);
+                // the output lanes then only accumulate.  The minimum stays a serial LDS scan
+                // (independent reads; a 6-step cross-lane reduction costs more for the few
+                // leaves most symbols have)
                 double dmin = INFINITY;
-                for (int k = lane; k < n_in; k += 64) dmin = fmin(dmin, lb[k]);
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) dmin = fmin(dmin, shfl_xor_d(dmin, off));
+                for (int k = 0; k < n_in; ++k) dmin = fmin(dmin, lb[k]);
                 double* lw = s_pb[wave][ib ^ 1];
                 for (int k = lane; k < n_in; k += 64) {
                     const double d = lb[k];
