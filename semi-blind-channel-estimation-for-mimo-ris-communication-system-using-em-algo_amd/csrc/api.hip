@@ -31,7 +31,7 @@ void read_debug_env(DebugConfig& c) {
     if ((v = env("SBCE_ESTEP_ROWB"))) c.estep_norowb = v[0] == '0';
     if ((v = env("SBCE_ESTEP_F32"))) c.estep_nof32 = v[0] == '0';
     if ((v = env("SBCE_CHOL_INV"))) c.chol_inv = (v[0] == 'l' || v[0] == 'p') ? v[0] : 0;
-    if ((v = env("SBCE_ESTEP_OCC"))) c.estep_occ2 = v[0] == '2';
+    if ((v = env("SBCE_ESTEP_OCC"))) c.estep_occ = (v[0] == '2' || v[0] == '3') ? v[0] : 0;
     if ((v = env("SBCE_PREP_UNI"))) c.prep_nouni = v[0] == '0';
     if ((v = env("SBCE_ESTEP_SPHERE"))) c.estep_nosphere = v[0] == '0';
     if ((v = env("SBCE_SPHERE_BUDGET"))) {
@@ -56,7 +56,7 @@ bool debug_nondefault() {
     return c.estep_valu != d.estep_valu || c.estep_noprune != d.estep_noprune ||
            c.estep_spw != d.estep_spw || c.estep_norowb != d.estep_norowb || c.estep_nof32 != d.estep_nof32 ||
            c.chol_inv != d.chol_inv ||
-           c.estep_occ2 != d.estep_occ2 || c.prep_nouni != d.prep_nouni ||
+           c.estep_occ != d.estep_occ || c.prep_nouni != d.prep_nouni ||
            c.estep_nosphere != d.estep_nosphere || c.sphere_budget != d.sphere_budget ||
            c.rhs_impl != d.rhs_impl || c.rb_tc32 != d.rb_tc32 || c.upd_waves8 != d.upd_waves8 ||
            c.backsub != d.backsub || c.chol_impl != d.chol_impl || c.estep_nopair != d.estep_nopair ||
@@ -286,8 +286,9 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
             if ((rc = hip_rc(launch_estep(pb, eas, estep_mode, s)))) return rc;
             if ((rc = hip_rc(launch_sup_shift_mom(pb, ea.mom, (const cd*)p->x_sup, ea.done, s))))
                 return rc;
-        } else if ((rc = hip_rc(launch_estep(pb, ea, estep_mode, s)))) {
-            return rc;
+        } else {
+            ea.wide = it == 0;
+            if ((rc = hip_rc(launch_estep(pb, ea, estep_mode, s)))) return rc;
         }
         if ((rc = hip_rc(launch_mstep_build(pb, ma, s, prefactor)))) return rc;
         // Gaussian prior, n_rx = 1: the reference's all-ones covariance term stays in A

@@ -1100,6 +1100,7 @@ __device__ __forceinline__ void load_ycomp(const cd* y, int L, int NR, int row0,
 // LDS of the factor body (cd entries): Xs (4 waves' 16 x 16 scratch), DiA, DiB, XA1, ybA, ybB
 constexpr int kFacXs = 0, kFacDiA = 4 * NB * NB, kFacDiB = kFacDiA + NB * NB, kFacXA1 = kFacDiB + NB * NB,
               kFacYbA = kFacXA1 + NB * NB, kFacYbB = kFacYbA + NB * 8, kFacLds = kFacYbB + NB * 8;
+template <bool G3 = false>
 __device__ __forceinline__ void panel_preupdate(const MstepArgs& a, int L, int jb, int ntile, int b,
                                                 cd* Lp);
 template <bool G3 = false, int DM = 1>   // diagonal blocks: 0 row-recurrence inverse, 1 recursive doubling, 2 + two columns per step
@@ -1273,7 +1274,7 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
     __shared__ int flag;
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
-    if (PRE && !(skip & 1)) panel_preupdate(a, L, jb, ntile, b, sm);
+    if (PRE && !(skip & 1)) panel_preupdate<G3>(a, L, jb, ntile, b, sm);
     panel_factor_body<G3, DM>(a, L, NR, jb, ntile, b, skip, sm, dinv, flag);
 }
 
@@ -1282,6 +1283,7 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
 // [jb-32, jb), written back to R: the part of panel j's left-looking update that the
 // look-ahead step could not make in the previous launch (panel j-1 was being factored there).
 // Lp: PW * (PW + 1) LDS entries (panel j-1's rows jb .. jb+31, the shared B operand).
+template <bool G3>
 __device__ __forceinline__ void panel_preupdate(const MstepArgs& a, int L, int jb, int ntile, int b,
                                                 cd* Lp) {
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1304,11 +1306,12 @@ __device__ __forceinline__ void panel_preupdate(const MstepArgs& a, int L, int j
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2) av[s2] = arow[4 * s2];
         const int nv = tau == 0 ? 1 : 2;                         // tile 0's right half: upper triangle
-        d4v cre[2], cim[2];
+        d4v cre[2], cim[2], c2[2];
 #pragma unroll
         for (int v = 0; v < 2; ++v) {
             cre[v] = d4v{0.0, 0.0, 0.0, 0.0};
             cim[v] = d4v{0.0, 0.0, 0.0, 0.0};
+            c2[v] = d4v{0.0, 0.0, 0.0, 0.0};
             if (v < nv) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -1320,6 +1323,7 @@ __device__ __forceinline__ void panel_preupdate(const MstepArgs& a, int L, int j
                     }
                 }
             }
+            csub_init<G3>(cre[v], cim[v], c2[v]);
         }
 #pragma unroll 1
         for (int k0 = 0; k0 < PW; k0 += 16) {
@@ -1332,11 +1336,8 @@ __device__ __forceinline__ void panel_preupdate(const MstepArgs& a, int L, int j
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     if (h >= nv) break;                          // wave-uniform
-                    const cd t = Lp[(16 * h + li) * (PW + 1) + k0 + 4 * s2 + lk];
-                    cre[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre[h], 0, 0, 0);
-                    cre[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre[h], 0, 0, 0);
-                    cim[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim[h], 0, 0, 0);
-                    cim[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim[h], 0, 0, 0);
+                    // C -= A conj(B)^T (three real MFMAs per complex product with G3)
+                    csub_step<G3>(cre[h], cim[h], c2[h], v, Lp[(16 * h + li) * (PW + 1) + k0 + 4 * s2 + lk]);
                 }
             }
 #pragma unroll
@@ -1348,7 +1349,7 @@ __device__ __forceinline__ void panel_preupdate(const MstepArgs& a, int L, int j
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int rr = row0 + lk + 4 * q, c = 16 * v + li;
-                if (rr < L && c < w2) R[(size_t)rr * L + jb + c] = cmk(cre[v][q], cim[v][q]);
+                if (rr < L && c < w2) R[(size_t)rr * L + jb + c] = csub_out<G3>(cre[v], cim[v], c2[v], q);
             }
         }
     }
@@ -1391,7 +1392,7 @@ void panel_la_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int gptU, in
         return;
     }
     __builtin_amdgcn_s_setprio(2);                           // F before U; its chain wave first
-    if (jb > 0 && !(skip & 1)) panel_preupdate(a, L, jb, ntile, b, sm);
+    if (jb > 0 && !(skip & 1)) panel_preupdate<false>(a, L, jb, ntile, b, sm);
     panel_factor_body(a, L, NR, jb, ntile, b, skip, sm, dinv, flag);
 }
 

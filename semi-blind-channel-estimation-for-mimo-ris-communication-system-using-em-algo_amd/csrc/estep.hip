@@ -2244,7 +2244,11 @@ hipError_t dispatch_mfma_mode(const MfmaConst& c, size_t lds, long blocks, const
             c.prep_stride != 4 + 2 * NT * NR + 16 + 6 * NR)
             return hipErrorInvalidValue;
         if constexpr (NR <= 4) {
-            if (!g_debug.estep_occ2) {                // SBCE_ESTEP_OCC=2: no VGPR cap (A/B)
+            // the 168-VGPR build (3 waves/SIMD) for the wide iteration-0 posteriors, the uncapped
+            // one (206 VGPRs, no spills) otherwise: converged E-step 0.566 -> 0.539 ms, iteration 0
+            // 5.17 vs 5.58 ms (profiles/r04/estep_f32_ab_20db.log); SBCE_ESTEP_OCC=2/3 forces one
+            const bool capped = g_debug.estep_occ == '3' || (g_debug.estep_occ != '2' && a.wide);
+            if (capped) {
                 if (mode == SBCE_ESTEP_HARD)
                     hipLaunchKernelGGL((estep_mfma_kernel_occ3<NT, NR, SBCE_ESTEP_HARD, 4, true>),
                                        dim3((unsigned)blocks), dim3(64 * kMfmaWaves), lds, s, a, c);

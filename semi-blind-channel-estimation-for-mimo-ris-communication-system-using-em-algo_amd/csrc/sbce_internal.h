@@ -161,7 +161,8 @@ struct DebugConfig {
     int estep_spw;       // SBCE_ESTEP_SPW         symbols per sweep wave (default 4)
     bool estep_norowb;   // SBCE_ESTEP_ROWB=0      no row-tile bounds
     bool estep_nof32;    // SBCE_ESTEP_F32=0       no FP32 screen of the sweep's tile groups
-    bool estep_occ2;     // SBCE_ESTEP_OCC=2       sweep without the VGPR cap
+    char estep_occ;      // SBCE_ESTEP_OCC         0 auto (the 168-VGPR sweep at EM iteration 0 only),
+                         //                        '2' never, '3' always
     bool prep_nouni;     // SBCE_PREP_UNI=0
     bool estep_nosphere; // SBCE_ESTEP_SPHERE=0    tile sweep only
     int sphere_budget;   // SBCE_SPHERE_BUDGET     path list cap per level (default 128)
@@ -206,6 +207,9 @@ struct EstepArgs {
                        // symbols the enumeration left to the factorised-weight pass;
                        // null: no sphere
     double* tree;      // [B*Td][32] the sphere pass's per-symbol search-tree records
+    // launch hint: theta is the pilot-only theta_0 (EM iteration 0), whose wide posteriors make
+    // the sweep exp-path heavy -- it then runs the 168-VGPR (three waves per SIMD) build
+    int wide = 0;
 };
 constexpr int kTreeRecDoubles = 32;   // (word 31: the factorised-weight pass's screen)
 constexpr int kEstepListCnt = 16;      // int32 counters after the sweep's list
