@@ -1103,9 +1103,11 @@ constexpr int kFacXs = 0, kFacDiA = 4 * NB * NB, kFacDiB = kFacDiA + NB * NB, kF
 template <bool G3 = false>
 __device__ __forceinline__ void panel_preupdate(const MstepArgs& a, int L, int jb, int ntile, int b,
                                                 cd* Lp);
-template <bool G3 = false, int DM = 1>   // diagonal blocks: 0 row-recurrence inverse, 1 recursive doubling, 2 + two columns per step
+template <bool G3 = false, int DM = 1, bool CLK = false>   // DM (diagonal blocks): 0 row-recurrence inverse,
+                                                         // 1 recursive doubling, 2 + two columns per step
 __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int NR, int jb, int ntile,
-                                                  int b, int skip, cd* sm, double* dinv, int& flag) {
+                                                  int b, int skip, cd* sm, double* dinv, int& flag,
+                                                  unsigned long long t_start = 0) {
     // skip: DIAGNOSTIC phase mask (timing only, results invalid): 2 diag factors, 8 trsm tiles
     cd* DiA = sm + kFacDiA;
     cd* DiB = sm + kFacDiB;
@@ -1124,8 +1126,20 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
     cd* y = a.rhs + (size_t)b * L * NR;
     cd* X = Xs + wave * NB * NB;
     const bool trsm = !(skip & 8);
+    // DIAGNOSTIC (skip & 64, trial 0 only): per-phase s_memtime sums of waves 0 and 1 in
+    // g_chol_clk[16 + 8 wave + phase] (timing only; results unchanged)
+    const bool clk = CLK && b == 0 && wave < 2;
+    unsigned long long tclk = clk ? (t_start ? t_start : __builtin_amdgcn_s_memtime()) : 0;
+    auto stamp = [&](int ph) {
+        if (clk && lane == 0) {
+            const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+            g_chol_clk[16 + 8 * wave + ph] += t2 - tclk;
+            tclk = t2;
+        }
+    };
     if (tid == 0) flag = 0;
     __syncthreads();
+    stamp(0);
     cd xv[4];
     // waves 1-3: their first row tile (A part) and y rows are in flight while wave 0 factors
     cd cur[4];
@@ -1160,12 +1174,14 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
             X[e] = (rr < wA && c <= rr) ? R[(size_t)(jb + rr) * L + jb + c] : czero();
         }
         wave_sync();
+        stamp(1);
         if (!(skip & 2)) {
             factor_diag_lds<DM != 0, DM != 0, DM == 2>(X, wA, lane, tol, a.solve_mode, DiA, dinv, &flag,
                             R + (size_t)jb * L + jb, L);
             forward_y_lds(DiA, ybA, y + jb * NR, wA, NR, lane);
         }
         wave_sync();
+        stamp(2);
         if (ntile > 1 && trsm) {
 #pragma unroll
             for (int h = 0; h < 4; ++h) X[lane + 64 * h] = t1[h];
@@ -1176,8 +1192,10 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
             for (int q = 0; q < 4; ++q) XA1[li * NB + lk + 4 * q] = xv[q];
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // B's diagonal tile is in DiB
+        stamp(3);
     }
     __syncthreads();
+    stamp(4);
     if (wave == 0) {
         if (wB > 0) {
             // B's diagonal tile: C_B1 -= X_A1 X_A1^H, then factor
@@ -1241,7 +1259,9 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
             wave_sync();
         }
     }
+    stamp(5);
     __syncthreads();
+    stamp(6);
     if (wB > 0 && trsm) {
         // row tiles tau >= 2: TRSM of the updated B part against D_B
         int tau = 2 + wave;
@@ -1259,6 +1279,7 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
             wave_sync();
         }
     }
+    stamp(7);
     const int st = ((flag & 1) ? a.clamp_status : 0) | ((flag & 2) ? SBCE_STATUS_RANK : 0) |
                    ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
     if (tid == 0 && st && a.status) atomicOr(&a.status[b], st);
@@ -1266,7 +1287,7 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
 
 // PRE (wide schedule, odd panels): first the rank-32 update of the panel by the previous panel's
 // columns [jb-32, jb) (panel_preupdate: the part panel_update2_kernel left), then the factor.
-template <bool G3 = false, bool PRE = false, int DM = 1>
+template <bool G3 = false, bool PRE = false, int DM = 1, bool CLK = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip) {
     __shared__ __attribute__((aligned(16))) cd sm[kFacLds];
@@ -1274,8 +1295,9 @@ void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip
     __shared__ int flag;
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
+    const unsigned long long t0 = CLK ? __builtin_amdgcn_s_memtime() : 0;   // diagnostic
     if (PRE && !(skip & 1)) panel_preupdate<G3>(a, L, jb, ntile, b, sm);
-    panel_factor_body<G3, DM>(a, L, NR, jb, ntile, b, skip, sm, dinv, flag);
+    panel_factor_body<G3, DM, CLK>(a, L, NR, jb, ntile, b, skip, sm, dinv, flag, t0);
 }
 
 // ---------------------------------------------------------------- look-ahead panel step
@@ -1905,6 +1927,12 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
                                pb.NR, jb, rem, skip);
         else if (g3 && g_debug.chol_inv == 'p')
             hipLaunchKernelGGL((panel_factor_kernel<true, false, 2>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
+                               pb.NR, jb, rem, skip);
+        else if (g3 && pre && (skip & 64))         // DIAGNOSTIC phase clocks (tools/chol_clock.py)
+            hipLaunchKernelGGL((panel_factor_kernel<true, true, 1, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
+                               pb.NR, jb, rem, skip);
+        else if (g3 && (skip & 64))
+            hipLaunchKernelGGL((panel_factor_kernel<true, false, 1, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
                                pb.NR, jb, rem, skip);
         else if (g3 && pre)
             hipLaunchKernelGGL((panel_factor_kernel<true, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR,
