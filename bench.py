@@ -28,6 +28,7 @@ Also reported (one JSON line on rank 0):
                 same workload, on this host's cores (rank 0, N=1 only).
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -116,6 +117,21 @@ def minnorm_flops_per_trial(L, n_rx, act, refined):
     tri = 4.0 * n_rx * a * a
     return (32.0 * L * L + fac + gram + cfac + 2 * gmul + 4 * tri
             + refined * (4 * gmul + 4 * tri))
+
+
+def panel_factor_mfma_per_trial(L, pw=32, nb=16):
+    """FP64 MFMAs (16x16x4) one trial's panel_factor_kernel launches issue under the wide schedule
+    (csrc/chol.hip, three MFMAs per complex product): per 32-column panel with n 16-row tiles,
+    the TRSM against D_A of tiles 1.. (12 + 8 for the fused y update), the in-panel update of their
+    B parts (12), the TRSM against D_B of tiles 2.. (20), and for odd panels the rank-32
+    pre-update of every tile (2 halves x 8 k-steps x 3; tile 0 one half)."""
+    total = 0
+    for j in range((L + pw - 1) // pw):
+        n = (L - j * pw + nb - 1) // nb
+        total += max(n - 1, 0) * (20 + 12) + max(n - 2, 0) * 20
+        if j & 1:
+            total += max(n - 1, 0) * 48 + 24
+    return total
 
 
 def chol_bytes_per_trial(L, n_rx):
@@ -603,6 +619,20 @@ def main(argv=None):
         torch.cuda.synchronize()
         rb_ms = e0.elapsed_time(e1) / args.kernel_reps
 
+    # ---- the Cholesky's own launches by HIP events between them (sbce_debug_chol_timing) ----
+    chol_launch = None
+    if n_tx * (N + 1) <= 512 and solve == "chol":
+        fn = eng.lib.sbce_debug_chol_timing
+        fn.restype = ctypes.c_int
+        out6 = (ctypes.c_double * 6)()
+        torch.cuda.synchronize()
+        if fn(1, None) == 0:                     # 512 events: up to 18 M-steps at cfg1
+            for _ in range(min(args.kernel_reps, 16)):
+                eng.mstep()
+            torch.cuda.synchronize()
+            if fn(0, out6) == 0 and out6[4] > 0:
+                chol_launch = [v / min(args.kernel_reps, 16) for v in out6]
+
     # ---- the Cholesky solve alone: whole M-step minus its build (R and B^H, phase 2) ----
     build_ms = None
     if n_tx * (N + 1) <= 512 and solve == "chol":
@@ -683,6 +713,26 @@ def main(argv=None):
                      "traffic_ratio": c_traffic / cbytes if c_traffic else None,
                      "hbm_GBps_traffic": c_traffic / (c_ms * 1e-3) / 1e9 if c_traffic else None,
                      "frac_of_measured_pipe": c_ach / FP64_MFMA_MEASURED_TFLOPS}
+        if chol_launch:
+            # panel_factor_kernel's own line: its launches of one M-step (HIP events around each
+            # launch on the launch stream), priced at the MFMAs it issues (2048 flop each)
+            f_ms, f_n = chol_launch[1], chol_launch[4]
+            pflops = panel_factor_mfma_per_trial(L_) * 2048.0 * B
+            p_traffic = kernel_traffic(pmc, "panel_factor_kernel") if pmc_ok else None
+            p_ach = pflops / (f_ms * 1e-3) / 1e12
+            chol_roof["panel_factor"] = {
+                "kernel": "panel_factor_kernel", "bound": "mfma", "launches": f_n, "ms": f_ms,
+                "flops_per_mstep": pflops, "achieved": p_ach, "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": p_ach / FP64_PEAK_TFLOPS,
+                "frac_of_measured_pipe": p_ach / FP64_MFMA_MEASURED_TFLOPS,
+                "traffic_per_mstep": p_traffic * f_n if p_traffic else None,
+                "note": "MFMA work only; the two diagonal-block chains per launch are FP64 VALU / "
+                        "LDS latency (DESIGN section 3.5)"}
+            chol_roof["launch_ms"] = {"panel_update2": chol_launch[0], "panel_factor": f_ms,
+                                      "back_substitution": chol_launch[2],
+                                      "launches": {"panel_update2": chol_launch[3],
+                                                   "panel_factor": f_n,
+                                                   "back_substitution": chol_launch[5]}}
     if mode in ("soft", "hard"):
         flops = estep_flops_per_trial_iter(n_tx, n_rx, T_d, M) * B
         algo_bytes = estep_bytes_per_trial_iter(n_tx, n_rx, P, T_d) * B

@@ -379,6 +379,15 @@ int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int 
     return hip_rc(launch_chol_solve(pb, ma, s));
 }
 
+// Diagnostic, not part of include/sbce.h: HIP-event timing of the L <= 512 Cholesky's update /
+// factor / back-substitution launches (bench.py's panel_factor line).  mode 1 arms it for the
+// following M-steps; mode 0 (after the caller synchronised) returns {update, factor, back
+// substitution} ms and launch counts in out6 and disarms it.
+int sbce_debug_chol_timing(int mode, double* out6) {
+    clear_stale_error();
+    return hip_rc(chol_debug_timing(mode, out6));
+}
+
 // Diagnostic, not part of include/sbce.h: per-phase cycle sums (32) of the MFMA Cholesky
 // (SBCE_CHOL_SKIP bit 64); reset != 0 clears them.
 int sbce_debug_chol_clock(unsigned long long* out32, int reset) {

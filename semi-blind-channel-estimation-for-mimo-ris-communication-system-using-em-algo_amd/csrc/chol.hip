@@ -1862,6 +1862,22 @@ void backsub4_kernel(MstepArgs a, int L) {
     }
 }
 
+// DIAGNOSTIC launch timing (sbce_debug_chol_timing): HIP events around the wide schedule's
+// update / factor / back-substitution launches of the next M-step(s) on the launch stream
+struct CholTimer {
+    bool on = false, made = false;
+    int n = 0;
+    hipEvent_t ev[512];
+    int kind[256];
+};
+CholTimer g_ct;
+void ct_begin(hipStream_t s, int kind) {
+    if (g_ct.on && g_ct.n + 2 <= 512) { g_ct.kind[g_ct.n / 2] = kind; (void)hipEventRecord(g_ct.ev[g_ct.n++], s); }
+}
+void ct_end(hipStream_t s) {
+    if (g_ct.on && (g_ct.n & 1)) (void)hipEventRecord(g_ct.ev[g_ct.n++], s);
+}
+
 hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_t s) {
     const int skip = g_chol_skip;                   // diagnostic only (see kernels)
     hipError_t e = launch_diag_tol(pb, a, s);
@@ -1894,6 +1910,7 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
         const int rem = (pb.L - jb + NB - 1) / NB;
         const bool g3 = g_debug.cplx3 && a.solve_mode == SBCE_SOLVE_CHOL;
         if (j >= 2 && !(j & 1)) {
+            ct_begin(s, 0);
             const int gpt0 = (rem + 3) / 4;
             const int gpt1 = j + 1 < npan ? (rem - 2 + 3) / 4 : 0;
             const long nblk = 8L * ((pb.B + 7) / 8) * (gpt0 + gpt1);
@@ -1903,6 +1920,7 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
             else
                 hipLaunchKernelGGL(panel_update2_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L,
                                    jb, rem, gpt0, gpt1, skip);
+            ct_end(s);
         }
         const bool pre = (j & 1) != 0 && g_debug.chol_impl != 's';
         if ((j & 1) && !pre) {
@@ -1916,6 +1934,7 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
                                    jb, rem, gpt, skip);
         }
         // SBCE_CHOL_INV=loop: the row-recurrence inverse, =pair: two columns per step (A/B)
+        ct_begin(s, 1);
         if (g3 && pre && g_debug.chol_inv == 'l')
             hipLaunchKernelGGL((panel_factor_kernel<true, true, 0>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
                                pb.NR, jb, rem, skip);
@@ -1946,6 +1965,7 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
         else
             hipLaunchKernelGGL((panel_factor_kernel<false, false>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
                                pb.NR, jb, rem, skip);
+        ct_end(s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     for (int j = 0; j < npan && !lookahead && !wide; ++j) {
@@ -1993,11 +2013,12 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
     const int bsv = g_debug.backsub;
     if (pb.L <= 272 && pb.NR <= 4 && bsv == 0 && !(skip & 16)) {
         switch (pb.NR) {
-            case 1: hipLaunchKernelGGL(backsub4_kernel<1>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
-            case 2: hipLaunchKernelGGL(backsub4_kernel<2>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
-            case 3: hipLaunchKernelGGL(backsub4_kernel<3>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
-            default: hipLaunchKernelGGL(backsub4_kernel<4>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+            case 1: ct_begin(s, 2); hipLaunchKernelGGL(backsub4_kernel<1>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+            case 2: ct_begin(s, 2); hipLaunchKernelGGL(backsub4_kernel<2>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+            case 3: ct_begin(s, 2); hipLaunchKernelGGL(backsub4_kernel<3>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+            default: ct_begin(s, 2); hipLaunchKernelGGL(backsub4_kernel<4>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
         }
+        ct_end(s);
         return hipGetLastError();
     }
     if (pb.L <= 272 && pb.NR <= 4 && bsv == 3 && !(skip & 16)) {
@@ -2075,6 +2096,33 @@ hipError_t launch_mfma(const Problem& pb, const MstepArgs& a, size_t ybytes, hip
 }
 
 }  // namespace
+
+// mode 1: time the launches of the following M-steps (events created once); mode 0: after the
+// caller synchronised, out6 = {update ms, factor ms, back substitution ms, and their launch
+// counts}, then timing is switched off
+hipError_t chol_debug_timing(int mode, double* out6) {
+    if (mode == 1) {
+        if (!g_ct.made) {
+            for (int i = 0; i < 512; ++i)
+                if (hipEventCreate(&g_ct.ev[i]) != hipSuccess) return hipErrorInvalidValue;
+            g_ct.made = true;
+        }
+        g_ct.n = 0;
+        g_ct.on = true;
+        return hipSuccess;
+    }
+    g_ct.on = false;
+    if (!out6) return hipErrorInvalidValue;
+    for (int k = 0; k < 6; ++k) out6[k] = 0.0;
+    for (int i = 0; i + 1 < g_ct.n; i += 2) {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, g_ct.ev[i], g_ct.ev[i + 1]) != hipSuccess) return hipErrorInvalidValue;
+        const int k = g_ct.kind[i / 2];
+        out6[k] += ms;
+        out6[3 + k] += 1.0;
+    }
+    return hipSuccess;
+}
 
 hipError_t chol_debug_clock(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chol_clk), sizeof(g_chol_clk), 0,

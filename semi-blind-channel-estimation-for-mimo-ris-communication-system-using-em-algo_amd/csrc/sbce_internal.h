@@ -275,7 +275,8 @@ hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t 
 bool chol_supported(const Problem& pb);
 constexpr int kLargeL = 512;   // L above this: tiled build + blocked right-looking Cholesky
 constexpr int kMaxL = 8192;    // largest supported L (R alone is 1 GiB per trial there)
-bool rbuild_herm_supported(const Problem& pb);   // MFMA build of the Hermitian R: NT in {4, 8}
+bool rbuild_herm_supported(const Problem& pb);
+hipError_t chol_debug_timing(int mode, double* out6);   // MFMA build of the Hermitian R: NT in {4, 8}
 hipError_t launch_pilot_factor(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_rbuild_herm(const Problem& pb, const MstepArgs& a, hipStream_t s);
 hipError_t launch_chol_large(const Problem& pb, const MstepArgs& a, hipStream_t s);
