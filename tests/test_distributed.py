@@ -198,3 +198,15 @@ def test_bench_reference_structured_work_model_follows_estep():
     assert b.hypotheses_per_symbol("pm_soft", 8, 16, 1) == 16        # cfg2: p = int(1/4) = 0
     assert b.hypotheses_per_symbol("pm", 4, 4, 2) == 16              # p = int(2/2) = 1
     assert b.host_threads() >= 1
+
+
+def test_bench_panel_factor_work_model():
+    """bench.panel_factor_mfma_per_trial counts the FP64 MFMAs the wide schedule's factor launches
+    issue (csrc/chol.hip): cfg1's L = 260 gives 5216 per trial; one 32-column panel of 2 tiles
+    has TRSM A + B-part update of tile 1 only (32), no TRSM B and no pre-update."""
+    b = _bench()
+    assert b.panel_factor_mfma_per_trial(260) == 5216
+    assert b.panel_factor_mfma_per_trial(32) == 32
+    # L = 48: panel 0 has 3 tiles (TRSM A + update of tiles 1, 2: 64; TRSM B of tile 2: 20);
+    # panel 1 (odd, one tile) only its rank-32 pre-update of tile 0's lower half (24)
+    assert b.panel_factor_mfma_per_trial(48) == 64 + 20 + 24
