@@ -42,7 +42,7 @@ void read_debug_env(DebugConfig& c) {
     if ((v = env("SBCE_RB_TC"))) c.rb_tc32 = v[0] == '3';
     if ((v = env("SBCE_UPD_WAVES"))) c.upd_waves8 = v[0] == '8';
     if ((v = env("SBCE_BACKSUB"))) c.backsub = (v[0] >= '1' && v[0] <= '3') ? v[0] - '0' : 0;
-    if ((v = env("SBCE_CHOL_IMPL"))) c.chol_impl = (v[0] == 'v' || v[0] == 'f' || v[0] == 'u' || v[0] == 'l' || v[0] == 'n' || v[0] == 's') ? v[0] : 0;
+    if ((v = env("SBCE_CHOL_IMPL"))) c.chol_impl = (v[0] == 'v' || v[0] == 'f' || v[0] == 'u' || v[0] == 'l' || v[0] == 'n' || v[0] == 's' || v[0] == 'o') ? v[0] : 0;
     if ((v = env("SBCE_ESTEP_PAIR"))) c.estep_nopair = v[0] == '0';
     if ((v = env("SBCE_CPLX3"))) c.cplx3 = v[0] != '0';
 }

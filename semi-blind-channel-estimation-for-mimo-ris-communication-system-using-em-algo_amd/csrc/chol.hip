@@ -1089,6 +1089,87 @@ __device__ __forceinline__ void load_ycomp(const cd* y, int L, int NR, int row0,
     }
 }
 
+// Lp layouts of the previous panel's top rows (the shared B operand, 32 x 32): SW false padded
+// rows of PW + 1 entries; SW true unpadded (exactly the Xs scratch of the factor body) with
+// the column index XOR-swizzled by c & 15, so the 16 rows a k-step reads fall in distinct banks
+template <bool SW>
+__device__ __forceinline__ int lp_idx(int c, int k) {
+    return SW ? c * PW + (k ^ (c & 15)) : c * (PW + 1) + k;
+}
+
+template <bool SW>
+__device__ __forceinline__ void preupdate_stage(const cd* R, int L, int jb, int w2, cd* Lp) {
+    for (int e = threadIdx.x; e < PW * PW; e += 256) {
+        const int c = e >> 5, k = e & (PW - 1);
+        Lp[lp_idx<SW>(c, k)] = c < w2 ? R[(size_t)(jb + c) * L + jb - PW + k] : czero();
+    }
+}
+
+// one wave: row tiles tau = tau0, tau0 + dt, ... < ntile of panel [jb, jb+32) -= (their columns
+// [jb-32, jb)) Lp^H  (tau0, dt wave-uniform)
+template <bool G3, bool SW>
+__device__ __forceinline__ void preupdate_tiles(cd* R, int L, int jb, int w2, int tau0, int dt, int ntile,
+                                                const cd* Lp, int li, int lk) {
+    const int k0c = jb - PW;
+#pragma unroll 1
+    for (int tau = tau0; tau < ntile; tau += dt) {
+        const int row0 = jb + tau * NB;
+        int r = row0 + li;
+        r = r < L ? r : L - 1;                                   // rows past L: harmless reads
+        const cd* arow = R + (size_t)r * L + k0c + lk;
+        cd av[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) av[s2] = arow[4 * s2];
+        const int nv = tau == 0 ? 1 : 2;                         // tile 0's right half: upper triangle
+        d4v cre[2], cim[2], c2[2];
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            cre[v] = d4v{0.0, 0.0, 0.0, 0.0};
+            cim[v] = d4v{0.0, 0.0, 0.0, 0.0};
+            c2[v] = d4v{0.0, 0.0, 0.0, 0.0};
+            if (v < nv) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int rr = row0 + lk + 4 * q, c = 16 * v + li;
+                    if (rr < L && c < w2) {
+                        const cd x = R[(size_t)rr * L + jb + c];
+                        cre[v][q] = x.x;
+                        cim[v][q] = x.y;
+                    }
+                }
+            }
+            csub_init<G3>(cre[v], cim[v], c2[v]);
+        }
+#pragma unroll 1
+        for (int k0 = 0; k0 < PW; k0 += 16) {
+            cd an[4];
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) an[s2] = k0 == 0 ? arow[16 + 4 * s2] : czero();
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const cd v = av[s2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if (h >= nv) break;                          // wave-uniform
+                    // C -= A conj(B)^T (three real MFMAs per complex product with G3)
+                    csub_step<G3>(cre[h], cim[h], c2[h], v, Lp[lp_idx<SW>(16 * h + li, k0 + 4 * s2 + lk)]);
+                }
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) av[s2] = an[s2];
+        }
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            if (v >= nv) break;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rr = row0 + lk + 4 * q, c = 16 * v + li;
+                if (rr < L && c < w2) R[(size_t)rr * L + jb + c] = csub_out<G3>(cre[v], cim[v], c2[v], q);
+            }
+        }
+    }
+}
+
 // panel_factor_kernel: one workgroup (4 waves) per trial, panel [jb, jb+32) as sub-panels
 // A = [jb, jb+16) and B = [jb+16, jb+32):
 //   wave 0: factor A's diagonal tile (factor_diag_lds), D_A^-1 y_A, TRSM of row tile 1
@@ -1100,11 +1181,14 @@ __device__ __forceinline__ void load_ycomp(const cd* y, int L, int NR, int row0,
 // LDS of the factor body (cd entries): Xs (4 waves' 16 x 16 scratch), DiA, DiB, XA1, ybA, ybB
 constexpr int kFacXs = 0, kFacDiA = 4 * NB * NB, kFacDiB = kFacDiA + NB * NB, kFacXA1 = kFacDiB + NB * NB,
               kFacYbA = kFacXA1 + NB * NB, kFacYbB = kFacYbA + NB * 8, kFacLds = kFacYbB + NB * 8;
+// overlapped pre-update (OV): wave 0's chain scratch moves past the body's LDS, so the Xs
+// region can hold the previous panel's rows (swizzled Lp) while waves 1-3 pre-update
+constexpr int kFacX0 = kFacLds, kFacLdsOv = kFacLds + NB * NB;
 template <bool G3 = false>
 __device__ __forceinline__ void panel_preupdate(const MstepArgs& a, int L, int jb, int ntile, int b,
                                                 cd* Lp);
-template <bool G3 = false, int DM = 1, bool CLK = false>   // DM (diagonal blocks): 0 row-recurrence inverse,
-                                                         // 1 recursive doubling, 2 + two columns per step
+template <bool G3 = false, int DM = 1, bool CLK = false,  // DM (diagonal blocks): 0 row-recurrence inverse,
+          bool OV = false>                               // 1 recursive doubling, 2 + two columns per step
 __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int NR, int jb, int ntile,
                                                   int b, int skip, cd* sm, double* dinv, int& flag,
                                                   unsigned long long t_start = 0) {
@@ -1124,7 +1208,7 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
     const double tol = a.tol[b];
     cd* R = a.R + (size_t)b * L * L;
     cd* y = a.rhs + (size_t)b * L * NR;
-    cd* X = Xs + wave * NB * NB;
+    cd* X = (OV && wave == 0) ? sm + kFacX0 : Xs + wave * NB * NB;
     const bool trsm = !(skip & 8);
     // DIAGNOSTIC (skip & 64, trial 0 only): per-phase s_memtime sums of waves 0 and 1 in
     // g_chol_clk[16 + 8 wave + phase] (timing only; results unchanged)
@@ -1140,6 +1224,13 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
     if (tid == 0) flag = 0;
     __syncthreads();
     stamp(0);
+    if (OV && wave != 0 && !(skip & 1)) {
+        // the rest of the pre-update (tiles 0-3 are done) beside wave 0's chain: wave w takes
+        // the tiles tau >= 4 it TRSMs against D_A below (tau = 1 + w mod 3), so its own loads
+        // of them need no barrier; Lp (swizzled, in Xs) stays intact until the next barrier
+        preupdate_tiles<G3, true>(R, L, jb, w2, wave == 3 ? 4 : wave + 4, 3, ntile, sm + kFacXs, li, lk);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // own stores before own reloads
+    }
     cd xv[4];
     // waves 1-3: their first row tile (A part) and y rows are in flight while wave 0 factors
     cd cur[4];
@@ -1285,19 +1376,33 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
     if (tid == 0 && st && a.status) atomicOr(&a.status[b], st);
 }
 
-// PRE (wide schedule, odd panels): first the rank-32 update of the panel by the previous panel's
-// columns [jb-32, jb) (panel_preupdate: the part panel_update2_kernel left), then the factor.
-template <bool G3 = false, bool PRE = false, int DM = 1, bool CLK = false>
+// PRE (wide schedule, odd panels): the rank-32 update of the panel by the previous panel's
+// columns [jb-32, jb) (the part panel_update2_kernel left) inside the factor launch.
+// PRE 1: all of it first (panel_preupdate), then the factor.  PRE 2 (overlapped): each wave
+// pre-updates row tile `wave` (tiles 0 and 1 are the chain's), then wave 0 starts the diagonal
+// chain while waves 1-3 pre-update the remaining tiles (panel_factor_body<OV>): the chain is
+// VALU/LDS-latency bound, the pre-update MFMA bound, so the two share the CU's time.
+template <bool G3 = false, int PRE = 0, int DM = 1, bool CLK = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip) {
-    __shared__ __attribute__((aligned(16))) cd sm[kFacLds];
+    __shared__ __attribute__((aligned(16))) cd sm[PRE == 2 ? kFacLdsOv : kFacLds];
     __shared__ double dinv[NB];
     __shared__ int flag;
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
     const unsigned long long t0 = CLK ? __builtin_amdgcn_s_memtime() : 0;   // diagnostic
-    if (PRE && !(skip & 1)) panel_preupdate<G3>(a, L, jb, ntile, b, sm);
-    panel_factor_body<G3, DM, CLK>(a, L, NR, jb, ntile, b, skip, sm, dinv, flag, t0);
+    if (PRE == 1 && !(skip & 1)) panel_preupdate<G3>(a, L, jb, ntile, b, sm);
+    if (PRE == 2 && !(skip & 1)) {
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+        const int w2 = (L - jb) < PW ? (L - jb) : PW;
+        cd* R = a.R + (size_t)b * L * L;
+        preupdate_stage<true>(R, L, jb, w2, sm + kFacXs);
+        __syncthreads();
+        preupdate_tiles<G3, true>(R, L, jb, w2, wave, 4, wave + 1 < ntile ? wave + 1 : ntile, sm + kFacXs,
+                                  lane & 15, lane >> 4);
+        // the body's first barrier publishes tiles 0-3
+    }
+    panel_factor_body<G3, DM, CLK, PRE == 2>(a, L, NR, jb, ntile, b, skip, sm, dinv, flag, t0);
 }
 
 // ---------------------------------------------------------------- look-ahead panel step
@@ -1904,7 +2009,7 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
     // +1.8 % at three streams).  SBCE_CHOL_IMPL=n: one update launch per 32-column panel;
     // SBCE_CHOL_IMPL=s: the odd pre-update as a launch of its own (panel_preupd_kernel; measured
     // M-step 2.32 vs 2.30 ms in-factor) -- both A/B only.
-    const bool wide = g_debug.chol_impl == 0 || g_debug.chol_impl == 's';
+    const bool wide = g_debug.chol_impl == 0 || g_debug.chol_impl == 's' || g_debug.chol_impl == 'o';
     for (int j = 0; j < npan && wide; ++j) {
         const int jb = j * PW;
         const int rem = (pb.L - jb + NB - 1) / NB;
@@ -1953,6 +2058,9 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
         else if (g3 && (skip & 64))
             hipLaunchKernelGGL((panel_factor_kernel<true, false, 1, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
                                pb.NR, jb, rem, skip);
+        else if (g3 && pre && g_debug.chol_impl == 'o')
+            hipLaunchKernelGGL((panel_factor_kernel<true, 2>), dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR,
+                               jb, rem, skip);
         else if (g3 && pre)
             hipLaunchKernelGGL((panel_factor_kernel<true, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR,
                                jb, rem, skip);

@@ -173,7 +173,8 @@ struct DebugConfig {
     char chol_impl;      // SBCE_CHOL_IMPL         0 default (wide update schedule), 's' wide with the odd
                          //                        pre-update launched separately, 'n' one update launch per
                          //                        panel, 'l' look-ahead panel steps, 'v' VALU, 'f' fused
-                         //                        one-workgroup, 'u' unified panel update + factor launch
+                         //                        one-workgroup, 'u' unified panel update + factor launch,
+                         //                        'o' wide with the odd pre-update overlapping the chain
     char chol_inv;       // SBCE_CHOL_INV          0 default (recursive-doubling inverse), 'l' (loop) the
                          //                        16-step row recurrence, 'p' (pair) two columns per step
     bool estep_nopair;   // SBCE_ESTEP_PAIR=0      no factorised-weight pass (estep_pair.hip)

@@ -470,7 +470,8 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape):
     # panels' rank-32 pre-update as a launch of its own instead of inside their factor launch
     # "batched_il": the diagonal-block inverse by the 16-step row recurrence instead of the
     # recursive doubling (SBCE_CHOL_INV=loop)
-    for impl in ("batched", "narrow", "spre", "lookahead", "batched_c4", "fused", "valu",
+    # "overlap": the odd panels' pre-update beside the diagonal chain (SBCE_CHOL_IMPL=o)
+    for impl in ("batched", "narrow", "spre", "overlap", "lookahead", "batched_c4", "fused", "valu",
                  "batched_bs1", "batched_bs2", "batched_il", "batched_pair"):
         with sbce._lib.debug_env(SBCE_CHOL_IMPL=impl.split("_")[0],
                                  SBCE_BACKSUB=impl[-1] if "_bs" in impl else "0",
@@ -491,6 +492,7 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape):
             assert rel(out[impl][0][i], ref) < 1e-9, impl
     assert rel(th_m, out["narrow"][0]) < 1e-12
     assert rel(th_m, out["spre"][0]) < 1e-12
+    assert rel(th_m, out["overlap"][0]) < 1e-12
     assert rel(th_m, out["batched_il"][0]) < 1e-12
     assert rel(th_m, out["batched_pair"][0]) < 1e-12
     assert rel(th_m, out["lookahead"][0]) < 1e-12
