@@ -59,6 +59,16 @@ CONFIGS = {
 # solve, np.linalg.lstsq of PM.py:108 (include/sbce.h SBCE_SOLVE_MINNORM).
 ESTEP = {"cfg1": ("soft", 0, "chol"), "plumbing": ("soft", 0, "chol"),
          "cfg2": ("pm_soft", 1, "lstsq"), "cfg4": ("soft", 0, "lstsq")}
+# BASELINE configs[4]: the SNR x T_d grid of "Proposed method/all_detectorsvsTd.py" (constants
+# :345-363: 2x2, N_RIS = 15, T_p = 20, itera = 5, partition_r = 1; driver :371-405: its five EMs
+# per T_d point, each with the oracle early stop on the true h and the np.linalg.solve M-step),
+# 64-QAM, 20 SNR x 8 T_d points.  The reference sweeps T_d = 15..90 in steps of 15 (:346); the
+# grid's 8 points continue that list to 120.  SNR -> varn = power / 10^(SNR/10) with power = the
+# 64-QAM symbol energy 42 (SNR/all_Detectors.py:351-354 uses its constellation's power the same way).
+GRID = {"cfg5": dict(n_tx=2, n_rx=2, N=15, T_p=20, T_d=(15, 30, 45, 60, 75, 90, 105, 120),
+                     SNR=tuple(float(s) for s in range(-5, 35, 2)), M=64, trials=64, iters=5,
+                     power=42.0, partition_r=1,
+                     detectors=("pm_soft", "hard", "zf", "mmse", "soft"))}
 
 
 def metric_name(n_tx, N, T_p, T_d):
@@ -378,7 +388,11 @@ def parse_args(argv=None):
                          "ranks are started here; under torchrun it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="cfg1", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="cfg1", choices=sorted(CONFIGS) + sorted(GRID))
+    ap.add_argument("--grid-batch", choices=["point", "snr"], default="snr",
+                    help="cfg5: one sbce_em per (T_d, SNR, detector) ('point') or per (T_d, "
+                         "detector) with the SNR axis batched through per-trial noise variances "
+                         "('snr', default)")
     ap.add_argument("--trials", type=int, default=None, help="trials per GPU")
     ap.add_argument("--iters", type=int, default=None, help="EM iterations per step")
     ap.add_argument("--snr", type=float, default=20.0)
@@ -499,6 +513,145 @@ def selftest(args, ranks):
     ranks.close()
 
 
+def grid_cpu_baseline(g, seed, td=60, snr=15.0):
+    """cfg5 CPU baseline: the oracle restatements of the five EMs (oracle/em_reduced.py exact and
+    log-max, oracle/detectors.py ZF / MMSE, oracle/pm.py soft PM list) on ONE trial at one grid
+    point (T_d = 60, 15 dB), every EM for all `iters` iterations (no early stop): EM-iterations/s
+    of the five EMs together."""
+    import importlib
+    from oracle.em_reduced import em_reduced
+    from oracle.detectors import em_detector
+    from oracle.pm import em_pm
+    pkg = importlib.import_module(
+        "semi-blind-channel-estimation-for-mimo-ris-communication-system-using-em-algo_amd")
+    n_tx, n_rx = g["n_tx"], g["n_rx"]
+    varn = float(pkg.signal_model.snr_to_varn(snr, g["power"]))
+    b = pkg.signal_model.synthetic_batch(1, n_tx, n_rx, g["N"], g["T_p"], td, g["M"], varn,
+                                         seed=seed + 4242)
+    a = (b["y_d"][0], b["y_p"][0], b["u_p"][0], b["psi_d"][0].T)
+    aps = pkg.qam.all_possible_symbols(b["cons"], n_tx)
+    it = g["iters"]
+    t0 = time.perf_counter()
+    em_pm(*a, varn, it, b["theta0"][0], n_tx, n_rx, g["partition_r"], b["cons"], soft=True)
+    em_reduced(*a, aps, varn, it, b["theta0"][0], mode="hard")
+    for kind in ("zf", "mmse"):
+        em_detector(*a, aps, varn, it, b["theta0"][0], n_tx, n_rx, kind)
+    em_reduced(*a, aps, varn, it, b["theta0"][0])
+    dt = time.perf_counter() - t0
+    threads = os.environ.get("OMP_NUM_THREADS")
+    return {"value": 5 * it / dt, "unit": "EM-iterations/s", "cores": host_threads(), "kind": "port",
+            "sample": f"1 trial at T_d={td}, SNR {snr:g} dB: the five EMs (oracle/pm.py soft PM r=1, "
+                      f"oracle/em_reduced.py log-max and exact, oracle/detectors.py ZF and MMSE), "
+                      f"{it} iterations each without early stop (NumPy float64, BLAS "
+                      f"threads={threads or 'default'}), {dt:.2f} s"}
+
+
+def grid_main(args, ranks, pkg):
+    """--config cfg5: one step = the whole SNR x T_d grid, five detector EMs per point, `trials`
+    Monte-Carlo trials per point on every rank.  Calls are spread over 3 HIP streams.  value =
+    trial-iterations EXECUTED (the oracle early stop ends a trial's EM; iters_done) / time."""
+    import torch
+    g = dict(GRID[args.config])
+    if args.trials:
+        g["trials"] = args.trials
+    if args.iters:
+        g["iters"] = args.iters
+    world, rank = ranks.world, ranks.rank
+    n_tx, n_rx, N, T_p, M, B, iters = (g[k] for k in ("n_tx", "n_rx", "N", "T_p", "M", "trials",
+                                                        "iters"))
+    T_D, SNR, dets = g["T_d"], g["SNR"], g["detectors"]
+    varns = [float(v) for v in pkg.signal_model.snr_to_varn(SNR, g["power"])]
+    ns, nt, nd = len(SNR), len(T_D), len(dets)
+    engines = []                     # (detector index, T_d index, SNR indices, engine)
+    for k, td in enumerate(T_D):
+        pts = [pkg.signal_model.synthetic_batch(B, n_tx, n_rx, N, T_p, td, M, vn,
+                                                seed=(args.seed * 1000003 + rank) * 1000 + k * 50 + j)
+               for j, vn in enumerate(varns)]
+        if args.grid_batch == "snr":
+            groups = [(list(range(ns)), {key: np.concatenate([p[key] for p in pts])
+                                         for key in ("y_d", "y_p", "psi_d", "u_p", "theta0", "h")},
+                       np.repeat(np.asarray(varns), B))]
+        else:
+            groups = [([j], pts[j], varns[j]) for j in range(ns)]
+        for js, batch, vn in groups:
+            batch = dict(batch, cons=pts[0]["cons"])
+            for di, det in enumerate(dets):
+                eng = pkg.EMEngine(batch, vn, mode=det, solve="chol", early_stop=True,
+                                   partition_r=g["partition_r"] if det == "pm_soft" else 0)
+                engines.append((di, k, js, eng))
+        del pts
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    cur = torch.cuda.current_stream()
+
+    def step():
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        for st in streams:
+            st.wait_event(ev)
+        for i, (_, _, _, eng) in enumerate(engines):
+            eng.run(iters, stream=streams[i % len(streams)])
+        for st in streams:
+            cur.wait_stream(st)
+
+    for _ in range(args.warmup):
+        step()
+    ranks.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    ranks.barrier()
+    elapsed = ranks.max_time(time.perf_counter() - t0)
+
+    # executed trial-iterations of one step (every step repeats the same EMs from theta_0)
+    done = torch.stack([eng.iters_done.sum() for _, _, _, eng in engines]).sum().to(torch.float64)
+    nominal = float(B * iters * ns * nt * nd)
+    # the one collective: [sum NMSE, count] of every (detector, T_d, SNR) point + executed its
+    acc = torch.zeros(nd * nt * ns * 2 + 1, dtype=torch.float64, device="cuda")
+    for di, k, js, eng in engines:
+        nm = eng.nmse().view(len(js), B)
+        for jj, j in enumerate(js):
+            base = ((di * nt + k) * ns + j) * 2
+            acc[base] += nm[jj].sum()
+            acc[base + 1] += B
+    acc[-1] = done
+    ranks.allreduce_sum(acc)
+    a = acc[:-1].view(nd, nt, ns, 2).cpu().numpy()
+    mean = a[..., 0] / a[..., 1]
+    executed = float(acc[-1].item())
+    flagged = sum(int((eng.status != 0).sum().item()) for _, _, _, eng in engines)
+    line = {
+        "metric": metric_name(n_tx, N, T_p, f"{T_D[0]}..{T_D[-1]}") + " (SNR x T_d grid, five EMs)",
+        "value": executed * args.steps / elapsed,
+        "unit": "EM-iterations/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (Rayleigh channels, 64-QAM, uniform RIS phases, CN noise; numpy Generator)",
+        "config": {"workload": args.config, "n_tx": n_tx, "n_rx": n_rx, "N_RIS": N, "T_p": T_p,
+                   "T_d": list(T_D), "snr_db": list(SNR), "snr_power": g["power"], "M": M,
+                   "trials_per_point_per_gpu": B, "em_iters": iters, "detectors": list(dets),
+                   "partition_r": g["partition_r"], "solve": "chol", "early_stop": "oracle (h)",
+                   "grid_batch": args.grid_batch, "sbce_em_calls_per_step": len(engines),
+                   "streams_per_gpu": len(streams), "parallelism": f"trials-sharded x{world}"},
+        "value_note": ("value counts the trial-iterations the EMs executed (each EM stops at the "
+                       "reference's oracle criterion, all_detectorsvsTd.py:87-89 etc.); "
+                       f"nominal {nominal * world:.0f} per step (all {iters} iterations), executed "
+                       f"{executed:.0f}"),
+        "executed_iterations_per_step": executed,
+        "nominal_iterations_per_step": nominal * world,
+        "nmse_grid_mean": {det: float(np.mean(mean[di])) for di, det in enumerate(dets)},
+        "nmse_at_max_td": {det: [float(v) for v in mean[di, -1]] for di, det in enumerate(dets)},
+        "status_flagged_trials": flagged,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = grid_cpu_baseline(g, args.seed)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ranks.close()
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse_args(argv)
@@ -522,6 +675,8 @@ def main(argv=None):
     pkg = ge.package()
     ranks = Ranks(args, world_env)
     world, rank = ranks.world, ranks.rank
+    if args.config in GRID:
+        return grid_main(args, ranks, pkg)
 
     cfg = list(CONFIGS[args.config])
     if args.trials:

@@ -43,6 +43,7 @@
  *   status   [B] int32               per-trial flags (SBCE_STATUS_*)
  *   x_dest   [B][T_d][n_tx]          optional output: last-iteration decisions
  *   x_sup    [B][T_d][n_tx]          optional superimposed pilot symbols
+ *   varn_t   [B] float64             optional per-trial noise variances (ABI 6)
  */
 #ifndef SBCE_H_
 #define SBCE_H_
@@ -54,7 +55,7 @@
 extern "C" {
 #endif
 
-#define SBCE_ABI_VERSION 5
+#define SBCE_ABI_VERSION 6
 
 /* return codes */
 #define SBCE_OK 0
@@ -151,6 +152,12 @@ typedef struct sbce_ptrs {
     const void* x_sup;      /* may be NULL; SOFT/HARD only: [B][T_d][n_tx] pilot
                                symbols superimposed on the data, hypotheses x_j + x_sup[t]
                                (Parallel/ParallelProtocol_Tp.py:63-86; t_p is then 0) */
+    const double* varn_t;   /* may be NULL (ABI 6): [B] noise variance parameter of each trial,
+                               used instead of dims.varn (which must still be > 0) by the E-step
+                               posterior (varn^2) and the LLF.  Lets one call carry the trials of
+                               several SNR points of a sweep (all_detectorsvsTd.py's grid, SNR/
+                               all_Detectors.py:351-354): every trial's result is the one a call
+                               with dims.varn = varn_t[b] gives.  8-byte aligned, values > 0 */
 } sbce_ptrs;
 
 /* ABI version (SBCE_ABI_VERSION). */

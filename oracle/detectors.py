@@ -69,11 +69,15 @@ def detector_moments(theta, Y_d, Psi, aps, varn, n_tx, n_rx, kind, cons=None):
     return m, S
 
 
-def em_detector(Y_d, Y_p, U_p, Psi, aps, varn, itera, theta0, n_tx, n_rx, kind, h=None):
+def em_detector(Y_d, Y_p, U_p, Psi, aps, varn, itera, theta0, n_tx, n_rx, kind, h=None,
+                cons=None):
+    """aps=None with cons given: the decisions through ecul_index (the closed form of the flat
+    argmin, pinned to ecul_literal by tests/test_oracle.py) instead of the literal scan over the
+    M^n_tx rows -- the same rows, ~20x faster at 64-QAM."""
     from .em_reduced import mstep_build, mstep_solve
     theta = np.asarray(theta0, dtype=complex).reshape(-1)
     for l in range(itera):
-        m, S = detector_moments(theta, Y_d, Psi, aps, varn, n_tx, n_rx, kind)
+        m, S = detector_moments(theta, Y_d, Psi, aps, varn, n_tx, n_rx, kind, cons=cons)
         R, rhs = mstep_build(U_p, Y_p, Psi, Y_d, m, S)
         theta = mstep_solve(R, rhs)
         if h is not None and np.abs(norm(theta) - norm(h)) < 1 and l != 0:

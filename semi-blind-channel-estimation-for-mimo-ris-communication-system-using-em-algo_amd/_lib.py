@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsbce.so")
 
-SBCE_ABI_VERSION = 5
+SBCE_ABI_VERSION = 6
 SBCE_ESTEP_SOFT = 0
 SBCE_ESTEP_HARD = 1
 SBCE_ESTEP_PM = 2
@@ -55,7 +55,7 @@ class Ptrs(ctypes.Structure):
                 ("h_true", ctypes.c_void_p), ("iters_done", ctypes.c_void_p),
                 ("status", ctypes.c_void_p), ("workspace", ctypes.c_void_p),
                 ("workspace_bytes", ctypes.c_size_t), ("x_dest", ctypes.c_void_p),
-                ("x_sup", ctypes.c_void_p)]
+                ("x_sup", ctypes.c_void_p), ("varn_t", ctypes.c_void_p)]
 
 
 _lib = None

@@ -190,6 +190,7 @@ int check_ptrs(const sbce_ptrs* p, const Problem& pb, bool need_ws, int solve = 
     for (const void* q : req)
         if (!q || !aligned16(q)) return SBCE_EINVAL;
     if (pb.Tp == 0) { /* pilots optional */ }
+    if (p->varn_t && ((uintptr_t)p->varn_t & 7)) return SBCE_EINVAL;
     if (need_ws) {
         if (!p->workspace || !aligned16(p->workspace)) return SBCE_EINVAL;
         if (p->workspace_bytes < carve(pb, solve).total) return SBCE_EWORKSPACE;
@@ -264,6 +265,7 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     ea.yd = (const cd*)p->y_d; ea.psid = (const cd*)p->psi_d; ea.theta = (const cd*)p->theta;
     ea.cons = (const cd*)p->cons; ea.mom = (cd*)(ws + c.mom); ea.done = early ? done : nullptr;
     ea.status = p->status;
+    ea.varn_t = p->varn_t;
     ea.prep = c.has_prep ? (double*)(ws + c.prep) : nullptr;
     ea.list = c.has_prep ? (int32_t*)(ws + c.list) : nullptr;
     ea.tree = c.has_prep ? (double*)(ws + c.tree) : nullptr;
@@ -297,7 +299,8 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
         if ((rc = hip_rc(launch_chol_solve(pb, ma, s)))) return rc;
         if (p->llf &&
             (rc = hip_rc(launch_llf(pb, ma.theta, ma.yp, ma.up, ma.yd, ma.psid,
-                                    (const cd*)p->x_d_true, p->llf, iters, it, ea.done, s))))
+                                    (const cd*)p->x_d_true, p->llf, iters, it, ea.done, p->varn_t,
+                                    s))))
             return rc;
         if (early &&
             (rc = hip_rc(launch_early_stop(pb, ma.theta, (const cd*)p->h_true, done, p->iters_done,
@@ -330,6 +333,7 @@ int sbce_estep(const sbce_dims* d, const sbce_ptrs* p, int estep_mode, void* mom
     ea.yd = (const cd*)p->y_d; ea.psid = (const cd*)p->psi_d; ea.theta = (const cd*)p->theta;
     ea.cons = (const cd*)p->cons; ea.mom = (cd*)moments; ea.done = nullptr;
     ea.status = p->status;
+    ea.varn_t = p->varn_t;
     ea.prep = nullptr;               // workspace optional here: use it when it is large enough
     ea.list = nullptr;
     ea.tree = nullptr;

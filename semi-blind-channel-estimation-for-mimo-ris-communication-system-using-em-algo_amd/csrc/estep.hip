@@ -93,6 +93,11 @@ __global__ __launch_bounds__(256) void estep_kernel(EstepArgs a, EstepConst c) {
     const int b = (int)(gsym / c.Td);
     const int t = (int)(gsym - (long)b * c.Td);
     if (a.done && a.done[b]) valid = false;
+    if (a.varn_t) {                                  // per-trial noise variance (ABI 6)
+        const TrialNoise tn = trial_noise(a.varn_t[b]);
+        c.inv_s2 = tn.inv_s2;
+        c.thr_d = tn.thr_d;
+    }
 
     // ---------------- effective channel H_eff(t): heff[a*NR + r] --------------
     {
@@ -752,6 +757,14 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     const int b = (int)(gsym / c.Td);
     const int t = (int)(gsym - (long)b * c.Td);
     const int mask = k_M - 1;
+    // the trial's noise constants (per-trial variances, ABI 6): wave-uniform, kept in SGPRs
+    double thr_d = c.thr_d, inv_s2 = c.inv_s2, reg = c.reg;
+    if (a.varn_t) {
+        const TrialNoise tn = trial_noise(a.varn_t[b]);
+        thr_d = uniform_d(tn.thr_d);
+        inv_s2 = uniform_d(tn.inv_s2);
+        reg = uniform_d(tn.reg);
+    }
 
     // ---------------- H_eff(t) ----------------
     if (prep) {
@@ -777,14 +790,13 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     }
     const cd* H = prep ? reinterpret_cast<const cd*>(s_rec + 4) : s_heff;
     const double* lbp = prep ? s_rec + 4 + 2 * NO : s_lb;        // column-tile bounds
-    const double inv_s2 = c.inv_s2;
     double cscale_d, d0, lb_scale;
     if (prep) {                      // estep_prep_kernel did these per symbol
         d0 = s_rec[0];
         cscale_d = s_rec[1];
         lb_scale = s_rec[2];
     } else {
-        d0 = candidate_distance<NT, NR>(H, a.yd + (size_t)gsym * NR, s_cons, k_M, c.reg,
+        d0 = candidate_distance<NT, NR>(H, a.yd + (size_t)gsym * NR, s_cons, k_M, reg,
                                         reinterpret_cast<cd*>(s_tab), lane, cscale_d);
         lb_scale = column_tile_bounds<NT, NR>(H, a.yd + (size_t)gsym * NR, s_cons, k_M, k_lm,
                                               k_JB >> 4, s_lb, reinterpret_cast<cd*>(s_tab), lane);
@@ -917,7 +929,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     // now; the bound only falls during the sweep, so each is checked again when reached
     unsigned long long ktmask = ~0ull;
     if (nktile <= 64) {
-        const double lim0 = ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin;
+        const double lim0 = ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + thr_d) + lb_margin;
         ktmask = __ballot(lane < nktile && !(lbp[lane < nktile ? lane : 0] > lim0));
     }
     for (int kt = 0; kt < nktile; ++kt) {
@@ -927,7 +939,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
             kt += __builtin_ctzll(m);
         }
         // exact column-tile bound: wave-uniform skip of the whole tile
-        if (lbp[kt] > ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin)
+        if (lbp[kt] > ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + thr_d) + lb_margin)
             continue;
         unsigned rowmask = 0xffffu;
         if (rowb) {
@@ -937,7 +949,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                 const double* rk = s_rk + 3 * kt;
                 bnd = fma(cabs2(x0), s_tab[63], rk[0] - 2.0 * (x0.x * rk[1] + x0.y * rk[2]));
             }
-            const double lim = ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + c.thr_d) + lb_margin;
+            const double lim = ((MODE == SBCE_ESTEP_HARD) ? hard_bound : mshift + thr_d) + lb_margin;
             rowmask = (unsigned)__ballot(bnd <= lim);
             if (!rowmask) continue;                      // no row tile of this column survives
         }
@@ -1070,7 +1082,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
 #pragma unroll
                     for (int u = 1; u < TU; ++u)
                         m32 = fminf(m32, fminf(fminf(s32[u][0], s32[u][1]), fminf(s32[u][2], s32[u][3])));
-                    const double lim = ((MODE == SBCE_ESTEP_HARD) ? best_d : mshift + c.thr_d) - gam +
+                    const double lim = ((MODE == SBCE_ESTEP_HARD) ? best_d : mshift + thr_d) - gam +
                                        0x1p-17 * (2.0 * amax + gam);
                     ++scr_n;
                     const bool pass = __any((double)m32 <= lim);
@@ -1114,7 +1126,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                 // worse than this lane's best); the common case skips everything below
                 if (MODE == SBCE_ESTEP_HARD) {
                     if (!__any(cm + gam <= best_d)) continue;
-                } else if (!__any(cm + gam <= mshift + c.thr_d)) {
+                } else if (!__any(cm + gam <= mshift + thr_d)) {
                     continue;
                 }
                 if (MODE == SBCE_ESTEP_HARD) {
@@ -1158,13 +1170,13 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                         for (int j = 0; j < 4; ++j) { R1[j] *= f; Q[j] = cscale(Q[j], f); }
                     }
                 }
-                if (!__any(cm <= mshift + c.thr_d)) continue;
+                if (!__any(cm <= mshift + thr_d)) continue;
                 touched = true;
 #pragma unroll
                 for (int u = 0; u < TU; ++u) {
                     const double cmu =
                         fmin(fmin(acc[u][0], acc[u][1]), fmin(acc[u][2], acc[u][3])) + gam;
-                    if (!__any(cmu <= mshift + c.thr_d)) continue;
+                    if (!__any(cmu <= mshift + thr_d)) continue;
                     if constexpr (V16) {
                         const cd x0 = s_cons[tg + u];          // stream 0 of the tile (i0 = 0)
                         const double n0 = cabs2(x0);
@@ -1172,7 +1184,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                         for (int j = 0; j < 4; ++j) {
                             const double dj = acc[u][j] + gam;
                             // rows with no lane inside the bound: weights < e^-50 of the maximum
-                            if (!__any(dj <= mshift + c.thr_d)) continue;
+                            if (!__any(dj <= mshift + thr_d)) continue;
                             const double w = fexp_neg((mshift - dj) * inv_s2);
                             R1[j] += w;
                             Q[j] = caxpy(Q[j], w, x0);
@@ -1707,6 +1719,10 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
     if (gsym >= nsym) return;
     const int b = (int)(gsym / c.Td);
     if (a.done && a.done[b]) return;
+    if (a.varn_t) {                                  // per-trial noise variance (ABI 6)
+        const TrialNoise tn = trial_noise(a.varn_t[b]);
+        c.reg = tn.reg; c.thr_d = tn.thr_d; c.inv_s2 = tn.inv_s2;
+    }
     cd H[NT][NR];
     heff_load<NT, NR>(a, c, gsym, b, H);
     cd y[NR];
@@ -1786,6 +1802,10 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
     bool live = gsym < nsym;
     const int b = live ? (int)(gsym / c.Td) : 0;
     if (live && a.done && a.done[b]) live = false;
+    if (live && a.varn_t) {                          // per-trial noise variance (ABI 6)
+        const TrialNoise tn = trial_noise(a.varn_t[b]);
+        c.reg = tn.reg; c.thr_d = tn.thr_d; c.inv_s2 = tn.inv_s2;
+    }
     bool single = false;
     if (live) {
     cd Lm[NT][NT], zf[NT];
@@ -1998,7 +2018,6 @@ __global__ __launch_bounds__(64 * kBfsWaves) void estep_bfs_kernel(EstepArgs a, 
     __syncthreads();
     double cmax2 = 0.0;
     for (int s = 0; s < c.M; ++s) cmax2 = fmax(cmax2, s_c2[s]);
-    const double slack = c.reg * cmax2;                  // per level below: T_j >= -slack
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const long nsym = (long)c.B * c.Td;
@@ -2024,6 +2043,15 @@ __global__ __launch_bounds__(64 * kBfsWaves) void estep_bfs_kernel(EstepArgs a, 
     issue(g0, 0);
     for (long gi = g0; gi < g1; ++gi) {
         const long gsym = elist[gi];
+        // the symbol's noise constants (per-trial variances, ABI 6); per level below: T_j >= -slack
+        double thr_d = c.thr_d, inv_s2 = c.inv_s2, reg = c.reg;
+        if (a.varn_t) {
+            const TrialNoise tn = trial_noise(a.varn_t[gsym / c.Td]);
+            thr_d = uniform_d(tn.thr_d);
+            inv_s2 = uniform_d(tn.inv_s2);
+            reg = uniform_d(tn.reg);
+        }
+        const double slack = reg * cmax2;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this symbol's record landed
         wave_sync();
         const double* rec = s_rec[wave][(gi - g0) & 1];
@@ -2032,7 +2060,7 @@ __global__ __launch_bounds__(64 * kBfsWaves) void estep_bfs_kernel(EstepArgs a, 
         bool listed = !((packed >> 16) & 1);
         const double R0 = rec[1];
         const double margin = 1e-9 * rec[2];
-        const double R = R0 + (SPH == 2 ? 0.0 : c.thr_d) + margin;
+        const double R = R0 + (SPH == 2 ? 0.0 : thr_d) + margin;
         double ui[NT];
         cd zf[NT], Lc[NP + 1];
 #pragma unroll
@@ -2056,7 +2084,7 @@ __global__ __launch_bounds__(64 * kBfsWaves) void estep_bfs_kernel(EstepArgs a, 
             double* pbo = s_pb[wave][ib ^ 1];
             int* pio = s_pi[wave][ib ^ 1];
             const double u = ui[l];
-            const double aa = fma(u, u, -c.reg), m2u = -2.0 * u;
+            const double aa = fma(u, u, -reg), m2u = -2.0 * u;
             const double lim = R + l * slack;
             const int total = n_in << lm;
             int n_out = 0;
@@ -2129,7 +2157,7 @@ __global__ __launch_bounds__(64 * kBfsWaves) void estep_bfs_kernel(EstepArgs a, 
                 double* lw = s_pb[wave][ib ^ 1];
                 for (int k = lane; k < n_in; k += 64) {
                     const double d = lb[k];
-                    lw[k] = d <= dmin + c.thr_d ? fexp_neg((dmin - d) * c.inv_s2) : 0.0;
+                    lw[k] = d <= dmin + thr_d ? fexp_neg((dmin - d) * inv_s2) : 0.0;
                 }
                 wave_sync();
                 if (lane < MS) {

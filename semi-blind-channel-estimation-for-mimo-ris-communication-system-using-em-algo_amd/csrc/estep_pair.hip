@@ -108,7 +108,7 @@ __global__ __launch_bounds__(64 * kPairWaves) __attribute__((amdgpu_waves_per_eu
         // ---- the six log tables, one at a time through LDS (few live registers): raw log
         //      values, their maxima, then the exponentials (A, E13, E03 into the registers of
         //      the MFMA operands / accumulator rows, B, E12, E02 back into LDS) ----
-        const double is2 = c.inv_s2;
+        const double is2 = a.varn_t ? uniform_d(trial_noise(a.varn_t[b]).inv_s2) : c.inv_s2;
         double yy = 0.0;
         cd G02 = czero(), G03 = czero(), G12 = czero(), G13 = czero();
 #pragma unroll

@@ -108,6 +108,11 @@ __global__ __launch_bounds__(64 * kPmWaves) void estep_pm_kernel(EstepArgs a, Pm
     if (gsym >= nsym) return;
     const int b = (int)(gsym / c.Td);
     if (a.done && a.done[b]) return;
+    if (a.varn_t) {                                  // per-trial noise variance (ABI 6)
+        const TrialNoise tn = trial_noise(a.varn_t[b]);
+        c.inv_s2 = uniform_d(tn.inv_s2);
+        c.s2 = uniform_d(tn.s2);
+    }
     const int NT = c.NT, NR = c.NR, NO = NT * NR, P = c.P, mask = c.M - 1;
 
     // ---- 1. H_true, H_off (lane = output a*NR + r), y ----

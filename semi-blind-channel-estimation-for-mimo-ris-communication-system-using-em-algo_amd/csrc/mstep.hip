@@ -446,10 +446,11 @@ __global__ __launch_bounds__(256) void llf_kernel(const cd* theta, const cd* yp,
                                                   const cd* yd, const cd* psid, const cd* xd,
                                                   double* llf, const int32_t* done, int P, int NT,
                                                   int NR, int Tp, int Td, int M, double varn,
-                                                  int iters, int it) {
+                                                  const double* varn_t, int iters, int it) {
     __shared__ double sh[4];
     const int b = blockIdx.x;
     if (done && done[b]) return;
+    if (varn_t) varn = varn_t[b];                    // per-trial noise variance (ABI 6)
     const int L = P * NT;
     const cd* th = theta + (size_t)b * L * NR;
     double sp = 0.0, sd = 0.0;
@@ -615,9 +616,9 @@ hipError_t launch_ser(const Problem& pb, const cd* xdest, const cd* xtrue, doubl
 
 hipError_t launch_llf(const Problem& pb, const cd* theta, const cd* yp, const cd* up, const cd* yd,
                       const cd* psid, const cd* xd, double* llf, int iters, int it,
-                      const int32_t* done, hipStream_t s) {
+                      const int32_t* done, const double* varn_t, hipStream_t s) {
     hipLaunchKernelGGL(llf_kernel, dim3(pb.B), dim3(256), 0, s, theta, yp, up, yd, psid, xd, llf, done,
-                       pb.P, pb.NT, pb.NR, pb.Tp, pb.Td, pb.M, pb.varn, iters, it);
+                       pb.P, pb.NT, pb.NR, pb.Tp, pb.Td, pb.M, pb.varn, varn_t, iters, it);
     return hipGetLastError();
 }
 

@@ -116,6 +116,11 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 __device__ __forceinline__ double shfl_xor_d(double v, int m) { return __shfl_xor(v, m); }
+// a wave-uniform double moved to SGPRs (readfirstlane of both halves)
+__device__ __forceinline__ double uniform_d(double v) {
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
 // ds_bpermute of a double from the lane whose byte address (4 * lane) is `addr`; with the
 // address computed once, a butterfly step costs no VALU beyond the combine
 __device__ __forceinline__ double bperm_d(double v, int addr) {
@@ -211,7 +216,23 @@ struct EstepArgs {
     // launch hint: theta is the pilot-only theta_0 (EM iteration 0), whose wide posteriors make
     // the sweep exp-path heavy -- it then runs the 168-VGPR (three waves per SIMD) build
     int wide = 0;
+    const double* varn_t = nullptr;   // [B] per-trial noise variances (sbce_ptrs.varn_t), or null
 };
+
+// The posterior constants of one noise variance v, in the operation order of the host's scalar
+// path (the launchers' 1 / (varn varn), kSkipThr varn varn, 0.1 varn varn), so that a trial with
+// varn_t[b] == dims.varn gets bitwise the constants of a scalar call.  kSkipThr = 50 (estep.hip).
+struct TrialNoise {
+    double inv_s2, thr_d, reg, s2;
+};
+__device__ __forceinline__ TrialNoise trial_noise(double v) {
+    TrialNoise n;
+    n.inv_s2 = 1.0 / (v * v);
+    n.thr_d = 50.0 * v * v;
+    n.reg = 0.1 * v * v;
+    n.s2 = v * v;
+    return n;
+}
 constexpr int kTreeRecDoubles = 32;   // (word 31: the factorised-weight pass's screen)
 constexpr int kEstepListCnt = 16;      // int32 counters after the sweep's list
 // the factorised-weight pass (estep_pair.hip) takes a symbol whose range D is at most this
@@ -323,7 +344,7 @@ hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* 
                        hipStream_t s);
 hipError_t launch_llf(const Problem& pb, const cd* theta, const cd* yp, const cd* up,
                       const cd* yd, const cd* psid, const cd* xd, double* llf, int iters,
-                      int it, const int32_t* done, hipStream_t s);
+                      int it, const int32_t* done, const double* varn_t, hipStream_t s);
 hipError_t launch_early_stop(const Problem& pb, const cd* theta, const cd* h,
                              int32_t* done, int32_t* iters_done, int it, hipStream_t s);
 

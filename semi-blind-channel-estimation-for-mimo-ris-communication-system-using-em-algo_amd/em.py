@@ -65,6 +65,22 @@ _SOLVES = {"chol": _lib.SBCE_SOLVE_CHOL, "drop": _lib.SBCE_SOLVE_CHOL_DROP,
            "lstsq": _lib.SBCE_SOLVE_MINNORM}
 
 
+def _varn_arg(torch, varn, B):
+    """(dims.varn, per-trial device tensor or None) for a scalar or (B,) noise variance."""
+    if np.ndim(varn) == 0 and not (isinstance(varn, torch.Tensor) and varn.dim() > 0):
+        v = float(varn)
+        if not v > 0:
+            raise ValueError("varn must be > 0")
+        return v, None
+    v = np.ascontiguousarray(varn.cpu().numpy() if isinstance(varn, torch.Tensor) else varn,
+                             dtype=np.float64).reshape(-1)
+    if v.size != B:
+        raise ValueError(f"per-trial varn has {v.size} entries, batch is {B}")
+    if not np.all(v > 0):
+        raise ValueError("varn must be > 0")
+    return float(v[0]), torch.from_numpy(v).to("cuda")
+
+
 def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_true=None,
              h_true=None, solve="chol", return_device=False, partition_r=0,
              return_decisions=False, x_sup=None, varx=1.0):
@@ -83,7 +99,9 @@ def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_t
     Gaussian-prior EM (MIMO_Gaussian_proposed.py:56-89) with prior variance parameter varx;
     psi_d then has P = N rows (no direct path), cons is ignored, theta is the reduced
     channel (gauss_expand_batch gives the reference's n_rx x Q matrix).
-    Inputs may be numpy arrays or CUDA complex128 tensors (used in place).
+    Inputs may be numpy arrays or CUDA complex128 tensors (used in place).  varn may be one
+    value or one per trial ((B,) array: the trials of several SNR points in one call, include/
+    sbce.h sbce_ptrs.varn_t; each trial's result is that of a call with its own varn).
     Returns dict(theta (B,K), llf (B,itera) or None, status (B,), iters_done (B,)).
     """
     torch = _torch()
@@ -109,7 +127,8 @@ def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_t
     M = Cs.shape[0]
     if th.shape != (B, L * n_rx):
         raise ValueError(f"theta0 shape {tuple(th.shape)} != {(B, L * n_rx)}")
-    dims = _lib.Dims(B, n_tx, n_rx, P, T_p, T_d, M, int(partition_r), float(varn), float(varx))
+    varn0, Vt = _varn_arg(torch, varn, B)
+    dims = _lib.Dims(B, n_tx, n_rx, P, T_p, T_d, M, int(partition_r), varn0, float(varx))
     ws_bytes = _lib.workspace_bytes(dims, _SOLVES[solve])
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device="cuda")
     status = torch.zeros(B, dtype=torch.int32, device="cuda")
@@ -127,7 +146,8 @@ def em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", x_d_t
                      Ht.data_ptr() if Ht is not None else None, iters_done.data_ptr(),
                      status.data_ptr(), ws.data_ptr(), ws.numel(),
                      xdest.data_ptr() if xdest is not None else None,
-                     Xs.data_ptr() if Xs is not None else None)
+                     Xs.data_ptr() if Xs is not None else None,
+                     Vt.data_ptr() if Vt is not None else None)
     stream = torch.cuda.current_stream().cuda_stream
     _lib.check(lib.sbce_em(dims, ptrs, int(itera), _MODES[mode], _SOLVES[solve], stream), "sbce_em")
     out = dict(theta=th, llf=llf, status=status, iters_done=iters_done)
@@ -554,7 +574,10 @@ class EMEngine:
     """
 
     def __init__(self, batch, varn, mode="soft", solve="chol", x_d_true=None, h_true=None,
-                 partition_r=0, varx=1.0, x_sup=None, streams=1):
+                 partition_r=0, varx=1.0, x_sup=None, streams=1, early_stop=False):
+        """early_stop=True: the reference's oracle early stop on the true channel (PM.py:110-112,
+        all_detectorsvsTd.py's five EMs) with h_true (or batch["h"]); ``iters_done`` then holds
+        the iterations each trial of the last run() performed."""
         torch = _torch()
         self.torch = torch
         self.lib = _lib.load()
@@ -575,7 +598,8 @@ class EMEngine:
         T_p, P, L = self.y_p.shape[1], self.psi_d.shape[2], self.u_p.shape[2]
         self.n_tx, self.n_rx, self.B, self.T_d, self.T_p, self.P = L // P, n_rx, B, T_d, T_p, P
         self.M = self.cons.shape[0]
-        self.varn = float(varn)
+        # one noise variance, or one per trial (the SNR axis of a sweep batched into one call)
+        self.varn, self.varn_t = _varn_arg(torch, varn, B)
         if mode == "gauss" and not varx > 0:
             raise ValueError("mode 'gauss' needs a prior variance varx > 0")
         if x_sup is not None and mode not in ("soft", "hard"):
@@ -605,10 +629,17 @@ class EMEngine:
         # rejects; the pilot buffers are never read then, so pass y_d as a placeholder (em_batch)
         yp = self.y_p.data_ptr() if T_p else self.y_d.data_ptr()
         up = self.u_p.data_ptr() if T_p else self.y_d.data_ptr()
+        if early_stop and self.h is None:
+            raise ValueError("early_stop needs the true channel (h_true or batch['h'])")
+        self.early_stop = bool(early_stop)
+        self.iters_done = torch.zeros(B, dtype=torch.int32, device="cuda")
+        hp = self.h.data_ptr() if self.early_stop else None
         self.ptrs = _lib.Ptrs(self.y_d.data_ptr(), yp, self.psi_d.data_ptr(), up,
-                              self.cons.data_ptr(), self.theta.data_ptr(), None, None, None, None,
-                              self.status.data_ptr(), self.ws.data_ptr(), self.ws.numel(), None,
-                              self.x_sup.data_ptr() if self.x_sup is not None else None)
+                              self.cons.data_ptr(), self.theta.data_ptr(), None, None, hp,
+                              self.iters_done.data_ptr(), self.status.data_ptr(), self.ws.data_ptr(),
+                              self.ws.numel(), None,
+                              self.x_sup.data_ptr() if self.x_sup is not None else None,
+                              self.varn_t.data_ptr() if self.varn_t is not None else None)
         self.subs = []
         if sub:
             off = 0
@@ -617,15 +648,19 @@ class EMEngine:
                 off += nb
                 ptrs = _lib.Ptrs(self.y_d[b0:b1].data_ptr(), self.y_p[b0:b1].data_ptr(),
                                  self.psi_d[b0:b1].data_ptr(), self.u_p[b0:b1].data_ptr(),
-                                 self.cons.data_ptr(), self.theta[b0:b1].data_ptr(), None, None, None,
-                                 None, self.status[b0:b1].data_ptr(), ws.data_ptr(), ws.numel(), None,
-                                 None)
+                                 self.cons.data_ptr(), self.theta[b0:b1].data_ptr(), None, None,
+                                 self.h[b0:b1].data_ptr() if self.early_stop else None,
+                                 self.iters_done[b0:b1].data_ptr(), self.status[b0:b1].data_ptr(),
+                                 ws.data_ptr(), ws.numel(), None, None,
+                                 self.varn_t[b0:b1].data_ptr() if self.varn_t is not None else None)
                 self.subs.append((dims, ptrs, ws, torch.cuda.Stream()))
 
-    def run(self, itera):
-        """One full EM (itera iterations) over the whole batch, stream-ordered."""
-        self.theta.copy_(self.theta0)
-        cur = self.torch.cuda.current_stream()
+    def run(self, itera, stream=None):
+        """One full EM (itera iterations) over the whole batch, stream-ordered on `stream`
+        (default: the current stream)."""
+        cur = self.torch.cuda.current_stream() if stream is None else stream
+        with self.torch.cuda.stream(cur):
+            self.theta.copy_(self.theta0)
         if not self.subs:
             rc = self.lib.sbce_em(self.dims, self.ptrs, int(itera), self.mode, self.solve,
                                   cur.cuda_stream)

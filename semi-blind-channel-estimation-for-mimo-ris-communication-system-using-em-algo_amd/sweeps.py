@@ -174,15 +174,32 @@ SNR_DETECTORS = {
 }
 
 
+def _snr_groups(points, varns, batch_snr):
+    """The sbce_em calls of an SNR axis: with batch_snr ONE call over the trials of every SNR
+    point (per-trial noise variances, include/sbce.h sbce_ptrs.varn_t), else one call per point.
+    Yields (SNR indices, trials per index, packed batch, varn scalar or (B,) array)."""
+    live = [k for k, t in enumerate(points) if t]
+    if not live:
+        return
+    if batch_snr and len(live) > 1:
+        trials = [t for k in live for t in points[k]]
+        vt = np.concatenate([np.full(len(points[k]), varns[k]) for k in live])
+        yield live, [len(points[k]) for k in live], _pack(trials, None), vt
+    else:
+        for k in live:
+            yield [k], [len(points[k])], _pack(points[k], None), varns[k]
+
+
 def nmse_vs_snr(SNR=(-5, 0, 5, 10, 15, 20), T_d=50, T_p=12, N=10, n_rx=2, n_tx=2, itera=5,
                 monte_iter=15, M=4, power=10.0, seed=0, replay=True, modes=tuple(SNR_DETECTORS),
-                varh=1.0, partition_r=1, return_status=False):
+                varh=1.0, partition_r=1, return_status=False, batch_snr=True):
     """Mean NMSE per SNR of the five EMs of PMd/SNR/all_Detectors.py (driver :362-395; varn =
     power / 10^(SNR/10), :351-354): em_pm (r = 1), em_ml, em_zf, em_mmse and the exact em, each
     with that script's own early-stop pattern (SNR_DETECTORS) and np.linalg.solve M-step.
 
-    One batched sbce_em per (SNR point, detector) over this rank's trials; the accumulators of
-    every (detector, SNR) point are all-reduced ONCE at the end.  Returns (SNR, {mode: curve});
+    One batched sbce_em per detector over this rank's trials of EVERY SNR point (per-trial noise
+    variances; batch_snr=False: one call per (SNR point, detector), the same results); the
+    accumulators of every (detector, SNR) point are all-reduced ONCE at the end.  Returns (SNR, {mode: curve});
     with return_status also {mode: (len(SNR),) count of trials whose status word is non-zero
     (e.g. SBCE_STATUS_DETECTOR: the reference's nearest_symbol_ecul would raise IndexError)}."""
     dist, world, rank = _dist()
@@ -192,18 +209,17 @@ def nmse_vs_snr(SNR=(-5, 0, 5, 10, 15, 20), T_d=50, T_p=12, N=10, n_rx=2, n_tx=2
     cons = qam_constellation(M)
     nm, ns = len(modes), len(SNR)
     acc = Accumulators(nm * ns, n_extra=1)
-    for k, trials in enumerate(points):
-        if not trials:
-            continue
-        b = _pack(trials, None)
+    for ks, counts, b, vn in _snr_groups(points, varns, batch_snr):
         for mi, mode in enumerate(modes):
             stop = SNR_DETECTORS[mode][1]
-            r = em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], cons, varns[k], itera,
+            r = em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], cons, vn, itera,
                          b["theta0"], mode=mode,
                          partition_r=partition_r if mode.startswith("pm") else 0,
                          h_true=b["h"] if stop else None)
-            acc.add(mi * ns + k, _nmse(r["theta"], b["h"]),
-                    extra_values=(r["status"] != 0).astype(float)[:, None])
+            err, flag = _nmse(r["theta"], b["h"]), (r["status"] != 0).astype(float)[:, None]
+            off = np.cumsum([0] + counts)
+            for k, o0, o1 in zip(ks, off[:-1], off[1:]):
+                acc.add(mi * ns + k, err[o0:o1], extra_values=flag[o0:o1])
     acc.allreduce(dist)                   # the sweep's only collective
     mean = acc.mean_nmse().reshape(nm, ns)
     curves = {mode: mean[mi] for mi, mode in enumerate(modes)}
@@ -424,12 +440,14 @@ def gen_detectors(T_d=(15, 30, 45, 60, 75, 90), SNR=None, T_p=20, N=15, n_rx=2, 
 
 def nmse_grid_detectors(T_d=(15, 30, 45, 60, 75, 90), SNR=None, T_p=20, N=15, n_rx=2, n_tx=2,
                         itera=5, monte_iter=1, M=4, varn=0.1, power=10.0, partition_r=1, seed=0,
-                        replay=True, detectors=tuple(DETECTORS), early_stop=True, varh=1.0):
+                        replay=True, detectors=tuple(DETECTORS), early_stop=True, varh=1.0,
+                        batch_snr=True):
     """Mean NMSE of the five EMs of PMd/all_detectorsvsTd.py (:384-405) per T_d point, and
     per SNR point when SNR is given (BASELINE configs[4]: 20 SNR x 8 T_d, 64-QAM).
 
-    One batched sbce_em per (T_d, SNR, detector) over this rank's trials; every EM keeps the
-    script's oracle early stop on the true h (:87-89, :128-130, :169-171, :243-245,
+    One batched sbce_em per (T_d, detector) over this rank's trials of every SNR point (per-trial
+    noise variances; batch_snr=False: one per (T_d, SNR, detector), the same results); every EM
+    keeps the script's oracle early stop on the true h (:87-89, :128-130, :169-171, :243-245,
     :291-293) unless early_stop=False, and its np.linalg.solve M-step (SBCE_SOLVE_CHOL).
     The accumulators of the whole grid are all-reduced once.  Returns (T_d, SNR or None,
     {detector: (len(T_d), len(SNR or [varn])) mean NMSE})."""
@@ -441,16 +459,15 @@ def nmse_grid_detectors(T_d=(15, 30, 45, 60, 75, 90), SNR=None, T_p=20, N=15, n_
     nd, nt, ns = len(detectors), len(T_d), len(varns)
     acc = Accumulators(nd * nt * ns)
     for k in range(nt):
-        for j in range(ns):
-            trials = points[k][j]
-            if not trials:
-                continue
-            b = _pack(trials, None)
+        for js, counts, b, vn in _snr_groups(points[k], varns, batch_snr):
+            off = np.cumsum([0] + counts)
             for di, det in enumerate(detectors):
-                r = em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], cons, varns[j], itera,
+                r = em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], cons, vn, itera,
                              b["theta0"], mode=det, partition_r=partition_r if det == "pm_soft" else 0,
                              h_true=b["h"] if early_stop else None)
-                acc.add((di * nt + k) * ns + j, _nmse(r["theta"], b["h"]))
+                nm = _nmse(r["theta"], b["h"])
+                for j, o0, o1 in zip(js, off[:-1], off[1:]):
+                    acc.add((di * nt + k) * ns + j, nm[o0:o1])
     acc.allreduce(dist)
     mean = acc.mean_nmse().reshape(nd, nt, ns)
     return (np.asarray(T_d), None if SNR is None else np.asarray(SNR),

@@ -38,9 +38,9 @@ def test_struct_layout_matches_c(sbce, tmp_path):
 #include <stddef.h>
 #include "sbce.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(sbce_dims), offsetof(sbce_dims, varn),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(sbce_dims), offsetof(sbce_dims, varn),
          sizeof(sbce_ptrs), offsetof(sbce_ptrs, workspace_bytes), offsetof(sbce_ptrs, x_dest),
-         offsetof(sbce_dims, partition_r), offsetof(sbce_dims, varx));
+         offsetof(sbce_dims, partition_r), offsetof(sbce_dims, varx), offsetof(sbce_ptrs, varn_t));
   return 0;
 }''')
     exe = tmp_path / "probe"
@@ -51,7 +51,7 @@ int main(void) {
     assert [int(v) for v in out] == [ctypes.sizeof(L.Dims), L.Dims.varn.offset,
                                      ctypes.sizeof(L.Ptrs), L.Ptrs.workspace_bytes.offset,
                                      L.Ptrs.x_dest.offset, L.Dims.partition_r.offset,
-                                     L.Dims.varx.offset]
+                                     L.Dims.varx.offset, L.Ptrs.varn_t.offset]
 
 
 def test_integration_snippet_matches_abi(sbce):

@@ -116,6 +116,38 @@ def test_detector_grid_snr_td_64qam_vs_oracle(sbce):
                 assert abs(curves[mode][k, j] / np.mean(vals) - 1) < 1e-8, (mode, k, j)
 
 
+def test_detector_grid_cfg5_full_size_vs_oracle(sbce):
+    """BASELINE configs[4] at its full per-point size: N_RIS = 15, 2x2, T_p = 20, 64-QAM (J = 4096,
+    L = 32), the five EMs of all_detectorsvsTd.py (:371-405, oracle early stop, 5 iterations) at
+    the T_d ends of the bench grid (15, 120) and SNR 0 / 15 / 30 dB with the 64-QAM power 42 that
+    bench.py --config cfg5 uses: every grid value vs the oracle restatements at 1e-8 (north-star
+    bar 1e-3).  ZF / MMSE decisions through the oracle's closed-form flat argmin (ecul_index,
+    pinned to the literal scan in test_oracle.py)."""
+    T_d, SNR = (15, 120), (0.0, 15.0, 30.0)
+    T_p, N, n_rx, n_tx, itera, mc, M, power = 20, 15, 2, 2, 5, 2, 64, 42.0
+    _, _, curves = sbce.sweeps.nmse_grid_detectors(T_d, SNR, T_p, N, n_rx, n_tx, itera, mc, M,
+                                                   power=power, partition_r=1, seed=5)
+    points, varns = sbce.sweeps.gen_detectors(T_d, SNR, T_p, N, n_rx, n_tx, mc, M, power=power,
+                                              seed=5)
+    cons = sbce.qam.qam_constellation(M)
+    aps = sbce.qam.all_possible_symbols(cons, n_tx)
+    for k in range(len(T_d)):
+        for j, vn in enumerate(varns):
+            ref = {m: [] for m in MODES.values()}
+            for t in points[k][j]:
+                a = (t["Y_d"], t["Y_p"], t["U_p"], t["Psi_d"])
+                h = t["h"]
+                ref["pm_soft"].append(nmse(em_pm(*a, vn, itera, t["h0"], n_tx, n_rx, 1, cons,
+                                                 soft=True, h=h), h))
+                ref["hard"].append(nmse(em_reduced(*a, aps, vn, itera, t["h0"], "hard", h=h), h))
+                for kind in ("zf", "mmse"):
+                    ref[kind].append(nmse(em_detector(*a, None, vn, itera, t["h0"], n_tx, n_rx,
+                                                      kind, h=h, cons=cons), h))
+                ref["soft"].append(nmse(em_reduced(*a, aps, vn, itera, t["h0"], h=h), h))
+            for mode, vals in ref.items():
+                assert abs(curves[mode][k, j] / np.mean(vals) - 1) < 1e-8, (mode, T_d[k], SNR[j])
+
+
 def test_llf_driver_matches_reference_fixture(sbce):
     """sweeps.llf_vs_iteration (IterationsvsLLF.py's driver, genie LLF :76) vs the
     reference's own per-trial LLF curves, averaged as the script does (:154)."""

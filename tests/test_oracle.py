@@ -584,7 +584,8 @@ def test_snr_sweep_five_detectors_one_collective(sbce, monkeypatch):
     def fake_em_batch(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft",
                       partition_r=0, h_true=None, **kw):
         seen.append((mode, partition_r, h_true is not None))
-        th = np.stack([_oracle_snr_em(mode, y_d[b], y_p[b], psi_d[b].T, u_p[b], cons, varn, itera,
+        vt = np.broadcast_to(np.asarray(varn, dtype=float), (len(y_d),))   # per-trial (ABI 6)
+        th = np.stack([_oracle_snr_em(mode, y_d[b], y_p[b], psi_d[b].T, u_p[b], cons, vt[b], itera,
                                       theta0[b], None if h_true is None else h_true[b],
                                       partition_r) for b in range(len(y_d))])
         return dict(theta=th, status=np.zeros(len(y_d), dtype=np.int32))
