@@ -63,6 +63,70 @@ def test_sharded_sweep_matches_single_process(sbce, world):
         assert np.allclose(got.mean_nmse(), ref.mean_nmse(), rtol=1e-14, atol=0)
 
 
+def _oracle_em_batch(calls):
+    """sweeps.em_batch stand-in: the oracle twin of each SNR-script EM per trial (per-trial or
+    scalar varn), recording (mode, trials) of every call."""
+    from test_oracle import _oracle_snr_em
+
+    def fake(y_d, y_p, psi_d, u_p, cons, varn, itera, theta0, mode="soft", partition_r=0,
+             h_true=None, **kw):
+        calls.append((mode, len(y_d)))
+        vt = np.broadcast_to(np.asarray(varn, dtype=float), (len(y_d),))
+        th = np.stack([_oracle_snr_em(mode, y_d[b], y_p[b], psi_d[b].T, u_p[b], cons, vt[b], itera,
+                                      theta0[b], None if h_true is None else h_true[b],
+                                      partition_r) for b in range(len(y_d))])
+        return dict(theta=th, status=np.zeros(len(y_d), dtype=np.int32))
+    return fake
+
+
+def _snr_sweep_worker(rank, world, port, monte_iter, out):
+    import importlib
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sbce = importlib.import_module(PKG)
+    calls, reduces = [], []
+    sbce.sweeps.em_batch = _oracle_em_batch(calls)
+    real = dist.all_reduce
+
+    def counted(t, *a, **kw):
+        reduces.append(t.numel())
+        return real(t, *a, **kw)
+    dist.all_reduce = counted
+    snr, curves = sbce.sweeps.nmse_vs_snr(monte_iter=monte_iter, seed=0)
+    dist.all_reduce = real
+    out[rank] = dict(curves={k: v.tolist() for k, v in curves.items()}, calls=calls,
+                     reduces=reduces)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_snr_sweep_driver_world2_matches_world1(sbce, monkeypatch):
+    """sweeps.nmse_vs_snr (the north-star NMSE-vs-SNR figure, SNR/all_Detectors.py:362-395) under
+    a real gloo world of 2: each rank runs its shard of the replayed trials (ONE call per detector
+    with the SNR axis batched), ONE all-reduce carries every (detector, SNR) accumulator, and the
+    five curves equal the world-1 run at 1e-14.  The oracle stands in for the device."""
+    monte_iter = 3
+    calls1 = []
+    monkeypatch.setattr(sbce.sweeps, "em_batch", _oracle_em_batch(calls1))
+    _, ref = sbce.sweeps.nmse_vs_snr(monte_iter=monte_iter, seed=0)
+    assert [c[1] for c in calls1] == [monte_iter * 6] * 5          # 5 calls: every SNR point
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_snr_sweep_worker, args=(2, _free_port(), monte_iter, out), nprocs=2, join=True)
+    trials = 0
+    for r in range(2):
+        got = out[r]
+        assert len(got["reduces"]) == 1 and got["reduces"][0] == 5 * 6 * 3   # nmse, count, flags
+        trials += got["calls"][0][1]
+        for mode, curve in ref.items():
+            assert np.allclose(got["curves"][mode], curve, rtol=1e-14, atol=0), (r, mode)
+    assert trials == monte_iter * 6
+
+
 def test_shard_partition_is_exact(sbce):
     for n in (1, 7, 1000):
         for world in (1, 2, 3, 8):
