@@ -16,8 +16,8 @@ namespace sbce {
 DebugConfig g_debug;
 
 namespace {
-constexpr DebugConfig kDebugDefault = {false, false, false, 4, false, false, false, false, false, 128,
-                                       0, false, false, 0, 0, 0, false, true};
+constexpr DebugConfig kDebugDefault = {false, false, false, false, 0, false, 128, false, false, false,
+                                       true};
 constexpr int kSphereBudgetMax = 256;      // estep.hip kBfsPmax
 
 void read_debug_env(DebugConfig& c) {
@@ -27,22 +27,15 @@ void read_debug_env(DebugConfig& c) {
     if ((v = env("SBCE_ESTEP_IMPL"))) c.estep_valu = v[0] == 'v';
     if ((v = env("SBCE_ESTEP_PRUNE"))) c.estep_noprune = v[0] == '0';
     if ((v = env("SBCE_ESTEP_COUNT"))) c.estep_count = v[0] == '1';
-    if ((v = env("SBCE_ESTEP_SPW"))) c.estep_spw = atoi(v) < 1 ? 1 : atoi(v);
-    if ((v = env("SBCE_ESTEP_ROWB"))) c.estep_norowb = v[0] == '0';
     if ((v = env("SBCE_ESTEP_F32"))) c.estep_nof32 = v[0] == '0';
-    if ((v = env("SBCE_CHOL_INV"))) c.chol_inv = (v[0] == 'l' || v[0] == 'p') ? v[0] : 0;
     if ((v = env("SBCE_ESTEP_OCC"))) c.estep_occ = (v[0] == '2' || v[0] == '3') ? v[0] : 0;
-    if ((v = env("SBCE_PREP_UNI"))) c.prep_nouni = v[0] == '0';
     if ((v = env("SBCE_ESTEP_SPHERE"))) c.estep_nosphere = v[0] == '0';
     if ((v = env("SBCE_SPHERE_BUDGET"))) {
         const int bu = atoi(v);
         c.sphere_budget = bu < 1 ? 1 : (bu > kSphereBudgetMax ? kSphereBudgetMax : bu);
     }
-    if ((v = env("SBCE_RHS_IMPL"))) c.rhs_impl = (v[0] == 'r' || v[0] == 'l') ? v[0] : 0;
-    if ((v = env("SBCE_RB_TC"))) c.rb_tc32 = v[0] == '3';
-    if ((v = env("SBCE_UPD_WAVES"))) c.upd_waves8 = v[0] == '8';
-    if ((v = env("SBCE_BACKSUB"))) c.backsub = (v[0] >= '1' && v[0] <= '3') ? v[0] - '0' : 0;
-    if ((v = env("SBCE_CHOL_IMPL"))) c.chol_impl = (v[0] == 'v' || v[0] == 'f' || v[0] == 'u' || v[0] == 'l' || v[0] == 'n' || v[0] == 's' || v[0] == 'o') ? v[0] : 0;
+    if ((v = env("SBCE_BACKSUB"))) c.backsub_general = v[0] == '1';
+    if ((v = env("SBCE_CHOL_IMPL"))) c.chol_valu = v[0] == 'v';
     if ((v = env("SBCE_ESTEP_PAIR"))) c.estep_nopair = v[0] == '0';
     if ((v = env("SBCE_CPLX3"))) c.cplx3 = v[0] != '0';
 }
@@ -54,13 +47,10 @@ bool debug_nondefault() {
     const DebugConfig& c = g_debug;
     const DebugConfig& d = kDebugDefault;
     return c.estep_valu != d.estep_valu || c.estep_noprune != d.estep_noprune ||
-           c.estep_spw != d.estep_spw || c.estep_norowb != d.estep_norowb || c.estep_nof32 != d.estep_nof32 ||
-           c.chol_inv != d.chol_inv ||
-           c.estep_occ != d.estep_occ || c.prep_nouni != d.prep_nouni ||
+           c.estep_nof32 != d.estep_nof32 || c.estep_occ != d.estep_occ ||
            c.estep_nosphere != d.estep_nosphere || c.sphere_budget != d.sphere_budget ||
-           c.rhs_impl != d.rhs_impl || c.rb_tc32 != d.rb_tc32 || c.upd_waves8 != d.upd_waves8 ||
-           c.backsub != d.backsub || c.chol_impl != d.chol_impl || c.estep_nopair != d.estep_nopair ||
-           c.cplx3 != d.cplx3 ||
+           c.backsub_general != d.backsub_general || c.chol_valu != d.chol_valu ||
+           c.estep_nopair != d.estep_nopair || c.cplx3 != d.cplx3 ||
            (chol_debug_skip_mask() & 31);
 }
 

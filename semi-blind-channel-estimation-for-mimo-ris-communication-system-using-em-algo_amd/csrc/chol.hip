@@ -368,11 +368,13 @@ __device__ __forceinline__ void diag_inverse_rd(const cd* A, cd* Di, const doubl
 // LDS round trip: every lane reads the pivot and the column entries it needs, then
 //   L[r][c] = A[r][c] / p,   A[r][c2] -= A[r][c] conj(A[c2][c]) / p^2   (r >= c2 > c)
 // are written together (the trailing update uses the unscaled column, so no second
-// pass).  Di = D^{-1} then goes row by row, four lanes per column j splitting the
-// sum over m (reduced by two xor-shuffles): 16 dependent steps of one round trip each.
-// Few registers, so the MFMA update loop keeps its occupancy.  Writes Di to LDS and the
-// factor rows + conj(Di) (strict upper) into R's diagonal block.
-template <bool RD = true, bool COLS2 = RD, bool PAIR = false>
+// pass).  Per lane, the role in column step c depends only on its column: col > c trailing,
+// col == c the column, col < c final (not stored), so every entry is m A[r][col] + A[r][c] f
+// with (m, f) per lane -- 6 FP64 ops per entry, no per-entry selects; the pivot's 1/sqrt is
+// seeded by v_rsq_f64 (fast_rsqrt64).  Di = D^{-1} by recursive doubling (diag_inverse_rd).
+// Few registers, so the MFMA phases keep their occupancy.  Writes Di to LDS and the factor
+// rows + conj(Di) (strict upper) into R's diagonal block.  The strict upper part of A is never
+// multiplied into a lower entry: it may hold the workspace's old contents (NaN included).
 __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double tol,
                                                 int solve_mode, cd* Di, double* dinv, int* flag,
                                                 cd* Rdiag, int L,
@@ -380,74 +382,8 @@ __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double t
     const int col = lane & 15, r0 = lane >> 4;
     unsigned long long tc = clk ? __builtin_amdgcn_s_memtime() : 0;
     bool bad_any = false, near_any = false;
-    if constexpr (PAIR) {
-        // Two columns per LDS round trip: column c1 = c + 1 is updated by column c in registers
-        // (A'[x][c1] = A[x][c1] - A[x][c] g, g = conj(A[c1][c]) / p0), its pivot follows from
-        // p1 = A[c1][c1] - |A[c1][c]|^2 / p0, and every entry takes both rank-1 steps at once:
-        //   col > c1: m = 1, f0 = -conj(A[col][c]) / p0, f1 = -conj(A'[col][c1]) / p1
-        //   col == c1: A'[r][c1] / sqrt(p1);   col == c: A[r][c] / sqrt(p0);   col < c: final.
-        // Garbage in the strict upper part meets only zero factors of entries that are upper
-        // themselves, except (c, c) (A[c][c1] is upper), which its owner then stores as (p0, 0).
 #pragma unroll 1
-        for (int c = 0; c < w; c += 2) {
-            const int c1 = c + 1;
-            const bool two = c1 < w;
-            const double dia0 = A[c * NB + c].x, dia1 = A[c1 * NB + c1].x;
-            const cd a10 = A[c1 * NB + c];
-            const cd lc0 = A[col * NB + c], lc1 = A[col * NB + c1];
-            cd arc0[4], arc1[4], arx[4];
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                const int r = r0 + 4 * h;
-                arc0[h] = A[r * NB + c];
-                arc1[h] = A[r * NB + c1];
-                arx[h] = A[r * NB + col];
-            }
-            const bool bad0 = !(dia0 > tol);
-            const bool drop0 = bad0 && solve_mode != SBCE_SOLVE_CHOL;
-            const double pv0 = bad0 ? tol : dia0;
-            const double rs0 = fast_rsqrt64(pv0);
-            const double piv0 = drop0 ? 0.0 : pv0 * rs0, inv0 = drop0 ? 0.0 : rs0;
-            const double q0 = inv0 * inv0;
-            const cd g = cmk(a10.x * q0, -a10.y * q0);                   // conj(a10) / p0
-            const double d1 = dia1 - fma(a10.x, g.x, -a10.y * g.y);      // A'[c1][c1]
-            const bool bad1 = two && !(d1 > tol);
-            const bool drop1 = bad1 && solve_mode != SBCE_SOLVE_CHOL;
-            const double pv1 = bad1 ? tol : d1;
-            const double rs1 = two ? fast_rsqrt64(pv1) : 0.0;
-            const double piv1 = (drop1 || !two) ? 0.0 : pv1 * rs1, inv1 = (drop1 || !two) ? 0.0 : rs1;
-            bad_any |= bad0 || bad1;
-            near_any |= solve_mode == SBCE_SOLVE_MINNORM &&
-                        ((dia0 > tol * (1.0 / 8) && dia0 < tol * 64) || (two && d1 > tol * (1.0 / 8) && d1 < tol * 64));
-            const cd t1 = csub(lc1, cmul(lc0, g));                       // A'[col][c1]
-            const double q1 = inv1 * inv1;
-            wave_sync();                                                 // all reads done
-            dinv[c] = inv0;
-            if (two) dinv[c1] = inv1;
-            const bool gt = col > c1, eq0 = col == c, eq1 = col == c1;
-            const double m = gt ? 1.0 : 0.0;
-            const double f0x = gt ? -lc0.x * q0 : (eq0 ? inv0 : 0.0), f0y = gt ? lc0.y * q0 : 0.0;
-            const double f1x = gt ? -t1.x * q1 : (eq1 ? inv1 : 0.0), f1y = gt ? t1.y * q1 : 0.0;
-            if (col >= c) {
-#pragma unroll
-                for (int h = 0; h < 4; ++h) {
-                    const int r = r0 + 4 * h;
-                    const cd a1 = csub(arc1[h], cmul(arc0[h], g));       // A'[r][c1]
-                    const double vx = fma(a1.x, f1x, fma(-a1.y, f1y, fma(arc0[h].x, f0x, fma(-arc0[h].y, f0y, m * arx[h].x))));
-                    const double vy = fma(a1.x, f1y, fma(a1.y, f1x, fma(arc0[h].x, f0y, fma(arc0[h].y, f0x, m * arx[h].y))));
-                    A[r * NB + col] = cmk(vx, vy);
-                }
-                if (eq0 && r0 == (c & 3)) A[c * NB + c] = cmk(piv0, 0.0);
-                if (eq1 && two && r0 == (c1 & 3)) A[c1 * NB + c1] = cmk(piv1, 0.0);
-            }
-            wave_sync();
-        }
-    }
-    // Branch-free: every entry (r, col) has exactly one owner lane, which rewrites it each
-    // column (unchanged entries get their old value back); divergent branches in this
-    // single-wave dependent chain cost more than the arithmetic.
-#pragma unroll 1
-    for (int c = 0; c < (PAIR ? 0 : w); ++c) {
+    for (int c = 0; c < w; ++c) {
         const double dia = A[c * NB + c].x;
         const cd lc = A[col * NB + c];                      // A[col][c] (unscaled)
         cd arc[4], arx[4];
@@ -464,50 +400,26 @@ __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double t
         near_any |= solve_mode == SBCE_SOLVE_MINNORM && dia > tol * (1.0 / 8) && dia < tol * 64;
         const bool drop = bad && solve_mode != SBCE_SOLVE_CHOL;
         const double pv = bad ? tol : dia;
-        const double rs = COLS2 ? fast_rsqrt64(pv) : fast_rsqrt(pv);
+        const double rs = fast_rsqrt64(pv);
         const double piv = drop ? 0.0 : pv * rs;
         const double inv = drop ? 0.0 : rs;
         const cd lcs = cscale(cconj(lc), inv * inv);
         if (clk && lane == 0) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); clk[9] += t2 - tc; tc = t2; }
         wave_sync();                                         // all reads of column c done
         dinv[c] = inv;                                       // same value from every lane
-        if constexpr (COLS2) {
-            // Per lane, the role in column step c depends only on its column (lane-uniform over
-            // the 4 entries): col > c trailing, new = A[r][col] - A[r][c] conj(A[col][c]) / p;
-            // col == c the column, new = A[r][c] / sqrt(p); col < c final (not stored).  So every
-            // entry is new = m A[r][col] + A[r][c] f with (m, f) per lane, and the rows above the
-            // diagonal are not excluded: they are the strict upper part (never read as L; its
-            // values, the workspace's old contents included, only pass through or become other
-            // garbage there).  Rows and columns past w are zero and stay zero.  The pivot entry is
-            // then stored as (piv, 0) by its owner.  6 FP64 ops per entry, no per-entry selects.
-            const bool gt = col > c, eq = col == c;
-            const double m = eq ? 0.0 : 1.0;
-            const double fx = gt ? -lcs.x : (eq ? inv : 0.0);
-            const double fy = gt ? -lcs.y : 0.0;
-            if (col >= c) {
+        const bool gt = col > c, eq = col == c;
+        const double m = eq ? 0.0 : 1.0;
+        const double fx = gt ? -lcs.x : (eq ? inv : 0.0);
+        const double fy = gt ? -lcs.y : 0.0;
+        if (col >= c) {
 #pragma unroll
-                for (int h = 0; h < 4; ++h) {
-                    const int r = r0 + 4 * h;
-                    const cd v = cmk(fma(arc[h].x, fx, fma(-arc[h].y, fy, m * arx[h].x)),
-                                     fma(arc[h].x, fy, fma(arc[h].y, fx, m * arx[h].y)));
-                    A[r * NB + col] = v;
-                }
-                if (eq && r0 == (c & 3)) A[c * NB + c] = cmk(piv, 0.0);
+            for (int h = 0; h < 4; ++h) {
+                const int r = r0 + 4 * h;
+                const cd v = cmk(fma(arc[h].x, fx, fma(-arc[h].y, fy, m * arx[h].x)),
+                                 fma(arc[h].x, fy, fma(arc[h].y, fx, m * arx[h].y)));
+                A[r * NB + col] = v;
             }
-        } else {
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            const int r = r0 + 4 * h;
-            const bool isdiag = col == c && r == c;
-            const bool iscol = col == c && r > c && r < w;
-            const bool istrail = col > c && col < w && r >= col && r < w;
-            const cd upd = csub(arx[h], cmul(arc[h], lcs));
-            const cd scl = cscale(arc[h], inv);
-            cd v = csel(istrail, upd, arx[h]);
-            v = csel(iscol, scl, v);
-            v = csel(isdiag, cmk(piv, 0.0), v);
-            A[r * NB + col] = v;
-        }
+            if (eq && r0 == (c & 3)) A[c * NB + c] = cmk(piv, 0.0);
         }
         wave_sync();
         if (clk && lane == 0) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); clk[10] += t2 - tc; tc = t2; }
@@ -515,29 +427,7 @@ __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double t
     if (bad_any) *flag |= 1;
     if (near_any) *flag |= 2;
     if (clk && lane == 0) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); clk[0] += t2 - tc; tc = t2; }
-    if constexpr (RD) {
-        diag_inverse_rd(A, Di, dinv, w, lane);
-    } else {
-    // Di[k][j] = (delta_kj - sum_{j<=m<k} L[k][m] Di[m][j]) / L[k][k]; lane = (j, part)
-        const int j = lane & 15, part = lane >> 4;
-#pragma unroll 1
-        for (int k = 0; k < NB; ++k) {
-            cd acc = czero();
-#pragma unroll
-            for (int mm = 0; mm < 4; ++mm) {
-                const int m = part + 4 * mm;
-                const bool on = m >= j && m < k;
-                const cd lkm = A[k * NB + m], dmj = Di[m * NB + j];
-                acc = cfma(acc, csel(on, lkm, czero()), csel(on, dmj, czero()));
-            }
-            acc.x += shfl_xor_d(acc.x, 16); acc.y += shfl_xor_d(acc.y, 16);
-            acc.x += shfl_xor_d(acc.x, 32); acc.y += shfl_xor_d(acc.y, 32);
-            const double inv = (k < w) ? dinv[k] : 0.0;     // 0 for dropped directions
-            const cd v = csel(k == j, cmk(1.0, 0.0), cmk(-acc.x, -acc.y));
-            Di[k * NB + j] = csel(k < w && j <= k && j < w, cscale(v, inv), czero());   // 4 lanes, same value
-            wave_sync();
-        }
-    }
+    diag_inverse_rd(A, Di, dinv, w, lane);
     if (clk && lane == 0) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); clk[1] += t2 - tc; tc = t2; }
     // factor rows (c <= r) and conj(Di[c][r]) (c > r) into R's diagonal block
 #pragma unroll
@@ -956,18 +846,6 @@ __device__ __forceinline__ void panel_update_body(const MstepArgs& a, int L, int
     }
 }
 
-template <int NWU, bool G3 = false>   // waves (= row tiles) per block: the staged panel rows serve NWU tiles
-__global__ __launch_bounds__(64 * NWU) void panel_update_kernel(MstepArgs a, int L, int jb, int ntile,
-                                                                int gpt, int skip) {
-    // skip: DIAGNOSTIC (timing only, results invalid): 1 no update
-    __shared__ __attribute__((aligned(16))) cd Bp[PW * (KBU + 1)];
-    const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
-    const int b = (slot / gpt) * 8 + xcd, grp = slot - (slot / gpt) * gpt;
-    if (b >= a.nbatch) return;
-    if (a.done && a.done[b]) return;
-    panel_update_body<NWU, G3>(a, L, jb, jb, ntile, b, grp, skip, Bp);
-}
-
 // panel_update2_kernel (wide left-looking step): the updates of panels j AND j+1 by the columns
 // [0, jb) in one launch -- for every trial gpt0 four-tile groups of panel j's rows and gpt1 of
 // panel j+1's (rows from jb + 32, k < jb; the rank-32 remainder by panel j is the next factor
@@ -986,21 +864,6 @@ __global__ __launch_bounds__(256) void panel_update2_kernel(MstepArgs a, int L, 
     if (a.done && a.done[b]) return;
     if (g < gpt0) panel_update_body<4, G3>(a, L, jb, jb, ntile, b, g, skip, Bp);
     else panel_update_body<4, G3>(a, L, jb + PW, jb, ntile - 2, b, g - gpt0, skip, Bp);
-}
-
-// panel_preupd_kernel (wide schedule, odd panels): the rank-32 update of panel jb by the previous
-// panel's columns [jb - 32, jb) -- the part panel_update2_kernel left -- as a launch of its own over
-// every trial's four-tile groups, instead of by the four waves of the trial's factor workgroup
-// ahead of its diagonal chain (SBCE_CHOL_IMPL=q keeps that in-factor pre-update, A/B).
-template <bool G3 = false>
-__global__ __launch_bounds__(256) void panel_preupd_kernel(MstepArgs a, int L, int jb, int ntile, int gpt,
-                                                           int skip) {
-    __shared__ __attribute__((aligned(16))) cd Bp[PW * (KBU + 1)];
-    const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
-    const int b = (slot / gpt) * 8 + xcd, grp = slot - (slot / gpt) * gpt;
-    if (b >= a.nbatch) return;
-    if (a.done && a.done[b]) return;
-    panel_update_body<4, G3>(a, L, jb, jb, ntile, b, grp, skip, Bp, jb - PW);
 }
 
 // 16 x 16 tile of R (rows row0.., columns c0.., w valid columns) into per-lane registers:
@@ -1089,87 +952,6 @@ __device__ __forceinline__ void load_ycomp(const cd* y, int L, int NR, int row0,
     }
 }
 
-// Lp layouts of the previous panel's top rows (the shared B operand, 32 x 32): SW false padded
-// rows of PW + 1 entries; SW true unpadded (exactly the Xs scratch of the factor body) with
-// the column index XOR-swizzled by c & 15, so the 16 rows a k-step reads fall in distinct banks
-template <bool SW>
-__device__ __forceinline__ int lp_idx(int c, int k) {
-    return SW ? c * PW + (k ^ (c & 15)) : c * (PW + 1) + k;
-}
-
-template <bool SW>
-__device__ __forceinline__ void preupdate_stage(const cd* R, int L, int jb, int w2, cd* Lp) {
-    for (int e = threadIdx.x; e < PW * PW; e += 256) {
-        const int c = e >> 5, k = e & (PW - 1);
-        Lp[lp_idx<SW>(c, k)] = c < w2 ? R[(size_t)(jb + c) * L + jb - PW + k] : czero();
-    }
-}
-
-// one wave: row tiles tau = tau0, tau0 + dt, ... < ntile of panel [jb, jb+32) -= (their columns
-// [jb-32, jb)) Lp^H  (tau0, dt wave-uniform)
-template <bool G3, bool SW>
-__device__ __forceinline__ void preupdate_tiles(cd* R, int L, int jb, int w2, int tau0, int dt, int ntile,
-                                                const cd* Lp, int li, int lk) {
-    const int k0c = jb - PW;
-#pragma unroll 1
-    for (int tau = tau0; tau < ntile; tau += dt) {
-        const int row0 = jb + tau * NB;
-        int r = row0 + li;
-        r = r < L ? r : L - 1;                                   // rows past L: harmless reads
-        const cd* arow = R + (size_t)r * L + k0c + lk;
-        cd av[4];
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) av[s2] = arow[4 * s2];
-        const int nv = tau == 0 ? 1 : 2;                         // tile 0's right half: upper triangle
-        d4v cre[2], cim[2], c2[2];
-#pragma unroll
-        for (int v = 0; v < 2; ++v) {
-            cre[v] = d4v{0.0, 0.0, 0.0, 0.0};
-            cim[v] = d4v{0.0, 0.0, 0.0, 0.0};
-            c2[v] = d4v{0.0, 0.0, 0.0, 0.0};
-            if (v < nv) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int rr = row0 + lk + 4 * q, c = 16 * v + li;
-                    if (rr < L && c < w2) {
-                        const cd x = R[(size_t)rr * L + jb + c];
-                        cre[v][q] = x.x;
-                        cim[v][q] = x.y;
-                    }
-                }
-            }
-            csub_init<G3>(cre[v], cim[v], c2[v]);
-        }
-#pragma unroll 1
-        for (int k0 = 0; k0 < PW; k0 += 16) {
-            cd an[4];
-#pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) an[s2] = k0 == 0 ? arow[16 + 4 * s2] : czero();
-#pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) {
-                const cd v = av[s2];
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    if (h >= nv) break;                          // wave-uniform
-                    // C -= A conj(B)^T (three real MFMAs per complex product with G3)
-                    csub_step<G3>(cre[h], cim[h], c2[h], v, Lp[lp_idx<SW>(16 * h + li, k0 + 4 * s2 + lk)]);
-                }
-            }
-#pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) av[s2] = an[s2];
-        }
-#pragma unroll
-        for (int v = 0; v < 2; ++v) {
-            if (v >= nv) break;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int rr = row0 + lk + 4 * q, c = 16 * v + li;
-                if (rr < L && c < w2) R[(size_t)rr * L + jb + c] = csub_out<G3>(cre[v], cim[v], c2[v], q);
-            }
-        }
-    }
-}
-
 // panel_factor_kernel: one workgroup (4 waves) per trial, panel [jb, jb+32) as sub-panels
 // A = [jb, jb+16) and B = [jb+16, jb+32):
 //   wave 0: factor A's diagonal tile (factor_diag_lds), D_A^-1 y_A, TRSM of row tile 1
@@ -1181,14 +963,10 @@ __device__ __forceinline__ void preupdate_tiles(cd* R, int L, int jb, int w2, in
 // LDS of the factor body (cd entries): Xs (4 waves' 16 x 16 scratch), DiA, DiB, XA1, ybA, ybB
 constexpr int kFacXs = 0, kFacDiA = 4 * NB * NB, kFacDiB = kFacDiA + NB * NB, kFacXA1 = kFacDiB + NB * NB,
               kFacYbA = kFacXA1 + NB * NB, kFacYbB = kFacYbA + NB * 8, kFacLds = kFacYbB + NB * 8;
-// overlapped pre-update (OV): wave 0's chain scratch moves past the body's LDS, so the Xs
-// region can hold the previous panel's rows (swizzled Lp) while waves 1-3 pre-update
-constexpr int kFacX0 = kFacLds, kFacLdsOv = kFacLds + NB * NB;
 template <bool G3 = false>
 __device__ __forceinline__ void panel_preupdate(const MstepArgs& a, int L, int jb, int ntile, int b,
                                                 cd* Lp);
-template <bool G3 = false, int DM = 1, bool CLK = false,  // DM (diagonal blocks): 0 row-recurrence inverse,
-          bool OV = false>                               // 1 recursive doubling, 2 + two columns per step
+template <bool G3 = false, bool CLK = false>
 __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int NR, int jb, int ntile,
                                                   int b, int skip, cd* sm, double* dinv, int& flag,
                                                   unsigned long long t_start = 0) {
@@ -1208,7 +986,7 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
     const double tol = a.tol[b];
     cd* R = a.R + (size_t)b * L * L;
     cd* y = a.rhs + (size_t)b * L * NR;
-    cd* X = (OV && wave == 0) ? sm + kFacX0 : Xs + wave * NB * NB;
+    cd* X = Xs + wave * NB * NB;
     const bool trsm = !(skip & 8);
     // DIAGNOSTIC (skip & 64, trial 0 only): per-phase s_memtime sums of waves 0 and 1 in
     // g_chol_clk[16 + 8 wave + phase] (timing only; results unchanged)
@@ -1224,13 +1002,6 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
     if (tid == 0) flag = 0;
     __syncthreads();
     stamp(0);
-    if (OV && wave != 0 && !(skip & 1)) {
-        // the rest of the pre-update (tiles 0-3 are done) beside wave 0's chain: wave w takes
-        // the tiles tau >= 4 it TRSMs against D_A below (tau = 1 + w mod 3), so its own loads
-        // of them need no barrier; Lp (swizzled, in Xs) stays intact until the next barrier
-        preupdate_tiles<G3, true>(R, L, jb, w2, wave == 3 ? 4 : wave + 4, 3, ntile, sm + kFacXs, li, lk);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // own stores before own reloads
-    }
     cd xv[4];
     // waves 1-3: their first row tile (A part) and y rows are in flight while wave 0 factors
     cd cur[4];
@@ -1267,7 +1038,7 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
         wave_sync();
         stamp(1);
         if (!(skip & 2)) {
-            factor_diag_lds<DM != 0, DM != 0, DM == 2>(X, wA, lane, tol, a.solve_mode, DiA, dinv, &flag,
+            factor_diag_lds(X, wA, lane, tol, a.solve_mode, DiA, dinv, &flag,
                             R + (size_t)jb * L + jb, L);
             forward_y_lds(DiA, ybA, y + jb * NR, wA, NR, lane);
         }
@@ -1308,7 +1079,7 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
             for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = csub_out<G3>(cre, cim, c2, q);
             wave_sync();
             if (!(skip & 2)) {
-                factor_diag_lds<DM != 0, DM != 0, DM == 2>(X, wB, lane, tol, a.solve_mode, DiB, dinv, &flag,
+                factor_diag_lds(X, wB, lane, tol, a.solve_mode, DiB, dinv, &flag,
                                 R + (size_t)jbB * L + jbB, L);
                 forward_y_lds(DiB, ybB, y + jbB * NR, wB, NR, lane);
             }
@@ -1377,32 +1148,19 @@ __device__ __forceinline__ void panel_factor_body(const MstepArgs& a, int L, int
 }
 
 // PRE (wide schedule, odd panels): the rank-32 update of the panel by the previous panel's
-// columns [jb-32, jb) (the part panel_update2_kernel left) inside the factor launch.
-// PRE 1: all of it first (panel_preupdate), then the factor.  PRE 2 (overlapped): each wave
-// pre-updates row tile `wave` (tiles 0 and 1 are the chain's), then wave 0 starts the diagonal
-// chain while waves 1-3 pre-update the remaining tiles (panel_factor_body<OV>): the chain is
-// VALU/LDS-latency bound, the pre-update MFMA bound, so the two share the CU's time.
-template <bool G3 = false, int PRE = 0, int DM = 1, bool CLK = false>
+// columns [jb-32, jb) (the part panel_update2_kernel left) inside the factor launch, first
+// (panel_preupdate), then the factor.
+template <bool G3 = false, bool PRE = false, bool CLK = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 void panel_factor_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip) {
-    __shared__ __attribute__((aligned(16))) cd sm[PRE == 2 ? kFacLdsOv : kFacLds];
+    __shared__ __attribute__((aligned(16))) cd sm[kFacLds];
     __shared__ double dinv[NB];
     __shared__ int flag;
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
     const unsigned long long t0 = CLK ? __builtin_amdgcn_s_memtime() : 0;   // diagnostic
-    if (PRE == 1 && !(skip & 1)) panel_preupdate<G3>(a, L, jb, ntile, b, sm);
-    if (PRE == 2 && !(skip & 1)) {
-        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-        const int w2 = (L - jb) < PW ? (L - jb) : PW;
-        cd* R = a.R + (size_t)b * L * L;
-        preupdate_stage<true>(R, L, jb, w2, sm + kFacXs);
-        __syncthreads();
-        preupdate_tiles<G3, true>(R, L, jb, w2, wave, 4, wave + 1 < ntile ? wave + 1 : ntile, sm + kFacXs,
-                                  lane & 15, lane >> 4);
-        // the body's first barrier publishes tiles 0-3
-    }
-    panel_factor_body<G3, DM, CLK, PRE == 2>(a, L, NR, jb, ntile, b, skip, sm, dinv, flag, t0);
+    if (PRE && !(skip & 1)) panel_preupdate<G3>(a, L, jb, ntile, b, sm);
+    panel_factor_body<G3, CLK>(a, L, NR, jb, ntile, b, skip, sm, dinv, flag, t0);
 }
 
 // ---------------------------------------------------------------- look-ahead panel step
@@ -1483,233 +1241,9 @@ __device__ __forceinline__ void panel_preupdate(const MstepArgs& a, int L, int j
     __syncthreads();
 }
 
-// One launch per panel j with two block roles (look-ahead): role F (one workgroup per trial)
-// applies panel j-1's rank-32 update to panel j and factors it (panel_factor_body); role U
-// (gptU four-tile groups per trial) updates panel j+1 by the columns [0, jb) -- everything
-// already factored.  The two roles touch disjoint columns, so the latency-bound diagonal
-// chains of F run beside U's MFMA streaming instead of in a launch of their own; a trial's
-// blocks are adjacent in dispatch order (F first) and sit on one XCD.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-void panel_la_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int gptU, int ntileU, int skip) {
-    __shared__ __attribute__((aligned(16))) cd sm[(PW * (KBU + 1)) > kFacLds ? (PW * (KBU + 1)) : kFacLds];
-    __shared__ double dinv[NB];
-    __shared__ int flag;
-    const int id = blockIdx.x, xcd = id & 7, k = id >> 3;
-    const int nT = (a.nbatch + 7) >> 3;                       // trials per XCD
-    // dispatch order per XCD: F and U blocks alternate until every F is out, then the rest of U
-    bool isF;
-    int it, grp = 0;
-    if (gptU == 0) { isF = true; it = k; }
-    else if (k < 2 * nT) {
-        isF = !(k & 1);
-        const int u = k >> 1;
-        it = isF ? u : u / gptU;
-        grp = isF ? 0 : u - (u / gptU) * gptU;
-    } else {
-        isF = false;
-        const int u = k - nT;
-        it = u / gptU;
-        grp = u - it * gptU;
-    }
-    const int b = it * 8 + xcd;
-    if (b >= a.nbatch) return;
-    if (a.done && a.done[b]) return;
-    if (!isF) {
-        panel_update_body<4>(a, L, jb + PW, jb, ntileU, b, grp, skip, sm);
-        return;
-    }
-    __builtin_amdgcn_s_setprio(2);                           // F before U; its chain wave first
-    if (jb > 0 && !(skip & 1)) panel_preupdate<false>(a, L, jb, ntile, b, sm);
-    panel_factor_body(a, L, NR, jb, ntile, b, skip, sm, dinv, flag);
-}
-
-// ---------------------------------------------------------------- fused panel step
-// panel_fused_kernel (panel jb > 0 with at most 16 row tiles): the panel update AND its factor
-// for one trial per workgroup of NWF waves, row tile tau owned by wave tau % NWF:
-//   U: C_tau = A[rows tau, jb:jb+32] - L[rows tau, 0:jb] L[jb:jb+32, 0:jb]^H into registers, the
-//      panel's top rows staged per KBU-column chunk in LDS by LDS-DMA once for all tiles;
-//   F: panel_factor_kernel's sequence on the register tiles: D_A (wave 0) and its y block, TRSM
-//      of every tile against it (row tile 1's X_A1 published), the in-panel update of the B
-//      halves, D_B (wave 1), TRSM of the B halves.
-// L is written once and the panel never makes the HBM round trip between an update and a factor
-// launch.  Measured slower at cfg1 (A/B only, SBCE_CHOL_IMPL=u): see launch_chol_batched.
-constexpr int NWF = 8;
-__global__ __launch_bounds__(64 * NWF) __attribute__((amdgpu_waves_per_eu(4)))
-void panel_fused_kernel(MstepArgs a, int L, int NR, int jb, int ntile, int skip) {
-    // Bp (update phase) and the waves' TRSM scratch (factor phase) share the LDS
-    __shared__ __attribute__((aligned(16))) cd smem_u[(PW * (KBU + 1)) > (NWF * NB * NB) ? (PW * (KBU + 1))
-                                                                                      : (NWF * NB * NB)];
-    __shared__ cd DiA[NB * NB], DiB[NB * NB], XA1[NB * NB];
-    __shared__ cd ybA[NB * 8], ybB[NB * 8];
-    __shared__ double dinv[NB];
-    __shared__ int flag;
-    cd* Bp = smem_u;
-    const int b = blockIdx.x;
-    if (a.done && a.done[b]) return;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int li = lane & 15, lk = lane >> 4;
-    const int w2 = (L - jb) < PW ? (L - jb) : PW;
-    const int wA = w2 < NB ? w2 : NB, wB = w2 - NB;
-    const int jbB = jb + NB;
-    const double tol = a.tol[b];
-    cd* R = a.R + (size_t)b * L * L;
-    cd* y = a.rhs + (size_t)b * L * NR;
-    if (tid == 0) flag = 0;
-    // ---- U: the two row tiles of this wave ----
-    d4v cre[2][2], cim[2][2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int tau = wave + NWF * u;
-        const int nv = tau == 0 ? 1 : 2;        // tile 0's right half: strict upper triangle
-#pragma unroll
-        for (int v = 0; v < 2; ++v) {
-            cre[u][v] = d4v{0.0, 0.0, 0.0, 0.0};
-            cim[u][v] = d4v{0.0, 0.0, 0.0, 0.0};
-            if (tau < ntile && v < nv) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int rr = jb + tau * NB + lk + 4 * q, c = 16 * v + li;
-                    if (rr < L && c < w2) {
-                        const cd x = R[(size_t)rr * L + jb + c];
-                        cre[u][v][q] = x.x;
-                        cim[u][v][q] = x.y;
-                    }
-                }
-            }
-        }
-    }
-    for (int kb0 = 0; kb0 < jb; kb0 += KBU) {
-        const int kbs = (jb - kb0) < KBU ? (jb - kb0) : KBU;        // multiple of 16
-        __syncthreads();
-        // panel top rows by LDS-DMA: wave w stages rows 4w .. 4w+3 (64 lanes = a row's KBU
-        // slots); lanes past kbs / rows past w2 read row jb
-#pragma unroll
-        for (int c4 = 0; c4 < PW / NWF; ++c4) {
-            const int c = wave * (PW / NWF) + c4;
-            const cd* src = R + (size_t)jb * L + kb0;
-            if (c < w2 && lane < kbs) src = R + (size_t)(jb + c) * L + kb0 + lane;
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                             (__attribute__((address_space(3))) void*)(Bp + c * (KBU + 1)),
-                                             16, 0, 0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int tau = wave + NWF * u;
-            if (tau >= ntile) continue;                          // wave-uniform
-            const int nv = tau == 0 ? 1 : 2;
-            int r = jb + tau * NB + li;
-            r = r < L ? r : L - 1;                               // rows past L: harmless reads
-            const cd* arow = R + (size_t)r * L + kb0 + lk;
-            cd av[4];
-#pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) av[s2] = arow[4 * s2];
-            for (int k0 = 0; k0 < kbs; k0 += 16) {
-                cd an[4];
-                const bool more = k0 + 16 < kbs;
-#pragma unroll
-                for (int s2 = 0; s2 < 4; ++s2) an[s2] = more ? arow[k0 + 16 + 4 * s2] : czero();
-#pragma unroll
-                for (int s2 = 0; s2 < 4; ++s2) {
-                    const cd v = av[s2];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        if (h >= nv) break;
-                        const cd t = Bp[(16 * h + li) * (KBU + 1) + k0 + 4 * s2 + lk];
-                        cre[u][h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre[u][h], 0, 0, 0);
-                        cre[u][h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre[u][h], 0, 0, 0);
-                        cim[u][h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim[u][h], 0, 0, 0);
-                        cim[u][h] = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim[u][h], 0, 0, 0);
-                    }
-                }
-#pragma unroll
-                for (int s2 = 0; s2 < 4; ++s2) av[s2] = an[s2];
-            }
-        }
-    }
-    // ---- F: the tiles' y rows in flight, then D_A (wave 0) ----
-    double ydA[2][4];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int tau = wave + NWF * u;
-        load_ycomp(y, L, NR, jb + tau * NB, li, lk, tau >= 1 && tau < ntile, ydA[u]);
-    }
-    __syncthreads();                                             // Bp reads done: scratch reuse
-    cd* X = smem_u + wave * NB * NB;
-    if (wave == 0) {
-        for (int e = lane; e < NB * NR; e += 64) ybA[e] = (e < wA * NR) ? y[jb * NR + e] : czero();
-#pragma unroll
-        for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = cmk(cre[0][0][q], cim[0][0][q]);
-        wave_sync();
-        factor_diag_lds(X, wA, lane, tol, a.solve_mode, DiA, dinv, &flag, R + (size_t)jb * L + jb, L);
-        forward_y_lds(DiA, ybA, y + jb * NR, wA, NR, lane);
-    }
-    __syncthreads();
-    // TRSM of the A halves; row tile 1 (= sub-panel B's rows) publishes X_A1 and stages its
-    // updated y rows in ybB
-    cd xv[2][4];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int tau = wave + NWF * u;
-        if (tau < 1 || tau >= ntile) continue;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = cmk(cre[u][0][q], cim[u][0][q]);
-        wave_sync();
-        trsm_tile16(R, y, DiA, X, ybA, L, NR, jb + tau * NB, jb, wA, li, lk, xv[u], ydA[u],
-                    tau == 1 ? ybB : nullptr);
-        if (tau == 1) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) XA1[li * NB + lk + 4 * q] = xv[u][q];
-        }
-        wave_sync();
-    }
-    __syncthreads();
-    // in-panel update of the B halves (tile 1's is B's diagonal block), D_B by wave 1
-    double ydB[2][4];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int tau = wave + NWF * u;
-        if (tau < 1 || tau >= ntile || wB <= 0) continue;
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-            const cd v = xv[u][s2], t = XA1[li * NB + 4 * s2 + lk];
-            cre[u][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.x, t.x, cre[u][1], 0, 0, 0);
-            cre[u][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.y, cre[u][1], 0, 0, 0);
-            cim[u][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(-v.y, t.x, cim[u][1], 0, 0, 0);
-            cim[u][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v.x, t.y, cim[u][1], 0, 0, 0);
-        }
-        // the y rows after the A update (this lane wrote them), for the B TRSM
-        load_ycomp(y, L, NR, jb + tau * NB, li, lk, tau >= 2, ydB[u]);
-    }
-    if (wave == 1 && wB > 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = cmk(cre[0][1][q], cim[0][1][q]);
-        wave_sync();
-        factor_diag_lds(X, wB, lane, tol, a.solve_mode, DiB, dinv, &flag, R + (size_t)jbB * L + jbB, L);
-        forward_y_lds(DiB, ybB, y + jbB * NR, wB, NR, lane);
-    }
-    __syncthreads();
-    if (wB > 0) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int tau = wave + NWF * u;
-            if (tau < 2 || tau >= ntile) continue;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) X[(lk + 4 * q) * NB + li] = cmk(cre[u][1][q], cim[u][1][q]);
-            wave_sync();
-            cd xb[4];
-            trsm_tile16(R, y, DiB, X, ybB, L, NR, jb + tau * NB, jbB, wB, li, lk, xb, ydB[u]);
-            wave_sync();
-        }
-    }
-    const int st = ((flag & 1) ? a.clamp_status : 0) | ((flag & 2) ? SBCE_STATUS_RANK : 0) |
-                   ((skip & 31) ? SBCE_STATUS_DEBUG : 0);
-    if (tid == 0 && st && a.status) atomicOr(&a.status[b], st);
-}
-
-// Back substitution L^H x = y (y staged in LDS) and theta = conj(x), one workgroup per trial.
+// ---------------------------------------------------------------- back substitution
+// General blocked back substitution L^H x = y (any L <= 512, any NR; SBCE_BACKSUB=1 forces it
+// for the shapes backsub4_kernel covers, as a cross-check), theta = conj(x).
 __global__ __launch_bounds__(256) void backsub_kernel(MstepArgs a, int L, int NR, int skip) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     cd* y = reinterpret_cast<cd*>(smem);
@@ -1727,91 +1261,12 @@ __global__ __launch_bounds__(256) void backsub_kernel(MstepArgs a, int L, int NR
     for (int e = tid; e < L * NR; e += nth) th[e] = cconj(y[e]);
 }
 
-// Back substitution for L <= 272 (every update column k < k0 <= 256 has one owner thread):
-// the 16 factor entries of block kb-2 are loaded while block kb is solved and applied, so
-// each block step waits on a load issued two steps earlier (two register buffers, the loop
-// unrolled by two so the buffers never need dynamic indexing); the diagonal blocks follow
-// the same two-ahead schedule.
-__device__ __forceinline__ void bs2_load(const cd* R, int L, int kb, int tid, cd* lv) {
-    const int k0 = kb * NB, w = (L - k0) < NB ? (L - k0) : NB;
-#pragma unroll
-    for (int c = 0; c < NB; ++c)
-        lv[c] = (kb >= 0 && tid < k0 && c < w) ? R[(size_t)(k0 + c) * L + tid] : czero();
-}
-__device__ __forceinline__ cd bs2_dload(const cd* R, int L, int kb, int tid) {
-    const int k0 = kb * NB, w = (L - k0) < NB ? (L - k0) : NB;
-    const int c = tid >> 4, c2 = tid & 15;
-    return (kb >= 0 && c < w && c2 < w && c2 >= c) ? R[(size_t)(k0 + c) * L + k0 + c2] : czero();
-}
-// one block step: publish the diagonal block d, solve it (wave 0), apply it to rows k < k0
-__device__ __forceinline__ void bs2_step(cd* y, cd* dblk, int L, int NR, int kb, int tid, int lane,
-                                         int wave, cd d, const cd* lv) {
-    const int k0 = kb * NB, w = (L - k0) < NB ? (L - k0) : NB;
-    dblk[tid] = d;
-    __syncthreads();
-    if (wave == 0) {
-        // x_blk = D^{-H} z_blk:  x[c] = z[c] / L[c][c] + sum_{c2>c} conj(Di[c2][c]) z[c2]
-        cd t0 = czero();
-        if (lane < w * NR) {
-            const int c = lane / NR, r = lane - c * NR;
-            const cd* Rc = dblk + c * NB;
-            const double lcc = Rc[c].x;
-            t0 = (lcc > 0.0) ? cscale(y[(k0 + c) * NR + r], 1.0 / lcc) : czero();
-            for (int c2 = c + 1; c2 < w; ++c2) t0 = cfma(t0, Rc[c2], y[(k0 + c2) * NR + r]);
-        }
-        wave_sync();
-        if (lane < w * NR) y[k0 * NR + lane] = t0;
-    }
-    __syncthreads();
-    if (tid < k0) {
-        for (int r = 0; r < NR; ++r) {
-            cd acc = y[tid * NR + r];
-#pragma unroll
-            for (int c = 0; c < NB; ++c)
-                if (c < w) acc = csub(acc, cmulc(y[(k0 + c) * NR + r], lv[c]));
-            y[tid * NR + r] = acc;
-        }
-    }
-    __syncthreads();
-}
-__global__ __launch_bounds__(256) void backsub2_kernel(MstepArgs a, int L, int NR) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    cd* y = reinterpret_cast<cd*>(smem);
-    cd* dblk = y + L * NR;
-    const int b = blockIdx.x;
-    if (a.done && a.done[b]) return;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const cd* R = a.R + (size_t)b * L * L;
-    const cd* yg = a.rhs + (size_t)b * L * NR;
-    const int nblk = (L + NB - 1) / NB;
-    cd lvA[NB], lvB[NB];
-    bs2_load(R, L, nblk - 1, tid, lvA);
-    cd dA = bs2_dload(R, L, nblk - 1, tid);
-    bs2_load(R, L, nblk - 2, tid, lvB);
-    cd dB = bs2_dload(R, L, nblk - 2, tid);
-    for (int e = tid; e < L * NR; e += 256) y[e] = yg[e];
-    for (int kb = nblk - 1; kb >= 0; kb -= 2) {
-        bs2_step(y, dblk, L, NR, kb, tid, lane, wave, dA, lvA);
-        bs2_load(R, L, kb - 2, tid, lvA);
-        dA = bs2_dload(R, L, kb - 2, tid);
-        if (kb - 1 < 0) break;
-        bs2_step(y, dblk, L, NR, kb - 1, tid, lane, wave, dB, lvB);
-        bs2_load(R, L, kb - 3, tid, lvB);
-        dB = bs2_dload(R, L, kb - 3, tid);
-    }
-    cd* th = a.theta + (size_t)b * L * NR;
-    for (int e = tid; e < L * NR; e += 256) th[e] = cconj(y[e]);
-}
-
-// Back substitution for L <= 272, NR <= 4 with ONE barrier per 16-column block step (the
-// two-ahead kernel above pays three).  Thread tid owns row k = tid < 256 of y in registers
-// (rows of the last block past 255 are only ever read, from the input).  Every
-// wave solves the block x = D^{-H} z itself (lane c*NR + r: output (c, r)) into a
-// wave-private LDS copy, so the update of the wave's own rows needs no workgroup barrier; the
-// owners of the next block's rows then publish them, every thread publishes its entry of the
-// next diagonal block (L_cc, conj(Di[c2][c]) above the diagonal; loaded two steps ahead with
-// its update column), both double-buffered in LDS, and the workgroup synchronises once.
+// Back substitution block step shared by backsub4_kernel: thread tid owns row k = tid < 256 of
+// y in registers; every wave solves the block x = D^{-H} z itself (lane c*NR + r: output (c, r))
+// into a wave-private LDS copy, so the update of the wave's own rows needs no workgroup barrier;
+// the owners of the next block's rows then publish them, every thread publishes its entry of the
+// next diagonal block (L_cc, conj(Di[c2][c]) above the diagonal), both double-buffered in LDS,
+// and the workgroup synchronises once per block.
 struct Bs3Buf {
     cd lv[NB];         // L[k0 + cc][tid], this thread's update column
     cd dd;             // entry (tid >> 4, tid & 15) of the diagonal block
@@ -1858,41 +1313,6 @@ __device__ __forceinline__ void bs3_step(int kb, int L, int tid, int lane, int w
         db[(kb - 1) & 1][tid] = dnext;
     }
     __syncthreads();
-}
-template <int NR>
-__global__ __launch_bounds__(256) void backsub3_kernel(MstepArgs a, int L) {
-    __shared__ cd zb[2][NB * NR];              // the current / next block's z rows
-    __shared__ cd db[2][NB * NB];              // the current / next diagonal block
-    __shared__ cd xw[4][NB * NR];              // per-wave block solution
-    const int b = blockIdx.x;
-    if (a.done && a.done[b]) return;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const cd* R = a.R + (size_t)b * L * L;
-    const cd* yg = a.rhs + (size_t)b * L * NR;
-    cd* th = a.theta + (size_t)b * L * NR;
-    const int nblk = (L + NB - 1) / NB;
-    const int c = lane / NR, r = lane - (lane / NR) * NR;     // block-solve output of this lane
-    cd yr[NR];                                                 // row k = tid of y
-#pragma unroll
-    for (int q = 0; q < NR; ++q) yr[q] = tid < L ? yg[(size_t)tid * NR + q] : czero();
-    Bs3Buf bA, bB;
-    bs3_load(R, L, nblk - 1, tid, bA);
-    bs3_load(R, L, nblk - 2, tid, bB);
-    {
-        // the last block's rows (k0 may be 256: no owner thread) straight from the input
-        const int k0 = (nblk - 1) * NB, w = L - k0;
-        if (tid < w * NR) zb[(nblk - 1) & 1][tid] = yg[(size_t)k0 * NR + tid];
-        db[(nblk - 1) & 1][tid] = bA.dd;
-    }
-    __syncthreads();
-    for (int kb = nblk - 1; kb >= 0; kb -= 2) {
-        bs3_step<NR>(kb, L, tid, lane, wave, c, r, bA, bB.dd, yr, zb, db, xw, th);
-        bs3_load(R, L, kb - 2, tid, bA);
-        if (kb - 1 < 0) break;
-        bs3_step<NR>(kb - 1, L, tid, lane, wave, c, r, bB, bA.dd, yr, zb, db, xw, th);
-        bs3_load(R, L, kb - 3, tid, bB);
-    }
 }
 
 // The same one-barrier block step with the factor entries loaded ONE step ahead into a single
@@ -1988,32 +1408,13 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
     hipError_t e = launch_diag_tol(pb, a, s);
     if (e != hipSuccess) return e;
     const int npan = (pb.L + PW - 1) / PW;
-    const int upd_waves = g_debug.upd_waves8 ? 8 : 4;
-    const bool lookahead = g_debug.chol_impl == 'l';   // A/B only: measured slower
-    if (lookahead) {
-        // look-ahead steps: launch j factors panel j and updates panel j+1 by panels 0..j-1
-        for (int j = 0; j < npan; ++j) {
-            const int jb = j * PW;
-            const int rem = (pb.L - jb + NB - 1) / NB;
-            const int remU = j + 1 < npan ? (pb.L - jb - PW + NB - 1) / NB : 0;
-            const int gptU = (jb > 0 && remU > 0) ? (remU + 3) / 4 : 0;
-            const long nblk = 8L * ((pb.B + 7) / 8) * (1 + gptU);
-            hipLaunchKernelGGL(panel_la_kernel, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L, pb.NR, jb,
-                               rem, gptU, remU, skip);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-        }
-    }
-    // default (round 4): the wide schedule -- even panels j >= 2 update panels j and j+1 by
-    // [0, jb) in one launch (panel_update2_kernel), odd panels are pre-updated by panel j-1 inside
-    // their factor launch: half the left-looking HBM re-reads (cfg1 M-step 2.32 -> 2.25 ms, EM
-    // +1.8 % at three streams).  SBCE_CHOL_IMPL=n: one update launch per 32-column panel;
-    // SBCE_CHOL_IMPL=s: the odd pre-update as a launch of its own (panel_preupd_kernel; measured
-    // M-step 2.32 vs 2.30 ms in-factor) -- both A/B only.
-    const bool wide = g_debug.chol_impl == 0 || g_debug.chol_impl == 's' || g_debug.chol_impl == 'o';
-    for (int j = 0; j < npan && wide; ++j) {
+    // the wide schedule: even panels j >= 2 update panels j and j+1 by [0, jb) in one launch
+    // (panel_update2_kernel), odd panels are pre-updated by panel j-1 inside their factor launch:
+    // half the left-looking HBM re-reads of one update launch per panel
+    const bool g3 = g_debug.cplx3 && a.solve_mode == SBCE_SOLVE_CHOL;
+    for (int j = 0; j < npan; ++j) {
         const int jb = j * PW;
         const int rem = (pb.L - jb + NB - 1) / NB;
-        const bool g3 = g_debug.cplx3 && a.solve_mode == SBCE_SOLVE_CHOL;
         if (j >= 2 && !(j & 1)) {
             ct_begin(s, 0);
             const int gpt0 = (rem + 3) / 4;
@@ -2027,40 +1428,14 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
                                    jb, rem, gpt0, gpt1, skip);
             ct_end(s);
         }
-        const bool pre = (j & 1) != 0 && g_debug.chol_impl != 's';
-        if ((j & 1) && !pre) {
-            const int gpt = (rem + 3) / 4;
-            const long nblk = 8L * ((pb.B + 7) / 8) * gpt;
-            if (g3)
-                hipLaunchKernelGGL(panel_preupd_kernel<true>, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L,
-                                   jb, rem, gpt, skip);
-            else
-                hipLaunchKernelGGL(panel_preupd_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L,
-                                   jb, rem, gpt, skip);
-        }
-        // SBCE_CHOL_INV=loop: the row-recurrence inverse, =pair: two columns per step (A/B)
+        const bool pre = (j & 1) != 0;
         ct_begin(s, 1);
-        if (g3 && pre && g_debug.chol_inv == 'l')
-            hipLaunchKernelGGL((panel_factor_kernel<true, true, 0>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
-                               pb.NR, jb, rem, skip);
-        else if (g3 && g_debug.chol_inv == 'l')
-            hipLaunchKernelGGL((panel_factor_kernel<true, false, 0>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
-                               pb.NR, jb, rem, skip);
-        else if (g3 && pre && g_debug.chol_inv == 'p')
-            hipLaunchKernelGGL((panel_factor_kernel<true, true, 2>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
-                               pb.NR, jb, rem, skip);
-        else if (g3 && g_debug.chol_inv == 'p')
-            hipLaunchKernelGGL((panel_factor_kernel<true, false, 2>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
-                               pb.NR, jb, rem, skip);
-        else if (g3 && pre && (skip & 64))         // DIAGNOSTIC phase clocks (tools/chol_clock.py)
-            hipLaunchKernelGGL((panel_factor_kernel<true, true, 1, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
+        if (g3 && pre && (skip & 64))               // DIAGNOSTIC phase clocks (tools/chol_clock.py)
+            hipLaunchKernelGGL((panel_factor_kernel<true, true, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
                                pb.NR, jb, rem, skip);
         else if (g3 && (skip & 64))
-            hipLaunchKernelGGL((panel_factor_kernel<true, false, 1, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
+            hipLaunchKernelGGL((panel_factor_kernel<true, false, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L,
                                pb.NR, jb, rem, skip);
-        else if (g3 && pre && g_debug.chol_impl == 'o')
-            hipLaunchKernelGGL((panel_factor_kernel<true, 2>), dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR,
-                               jb, rem, skip);
         else if (g3 && pre)
             hipLaunchKernelGGL((panel_factor_kernel<true, true>), dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR,
                                jb, rem, skip);
@@ -2076,71 +1451,17 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
         ct_end(s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    for (int j = 0; j < npan && !lookahead && !wide; ++j) {
-        const int jb = j * PW;
-        const int rem = (pb.L - jb + NB - 1) / NB;               // 16-row tiles from jb
-        // SBCE_CHOL_IMPL=u (A/B runs): update and factor of a panel of at most 16 row tiles in
-        // one launch -- 8-17 % slower per panel at cfg1: a trial's register-resident panel
-        // (128 KB) allows two trials per CU, so the 1000 trials take two rounds and each pays
-        // the serial diagonal chain the separate factor launch runs once for all of them
-        if (j > 0 && rem <= 2 * NWF && pb.NR <= 8 && g_debug.chol_impl == 'u') {
-            hipLaunchKernelGGL(panel_fused_kernel, dim3(pb.B), dim3(64 * NWF), 0, s, a, pb.L, pb.NR,
-                               jb, rem, skip);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-            continue;
-        }
-        if (j > 0) {
-            // four-tile blocks; SBCE_UPD_WAVES=8: eight-tile blocks (A/B runs: 4 % slower at
-            // cfg1 -- the panel rows' re-reads by the blocks of a trial are L2 hits)
-            if (upd_waves == 4) {
-                const int gpt = (rem + 3) / 4;
-                const long nblk = 8L * ((pb.B + 7) / 8) * gpt;
-                if (g_debug.cplx3 && a.solve_mode == SBCE_SOLVE_CHOL)
-                    hipLaunchKernelGGL((panel_update_kernel<4, true>), dim3((unsigned)nblk), dim3(256), 0, s,
-                                       a, pb.L, jb, rem, gpt, skip);
-                else
-                    hipLaunchKernelGGL((panel_update_kernel<4, false>), dim3((unsigned)nblk), dim3(256), 0, s,
-                                       a, pb.L, jb, rem, gpt, skip);
-            } else {
-                const int gpt = (rem + 7) / 8;
-                const long nblk = 8L * ((pb.B + 7) / 8) * gpt;
-                hipLaunchKernelGGL(panel_update_kernel<8>, dim3((unsigned)nblk), dim3(512), 0, s, a,
-                                   pb.L, jb, rem, gpt, skip);
-            }
-        }
-        if (g_debug.cplx3 && a.solve_mode == SBCE_SOLVE_CHOL)
-            hipLaunchKernelGGL(panel_factor_kernel<true>, dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR, jb,
-                               rem, skip);
-        else
-            hipLaunchKernelGGL(panel_factor_kernel<false>, dim3(pb.B), dim3(256), 0, s, a, pb.L, pb.NR, jb,
-                               rem, skip);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
-    // default: one-buffer one-barrier kernel (backsub4); SBCE_BACKSUB=3 the two-buffer one-barrier
-    // kernel, =2 the two-ahead three-barrier kernel, =1 the one-step-prefetch kernel (A/B runs)
-    const int bsv = g_debug.backsub;
-    if (pb.L <= 272 && pb.NR <= 4 && bsv == 0 && !(skip & 16)) {
+    // default (L <= 272, NR <= 4): the one-buffer one-barrier kernel; otherwise, or with
+    // SBCE_BACKSUB=1 (cross-check), the general kernel
+    if (pb.L <= 272 && pb.NR <= 4 && !g_debug.backsub_general && !(skip & 16)) {
+        ct_begin(s, 2);
         switch (pb.NR) {
-            case 1: ct_begin(s, 2); hipLaunchKernelGGL(backsub4_kernel<1>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
-            case 2: ct_begin(s, 2); hipLaunchKernelGGL(backsub4_kernel<2>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
-            case 3: ct_begin(s, 2); hipLaunchKernelGGL(backsub4_kernel<3>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
-            default: ct_begin(s, 2); hipLaunchKernelGGL(backsub4_kernel<4>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+            case 1: hipLaunchKernelGGL(backsub4_kernel<1>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+            case 2: hipLaunchKernelGGL(backsub4_kernel<2>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+            case 3: hipLaunchKernelGGL(backsub4_kernel<3>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
+            default: hipLaunchKernelGGL(backsub4_kernel<4>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
         }
         ct_end(s);
-        return hipGetLastError();
-    }
-    if (pb.L <= 272 && pb.NR <= 4 && bsv == 3 && !(skip & 16)) {
-        switch (pb.NR) {
-            case 1: hipLaunchKernelGGL(backsub3_kernel<1>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
-            case 2: hipLaunchKernelGGL(backsub3_kernel<2>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
-            case 3: hipLaunchKernelGGL(backsub3_kernel<3>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
-            default: hipLaunchKernelGGL(backsub3_kernel<4>, dim3(pb.B), dim3(256), 0, s, a, pb.L); break;
-        }
-        return hipGetLastError();
-    }
-    if (pb.L <= 272 && pb.NR <= 4 && bsv != 1 && !(skip & 16)) {
-        hipLaunchKernelGGL(backsub2_kernel, dim3(pb.B), dim3(256),
-                           ((size_t)pb.L * pb.NR + NB * NB) * sizeof(cd), s, a, pb.L, pb.NR);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(backsub_kernel, dim3(pb.B), dim3(256),
@@ -2165,42 +1486,6 @@ hipError_t launch_y(const Problem& pb, const MstepArgs& a, int nth, int rpt, siz
         case 2: return launch_rpt<2, YLDS>(pb, a, nth, lds, s);
     }
     return hipErrorInvalidValue;
-}
-
-template <bool YLDS, int NWB, int KB>
-hipError_t launch_mfma_cfg(const Problem& pb, const MstepArgs& a, int nw, int maxt, size_t lds,
-                           hipStream_t s) {
-    const int skip = g_chol_skip;                   // diagnostic only (see kernel)
-    const dim3 g(pb.B), blk(64 * nw);
-    CholGeom geo;
-    geo.ld = pb.L; geo.off = 0; geo.stride = (size_t)pb.L * pb.L; geo.tolp = nullptr; geo.ext = nullptr;
-#define SBCE_CM(t)                                                                                \
-    case t:                                                                                       \
-        hipLaunchKernelGGL((chol_mfma_kernel<t, YLDS, NWB, KB>), g, blk, lds, s, a, pb.L, pb.NR,  \
-                           skip, geo);                                                            \
-        break;
-    switch (maxt) {
-        SBCE_CM(1) SBCE_CM(2) SBCE_CM(3) SBCE_CM(4) SBCE_CM(5)
-        default: return hipErrorInvalidValue;
-    }
-#undef SBCE_CM
-    return hipGetLastError();
-}
-
-// Geometry: L <= 320 -> 4-wave workgroups (two trials resident per CU, so one trial's serial
-// diagonal-block phase overlaps the other's MFMA update), up to 5 tiles per wave, 128-column
-// k-blocks; 320 < L <= 512 -> 8 waves, up to 4 tiles per wave, 256-column k-blocks.
-template <bool YLDS>
-hipError_t launch_mfma(const Problem& pb, const MstepArgs& a, size_t ybytes, hipStream_t s) {
-    const int ntile = (pb.L + NB - 1) / NB;
-    const bool small = ntile <= 20;
-    const int nwb = small ? 4 : 8, kb = small ? 128 : 256;
-    const int nw = ntile < nwb ? ntile : nwb;
-    const int maxt = (ntile + nw - 1) / nw;
-    const size_t lds = (size_t)(NB * (kb + 1) + NB * NB + nw * NB * NB) * sizeof(cd) +
-                       18 * sizeof(double) + (YLDS ? ybytes : 0);
-    if (small) return launch_mfma_cfg<YLDS, 4, 128>(pb, a, nw, maxt, lds, s);
-    return launch_mfma_cfg<YLDS, 8, 256>(pb, a, nw, maxt, lds, s);
 }
 
 }  // namespace
@@ -2265,17 +1550,10 @@ hipError_t launch_chol_tile(const Problem& pb, const MstepArgs& a, int k0, int w
 hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s) {
     if (!chol_supported(pb)) return hipErrorInvalidValue;
     if (a.solve_mode == SBCE_SOLVE_MINNORM) return launch_minnorm(pb, a, s);
-    const char impl = g_debug.chol_impl;            // 'v' VALU kernel, 'f' fused (A/B runs)
-    if (pb.L > kLargeL && !(impl == 'v' && pb.L <= 1024)) return launch_chol_large(pb, a, s);
+    const bool force_valu = g_debug.chol_valu;       // SBCE_CHOL_IMPL=valu: VALU cross-check
+    if (pb.L > kLargeL && !(force_valu && pb.L <= 1024)) return launch_chol_large(pb, a, s);
     const size_t ybytes = (size_t)pb.L * pb.NR * sizeof(cd);
-    const bool force_valu = impl == 'v';
-    if (!force_valu && pb.L <= 512) {
-        // default: batched panel launches; SBCE_CHOL_IMPL=fused keeps the one-workgroup-per-
-        // trial kernel (A/B runs)
-        if (impl != 'f') return launch_chol_batched(pb, a, s);
-        if (ybytes <= 24 * 1024) return launch_mfma<true>(pb, a, ybytes, s);
-        return launch_mfma<false>(pb, a, ybytes, s);
-    }
+    if (!force_valu) return launch_chol_batched(pb, a, s);   // batched panel launches
     int nth = (pb.L + 63) / 64 * 64;
     if (nth > 512) nth = 512;
     const int rpt = (pb.L + nth - 1) / nth;

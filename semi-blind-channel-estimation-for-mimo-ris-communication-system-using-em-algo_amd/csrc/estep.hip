@@ -2252,9 +2252,9 @@ bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     c.prep_stride = c.rowb_off + (pb.NT == 4 ? 6 * pb.NR : 0);
     c.rec_words = c.prep_stride + 2 * pb.NR;
     c.tab_d = mfma_tab_d(NO, c.chunk, steps, pb.M, c.nkt_pad, c.rec_words);
-    c.spw = g_debug.estep_spw;                           // symbols per wave (A/B runs)
+    c.spw = 4;                                           // symbols per wave
     c.screen = !g_debug.estep_nof32;                     // FP32 tile-group screen (V16)
-    c.rowb = pb.NT == 4 && c.prune && !g_debug.estep_norowb;
+    c.rowb = pb.NT == 4 && c.prune;
     lds = 64 * sizeof(cd) + (size_t)kMfmaWaves * c.tab_d * sizeof(double);
     const long nsym = (long)pb.B * pb.Td;
     const long per_block = (long)kMfmaWaves * c.spw;
@@ -2447,7 +2447,7 @@ hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStre
             PrepConst pc;
             pc.B = pb.B; pc.Td = pb.Td; pc.P = pb.P; pc.M = pb.M; pc.lm = mc.lm;
             pc.nkt = mc.JB >> 4; pc.stride = mc.prep_stride; pc.reg = mc.reg;
-            pc.uni = !g_debug.prep_nouni;
+            pc.uni = 1;
             // sphere pass instead of the preparation pass (SBCE_ESTEP_SPHERE=0 disables: A/B);
             // n_rx < n_tx (singular H^H H) always leaves the symbol to the sweep: not compiled
             const bool sphere = a.list && a.tree && pb.NR >= pb.NT && !g_debug.estep_nosphere;

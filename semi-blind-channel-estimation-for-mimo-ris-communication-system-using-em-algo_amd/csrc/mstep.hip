@@ -532,14 +532,13 @@ hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a0, hipStream_
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const char rimpl = g_debug.rhs_impl;                // 'r': thread-per-row kernel (A/B)
-    if (pb.L <= 512 && rimpl != 'r') {
+    if (pb.L <= 512) {
         const int nth = (pb.L + 63) / 64 * 64;
         const int tcr = pb.P <= 128 ? 16 : 4;             // <= 33 KB of phases per chunk
         const size_t lds = (size_t)tcr * (pb.P + pb.NT + pb.NR) * sizeof(cd);
-        // default: LDS-DMA double-buffered chunks when two buffers fit 64 KB (cfg1: 37 KB);
-        // SBCE_RHS_IMPL=lds keeps the single-buffer kernel (A/B runs)
-        if (2 * lds <= 64 * 1024 && rimpl != 'l') {
+        // LDS-DMA double-buffered chunks when two buffers fit 64 KB (cfg1: 37 KB), else the
+        // single-buffer kernel
+        if (2 * lds <= 64 * 1024) {
             switch (pb.NR) {
 #define SBCE_RHSD(n) case n: hipLaunchKernelGGL(rhs_dma_kernel<n>, dim3(pb.B), dim3(nth), 2 * lds, s, a, pb.P, pb.NT, pb.Tp, pb.Td, pb.L, tcr); break;
                 SBCE_RHSD(1) SBCE_RHSD(2) SBCE_RHSD(3) SBCE_RHSD(4) SBCE_RHSD(5) SBCE_RHSD(6) SBCE_RHSD(7) SBCE_RHSD(8)

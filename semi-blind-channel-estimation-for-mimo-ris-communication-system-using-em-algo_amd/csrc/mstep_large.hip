@@ -789,9 +789,8 @@ hipError_t launch_rbuild_herm(const Problem& pb, const MstepArgs& a, hipStream_t
         const int smax = pb.P < 257 ? pb.P : 257;
         // 16-symbol chunks (19 KB of LDS per block: more resident blocks per CU); measured
         // at cfg1 against 8 / 32 / 64 and 2 / 6 / 8 tiles per wave: 16 x 4 and 16 x 6 lead by
-        // ~2 % of the M-step.  SBCE_RB_TC=32: the previous 32-symbol chunks (A/B runs)
-        if (smax <= 68 && !g_debug.rb_tc32) return launch_herm<4, 4, 16, 68>(pb, a, smax, s);
-        if (smax <= 68) return launch_herm<4, 4, 32, 68>(pb, a, smax, s);
+        // ~2 % of the M-step
+        if (smax <= 68) return launch_herm<4, 4, 16, 68>(pb, a, smax, s);
         return smax <= 130 ? launch_herm<4, 4, 32, 0>(pb, a, smax, s)
                            : launch_herm<4, 4, 8, 0>(pb, a, smax, s);
     }
