@@ -81,10 +81,8 @@ def metric_name(n_tx, N, T_p, T_d):
 ESTEP_KERNELS = ["estep_tree_kernel", "estep_bfs_kernel", "estep_pair_kernel", "estep_bounds_kernel", "estep_prep_kernel",
                  "estep_mfma_kernel_occ3", "estep_mfma_kernel"]
 MSTEP_KERNELS = ["pilot_factor_kernel", "pilot_rhs_kernel", "rbuild_herm_kernel", "rbuild_kernel", "rhs_lds_kernel",
-                 "rhs_dma_kernel", "rhs_kernel", "diag_tol_kernel", "panel_update_kernel",
-                 "panel_update2_kernel", "panel_factor_kernel",
-                 "backsub_kernel", "backsub2_kernel", "backsub3_kernel",
-                 "backsub4_kernel", "chol_mfma_kernel"]
+                 "rhs_dma_kernel", "rhs_kernel", "diag_tol_kernel", "panel_update2_kernel",
+                 "panel_factor_kernel", "backsub_kernel", "backsub4_kernel"]
 MSTEP_KERNELS_LARGE = ["pilot_factor_kernel", "pilot_rhs_kernel", "rbuild_herm_kernel",
                        "rbuild_wide_kernel", "rhs_kernel", "rhs_dma_kernel", "rhs_lds_kernel",
                        "diag_tol_kernel", "chol_mfma_kernel", "tile_inverse_kernel",
@@ -98,8 +96,8 @@ MSTEP_KERNELS_LARGE = ["pilot_factor_kernel", "pilot_rhs_kernel", "rbuild_herm_k
 # over the run's M-steps)
 MSTEP_ANCHORS = ["diag_tol_kernel", "lanczos_tol_kernel"]   # once per full M-step solve
 # the L <= 512 Cholesky solve's launches (csrc/chol.hip; diag_tol_kernel runs once per M-step)
-CHOL_KERNELS = ["diag_tol_kernel", "panel_update_kernel", "panel_update2_kernel", "panel_factor_kernel",
-                "backsub4_kernel", "backsub3_kernel", "backsub2_kernel", "backsub_kernel"]
+CHOL_KERNELS = ["diag_tol_kernel", "panel_update2_kernel", "panel_factor_kernel", "backsub4_kernel",
+                "backsub_kernel"]
 CHOL_ANCHORS = ["diag_tol_kernel"]
 
 
@@ -761,6 +759,9 @@ def main(argv=None):
     e1.record(stream)
     torch.cuda.synchronize()
     mstep_ms = e0.elapsed_time(e1) / args.kernel_reps
+    # the min-norm solve's per-trial extent / rank / refinement, read from the workspace of the
+    # M-step just timed (the R-build timings below overwrite R, where G lives)
+    rk = eng.minnorm_rank() if solve == "lstsq" else None
 
     # ---- dominant kernel: the R build (rbuild_herm_kernel, n_tx in {4, 8}) timed alone ----
     rb_ms = None
@@ -811,7 +812,6 @@ def main(argv=None):
         # the min-norm factorisation stops at R's numerical rank (left-looking, minnorm.hip):
         # priced per trial at the extent it reached (the last timed M-step's workspace)
         L_ = (N + 1) * n_tx
-        rk = eng.minnorm_rank()
         mn = sum(minnorm_flops_per_trial(L_, n_rx, int(a_), int(r_)) for a_, _, r_ in rk)
         mflops = (rbuild_flops_per_trial_iter(n_tx, N, T_p, T_d) + 8 * n_rx * L_ * (T_d + T_p)) * B + mn
         mn_stats = {"extent_mean": float(rk[:, 0].mean()), "rank_mean": float(rk[:, 1].mean()),

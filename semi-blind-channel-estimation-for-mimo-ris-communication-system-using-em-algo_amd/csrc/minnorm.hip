@@ -535,7 +535,9 @@ __global__ __launch_bounds__(256) void gz_kernel(MstepArgs a, int L, int NR, int
 // Refinement gate: C = F F^H's conditioning from F's diagonal over the kept columns of G.  The
 // first solve's relative error grows like eps cond(C) (times a modest factor: 6e-5 measured at
 // cond 9e8, tools/rank_study.py); trials with max/min F_kk^2 below 1e4 are already at the
-// rounding level and skip the refinement step (skip[b] = 1, also for trials already done).
+// rounding level and skip the refinement step (skip[b] = 1, also for trials already done).  The
+// diagonal ratio only bounds cond(C) from below, so a trial flagged SBCE_STATUS_RANK (a clamped
+// pivot of C, or a pivot of R near the cut, in this call) is refined whatever its ratio.
 __global__ __launch_bounds__(256) void mn_gate_kernel(MstepArgs a, int L) {
     const int b = blockIdx.x;
     __shared__ double red[4];
@@ -557,7 +559,8 @@ __global__ __launch_bounds__(256) void mn_gate_kernel(MstepArgs a, int L) {
     mx = block_max(mx, red);
     __syncthreads();
     mn = -block_max(-mn, red);
-    if (threadIdx.x == 0) a.mnskip[b] = (act == 0 || mn * 1e4 >= mx) ? 1 : 0;
+    const bool flagged = a.status && (a.status[b] & SBCE_STATUS_RANK);
+    if (threadIdx.x == 0) a.mnskip[b] = (act == 0 || (!flagged && mn * 1e4 >= mx)) ? 1 : 0;
 }
 
 // DIAGNOSTIC (bench.py's executed-flop count): per trial the active extent act[b] the rank-cut

@@ -641,6 +641,7 @@ class EMEngine:
                               self.x_sup.data_ptr() if self.x_sup is not None else None,
                               self.varn_t.data_ptr() if self.varn_t is not None else None)
         self.subs = []
+        self._minnorm_ws = False        # the workspace holds a whole-batch min-norm M-step
         if sub:
             off = 0
             for (b0, b1), dims, nb in zip(zip(bounds[:-1], bounds[1:]), sub_dims, sub_bytes):
@@ -658,6 +659,8 @@ class EMEngine:
     def run(self, itera, stream=None):
         """One full EM (itera iterations) over the whole batch, stream-ordered on `stream`
         (default: the current stream)."""
+        # with stream sub-batches the workspace holds their layouts, not the whole batch's
+        self._minnorm_ws = not self.subs and self.solve == _lib.SBCE_SOLVE_MINNORM
         cur = self.torch.cuda.current_stream() if stream is None else stream
         with self.torch.cuda.stream(cur):
             self.theta.copy_(self.theta0)
@@ -687,10 +690,12 @@ class EMEngine:
         rc = self.lib.sbce_mstep(self.dims, self.ptrs, self.mom.data_ptr(), self.solve, None,
                                  None, self.torch.cuda.current_stream().cuda_stream)
         _lib.check(rc, "sbce_mstep")
+        self._minnorm_ws = self.solve == _lib.SBCE_SOLVE_MINNORM
 
     def mstep_phase(self, phase):
         """One piece of the M-step from the last moments (kernel timing, sbce_debug_mstep_phase):
         0 pilot factorisation, 1 the R build kernel alone, 2 R and B^H."""
+        self._minnorm_ws = False                       # R (where G lives) is rebuilt
         fn = self.lib.sbce_debug_mstep_phase
         fn.restype = ctypes.c_int
         rc = fn(ctypes.byref(self.dims), ctypes.byref(self.ptrs), ctypes.c_void_p(self.mom.data_ptr()),
@@ -704,6 +709,10 @@ class EMEngine:
     def minnorm_rank(self):
         """(B, 3) int32: active extent, rank of G and whether the refinement step ran, of the
         last whole-batch min-norm M-step (sbce_debug_minnorm_rank; solve='lstsq' only)."""
+        if not self._minnorm_ws:
+            raise RuntimeError("minnorm_rank: the workspace does not hold a whole-batch min-norm "
+                               "M-step (call mstep() with solve='lstsq' first; a streamed run() or "
+                               "mstep_phase() overwrites it)")
         out = self.torch.zeros((self.B, 3), dtype=self.torch.int32, device="cuda")
         fn = self.lib.sbce_debug_minnorm_rank
         fn.restype = ctypes.c_int

@@ -226,3 +226,33 @@ def test_minnorm_cfg2_rank_flagged_trials_vs_lstsq(sbce):
         nm, nm0 = nmse(th[i], sub["h"][i]), nmse(th0, sub["h"][i])
         assert abs(nm / nm0 - 1) < 1e-6, (nm, nm0)                # measured <= 1e-7
         assert rel(th[i], th0) < 1e-3, rel(th[i], th0)           # measured <= 6.1e-5
+
+
+def test_minnorm_rank_diagnostic_matches_lstsq_rank(sbce):
+    """The min-norm solve's per-trial diagnostic (EMEngine.minnorm_rank, sbce_debug_minnorm_rank:
+    active extent, kept pivots of G, refinement ran) at full BASELINE cfg 2 size (8 trials, PM_beta
+    r = 1, 20 dB, the M-step after two EM iterations) against numpy: the kept-pivot rank is at most
+    the extent and within 1 of the rank lstsq uses on the same normal equations (R's eigenvalues
+    above eps K lambda_max, PM.py:108), R rebuilt from the device's own moments.  (Round 4's bench
+    read the diagnostic after its R-build timings had overwritten G with a fresh R and reported
+    rank = extent; EMEngine now refuses to read a workspace that no longer holds the solve.)"""
+    n_tx, n_rx, N, T_p, T_d, B = 8, 8, 256, 32, 1024, 8
+    varn = float(sbce.signal_model.snr_to_varn(20.0))
+    b = sbce.signal_model.synthetic_batch(B, n_tx, n_rx, N, T_p, T_d, 16, varn, seed=2)
+    eng = sbce.EMEngine(b, varn, mode="pm_soft", partition_r=1, solve="lstsq")
+    eng.run(2)
+    eng.estep()
+    eng.mstep()
+    rk = eng.minnorm_rank()
+    mom = eng.mom.cpu().numpy()
+    m, S = mom[..., :n_tx], mom[..., n_tx:].reshape(B, T_d, n_tx, n_tx)
+    L = (N + 1) * n_tx
+    for i in range(B):
+        R0, _ = mstep_build_gemm(b["u_p"][i], b["y_p"][i], b["psi_d"][i].T, b["y_d"][i], m[i], S[i])
+        ev = np.linalg.eigvalsh(R0)
+        rank_np = int((ev > np.finfo(float).eps * L * n_rx * ev.max()).sum())
+        assert 0 < rk[i, 1] <= rk[i, 0] <= L, (i, rk[i])
+        assert abs(int(rk[i, 1]) - rank_np) <= 1, (i, rk[i], rank_np)
+    eng.mstep_phase(1)                       # the R build alone overwrites G
+    with pytest.raises(RuntimeError):
+        eng.minnorm_rank()
