@@ -525,7 +525,7 @@ def grid_cpu_baseline(g, seed, td=60, snr=15.0):
     n_tx, n_rx = g["n_tx"], g["n_rx"]
     varn = float(pkg.signal_model.snr_to_varn(snr, g["power"]))
     b = pkg.signal_model.synthetic_batch(1, n_tx, n_rx, g["N"], g["T_p"], td, g["M"], varn,
-                                         seed=seed + 4242)
+                                         seed=seed + 4242, pinv="scipy")
     a = (b["y_d"][0], b["y_p"][0], b["u_p"][0], b["psi_d"][0].T)
     aps = pkg.qam.all_possible_symbols(b["cons"], n_tx)
     it = g["iters"]
@@ -562,7 +562,9 @@ def grid_main(args, ranks, pkg):
     ns, nt, nd = len(SNR), len(T_D), len(dets)
     engines = []                     # (detector index, T_d index, SNR indices, engine)
     for k, td in enumerate(T_D):
-        pts = [pkg.signal_model.synthetic_batch(B, n_tx, n_rx, N, T_p, td, M, vn,
+        # h_initial with scipy.linalg.pinv's cut, as all_detectorsvsTd.py:341 has it (T_p = 20 >
+        # N_RIS = 15: the DFT pilot phases repeat; numpy's 1e-15 cut would give theta_0 ~ 1e13)
+        pts = [pkg.signal_model.synthetic_batch(B, n_tx, n_rx, N, T_p, td, M, vn, pinv="scipy",
                                                 seed=(args.seed * 1000003 + rank) * 1000 + k * 50 + j)
                for j, vn in enumerate(varns)]
         if args.grid_batch == "snr":

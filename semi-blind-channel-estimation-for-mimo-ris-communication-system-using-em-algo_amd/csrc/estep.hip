@@ -837,7 +837,12 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     }
 
     // lane-level accumulators (see VALU kernel)
-    double mshift = d0;              // a real hypothesis' distance (candidate_distance)
+    // the running shift starts at a real hypothesis' distance (candidate_distance) plus a rounding
+    // margin: the sweep's own distances (alpha + gamma - 2 Re p^H q) differ from d0 by rounding of
+    // order eps * cscale_d, and a shift below every swept distance by more than 50 varn^2 would
+    // skip every group and leave the posterior empty (0/0).  (A theta_0 ~1e13 from a near-singular
+    // pinv puts that rounding at ~1e12 >> varn^2.)  The shift then falls to the true minimum.
+    double mshift = d0 + 1e-10 * cscale_d;
     double tot_c = 0.0;
     cd tot_muA[NA];
     double nu[NA];

@@ -189,8 +189,12 @@ def snr_to_varn(snr_db, power=10.0):
 # ----------------------------------------------------------------- batch generator
 
 def synthetic_batch(B, n_tx, n_rx, N, T_p, T_d, M, varn, seed=0, varh=1.0, direct=True,
-                    pilot="dft_n"):
-    """Vectorised Monte-Carlo batch with the reference's distributions.
+                    pilot="dft_n", pinv="numpy"):
+    """Vectorised Monte-Carlo batch with the reference's distributions.  pinv: the cut of
+    h_initial's pseudo-inverse, "numpy" (np.linalg.pinv's 1e-15, Proposed_method_NMSEvsTp.py:129)
+    or "scipy" (max(M, N) eps, the scipy.linalg.pinv of all_detectorsvsTd.py:341; see
+    initial_estimate).  With T_p > N the DFT pilot phases repeat and the numpy cut keeps
+    rounding-level singular values: theta_0 ~ 1e13.
 
     Returns a dict of batch-major arrays in the C-ABI layout:
       y_d (B,T_d,n_rx), y_p (B,T_p,n_rx), psi_d (B,T_d,P), u_p (B,T_p,L),
@@ -233,8 +237,9 @@ def synthetic_batch(B, n_tx, n_rx, N, T_p, T_d, M, varn, seed=0, varh=1.0, direc
     y_d = np.einsum("brl,btl->btr", Hm, u_d) + (g.normal(0, sn, (B, T_d, n_rx))
                                                 + 1j * g.normal(0, sn, (B, T_d, n_rx)))
     # h_initial = H_0 = Y_p^T pinv(U_p^T), batched
-    pinv = np.linalg.pinv(np.transpose(u_p, (0, 2, 1)))           # (B, T_p, L)
-    H0 = np.einsum("btr,btl->brl", y_p, pinv)                       # (B, n_rx, L)
+    rc = (max(T_p, P * n_tx) * n_rx * np.finfo(float).eps if pinv == "scipy" else 1e-15)
+    Pi = np.linalg.pinv(np.transpose(u_p, (0, 2, 1)), rcond=rc)    # (B, T_p, L)
+    H0 = np.einsum("btr,btl->brl", y_p, Pi)                         # (B, n_rx, L)
     theta0 = np.transpose(H0, (0, 2, 1)).reshape(B, -1)
     return dict(y_d=y_d, y_p=y_p, psi_d=psi_d, u_p=u_p, h=h, theta0=theta0, x_d=x_d,
                 cons=cons, varn=float(varn), n_tx=n_tx, n_rx=n_rx, P=P, T_p=T_p, T_d=T_d, M=M)

@@ -734,7 +734,7 @@ def test_workspace_contents_never_leak_into_results(sbce, case):
     elif case == "pm_lstsq":
         shape, kw = (4, 3, 3, 40, 12, 40, 16), dict(mode="pm_soft", partition_r=1, solve="lstsq")
     elif case == "large_chol":
-        shape = (2, 4, 4, 149, 16, 200, 16)              # L = 600: tiled factorisation
+        shape = (2, 4, 4, 149, 16, 700, 16)              # L = 600 < T_p + T_d: tiled, HPD
     elif case == "cfg1_chol_streams":
         kw = dict(streams=2)
     b = sbce.signal_model.synthetic_batch(*shape, varn, seed=11)
