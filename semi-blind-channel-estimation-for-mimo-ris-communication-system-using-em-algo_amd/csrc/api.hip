@@ -17,7 +17,7 @@ DebugConfig g_debug;
 
 namespace {
 constexpr DebugConfig kDebugDefault = {false, false, false, false, 0, false, 128, false, false, false,
-                                       true};
+                                       true, false};
 constexpr int kSphereBudgetMax = 256;      // estep.hip kBfsPmax
 
 void read_debug_env(DebugConfig& c) {
@@ -38,6 +38,7 @@ void read_debug_env(DebugConfig& c) {
     if ((v = env("SBCE_CHOL_IMPL"))) c.chol_valu = v[0] == 'v';
     if ((v = env("SBCE_ESTEP_PAIR"))) c.estep_nopair = v[0] == '0';
     if ((v = env("SBCE_CPLX3"))) c.cplx3 = v[0] != '0';
+    if ((v = env("SBCE_PM_IMPL"))) c.pm_wave = v[0] == 'w';
 }
 
 __attribute__((constructor)) void load_debug_env() { read_debug_env(g_debug); }

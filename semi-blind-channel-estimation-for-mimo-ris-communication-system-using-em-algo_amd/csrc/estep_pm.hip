@@ -327,6 +327,139 @@ __global__ __launch_bounds__(64 * kPmWaves) void estep_pm_kernel(EstepArgs a, Pm
     }
 }
 
+// ZF / MMSE hard decisions for n_tx <= 2 with ONE THREAD per symbol (64 symbols per wave side
+// by side) instead of one wave: the 2 x 2 Gram inverse, pinv and the nearest-point scans are a
+// few hundred scalar FP64 ops, which the wave form spreads over lanes at the price of an LDS
+// round trip and a wave barrier per step.  The arithmetic is the wave kernel's, operation for
+// operation (gram: cfmac over r; Gauss-Jordan on [G | I] reading row c and column c before the
+// step; GB and z in the same loop orders; strict-< scans), so the decisions and moments are
+// bitwise those of estep_pm_kernel<4/5> (test_gpu_em.py::test_small_detector_estep_bitwise).
+template <int NT, int NR, int MODE>
+__global__ __launch_bounds__(256) void estep_det_thread_kernel(EstepArgs a, PmConst c) {
+    static_assert(NT >= 1 && NT <= 2 && (MODE == 4 || MODE == 5), "n_tx <= 2 ZF / MMSE");
+    constexpr int NO = NT * NR;
+    __shared__ cd s_cons[64];
+    if ((int)threadIdx.x < c.M) s_cons[threadIdx.x] = a.cons[threadIdx.x];
+    __syncthreads();
+    const long nsym = (long)c.B * c.Td;
+    const long gsym = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gsym >= nsym) return;
+    const int b = (int)(gsym / c.Td);
+    if (a.done && a.done[b]) return;
+    double s2 = c.s2;
+    if (a.varn_t) s2 = trial_noise(a.varn_t[b]).s2;      // per-trial noise variance (ABI 6)
+    const int P = c.P, mask = c.M - 1;
+    // off-by-one channel H_off[o] = theta[0][o] + sum_{p < P-1} psi_p theta[p+1][o]
+    cd Ho[NO];
+    {
+        const cd* th = a.theta + (size_t)b * P * NO;
+        const cd* ps = a.psid + (size_t)gsym * P;
+#pragma unroll
+        for (int o = 0; o < NO; ++o) Ho[o] = th[o];
+        for (int p = 0; p + 1 < P; ++p) {
+            const cd psi = ps[p];
+#pragma unroll
+            for (int o = 0; o < NO; ++o) Ho[o] = cfma(Ho[o], psi, th[(p + 1) * NO + o]);
+        }
+    }
+    cd yv[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) yv[r] = a.yd[(size_t)gsym * NR + r];
+    // [G | I], G[u][v] = sum_r conj(H[u][r]) H[v][r] (+ varn^2 on the diagonal for MMSE)
+    cd G[NT][NT], I[NT][NT];
+#pragma unroll
+    for (int u = 0; u < NT; ++u)
+#pragma unroll
+        for (int v = 0; v < NT; ++v) {
+            cd acc = czero();
+#pragma unroll
+            for (int r = 0; r < NR; ++r) acc = cfmac(acc, Ho[v * NR + r], Ho[u * NR + r]);
+            G[u][v] = acc;
+            I[u][v] = (u == v) ? cmk(1.0, 0.0) : czero();
+        }
+    if (MODE == 5) {
+#pragma unroll
+        for (int u = 0; u < NT; ++u) G[u][u].x += s2;
+    }
+    // Gauss-Jordan (gj_inverse): the inverse ends in I
+#pragma unroll
+    for (int cc = 0; cc < NT; ++cc) {
+        const cd piv = G[cc][cc];
+        const double den = cabs2(piv);
+        const cd inv = cmk(piv.x / den, -piv.y / den);
+        cd rg[NT], ri[NT], fi[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) { rg[j] = G[cc][j]; ri[j] = I[cc][j]; }
+#pragma unroll
+        for (int i = 0; i < NT; ++i) fi[i] = G[i][cc];
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const cd rsg = cmul(rg[j], inv), rsi = cmul(ri[j], inv);
+                G[i][j] = (i == cc) ? rsg : csub(G[i][j], cmul(fi[i], rsg));
+                I[i][j] = (i == cc) ? rsi : csub(I[i][j], cmul(fi[i], rsi));
+            }
+    }
+    // z = (G^-1 H^H) y, nearest constellation point per stream (first minimum in table order)
+    double dbest[NT];
+    int sbest[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+        cd GB[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            cd acc = czero();
+#pragma unroll
+            for (int b2 = 0; b2 < NT; ++b2) acc = cfma(acc, I[q][b2], cconj(Ho[b2 * NR + r]));
+            GB[r] = acc;
+        }
+        cd z = czero();
+#pragma unroll
+        for (int r = 0; r < NR; ++r) z = cfma(z, GB[r], yv[r]);
+        int sb = 0;
+        double db = cabs2(csub(z, s_cons[0]));
+        for (int s = 1; s < c.M; ++s) {
+            const double dd = cabs2(csub(z, s_cons[s]));
+            if (dd < db) { db = dd; sb = s; }
+        }
+        dbest[q] = db;
+        sbest[q] = sb;
+    }
+    int as = 0;
+#pragma unroll
+    for (int q = 1; q < NT; ++q)
+        if (dbest[q] < dbest[as]) as = q;
+    const int ss = NT == 1 ? sbest[0] : (as == 0 ? sbest[0] : sbest[1]);
+    long long flat = ss == 0 ? (long long)as * NT : (long long)ss * NT * NT + as * NT + NT - 1;
+    if (c.lm * NT < 62 && flat >= (1LL << (c.lm * NT))) {
+        // the reference raises IndexError here (all_possibleSymbols[flat], :52)
+        if (a.status) atomicOr(&a.status[b], SBCE_STATUS_DETECTOR);
+        flat %= (1LL << (c.lm * NT));
+    }
+    cd x[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) x[q] = s_cons[(flat >> (c.lm * (NT - 1 - q))) & mask];
+    cd* out = a.mom + (size_t)gsym * (NT + NT * NT);
+#pragma unroll
+    for (int ai = 0; ai < NT; ++ai) {
+        out[ai] = x[ai];
+#pragma unroll
+        for (int bi = 0; bi < NT; ++bi) out[NT + ai * NT + bi] = cmulc(x[ai], x[bi]);
+    }
+}
+
+template <int NT, int MODE>
+hipError_t launch_det_thread_nr(int NR, dim3 g, hipStream_t s, const EstepArgs& a, const PmConst& c) {
+    switch (NR) {
+#define SBCE_DT(n) case n: hipLaunchKernelGGL((estep_det_thread_kernel<NT, n, MODE>), g, dim3(256), 0, s, a, c); break;
+        SBCE_DT(1) SBCE_DT(2) SBCE_DT(3) SBCE_DT(4) SBCE_DT(5) SBCE_DT(6) SBCE_DT(7) SBCE_DT(8)
+#undef SBCE_DT
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 }  // namespace
 
 bool estep_pm_supported(const Problem& pb, int partition_r, int mode) {
@@ -357,8 +490,19 @@ hipError_t launch_estep_pm(const Problem& pb, const EstepArgs& a, int mode, int 
     c.inv_s2 = 1.0 / (pb.varn * pb.varn);
     c.s2 = pb.varn * pb.varn;
     c.vx = pb.varx * pb.varx;
-    const size_t lds = (64 + (size_t)kPmWaves * PmLds::TOTAL) * sizeof(cd);
     const long nsym = (long)pb.B * pb.Td;
+    if ((mode == SBCE_ESTEP_ZF || mode == SBCE_ESTEP_MMSE) && pb.NT <= 2 && !g_debug.pm_wave) {
+        // thread per symbol (BASELINE cfg 5: 2 x 2); bitwise the wave kernel's results
+        const long tb = (nsym + 255) / 256;
+        if (tb == 0) return hipSuccess;
+        const dim3 g((unsigned)tb);
+        if (pb.NT == 1)
+            return mode == SBCE_ESTEP_ZF ? launch_det_thread_nr<1, 4>(pb.NR, g, s, a, c)
+                                         : launch_det_thread_nr<1, 5>(pb.NR, g, s, a, c);
+        return mode == SBCE_ESTEP_ZF ? launch_det_thread_nr<2, 4>(pb.NR, g, s, a, c)
+                                     : launch_det_thread_nr<2, 5>(pb.NR, g, s, a, c);
+    }
+    const size_t lds = (64 + (size_t)kPmWaves * PmLds::TOTAL) * sizeof(cd);
     const long blocks = (nsym + kPmWaves - 1) / kPmWaves;
     if (blocks == 0) return hipSuccess;
     const dim3 g((unsigned)blocks), blk(64 * kPmWaves);

@@ -174,6 +174,8 @@ struct DebugConfig {
     bool chol_valu;      // SBCE_CHOL_IMPL=valu    VALU blocked Cholesky (L <= 1024)
     bool estep_nopair;   // SBCE_ESTEP_PAIR=0      no factorised-weight pass (estep_pair.hip)
     bool cplx3;          // SBCE_CPLX3=0           four real MFMAs per complex product (default: three, Gauss)
+    bool pm_wave;        // SBCE_PM_IMPL=wave      ZF/MMSE E-step one wave per symbol at n_tx <= 2 too
+                         //                        (bitwise the thread kernel's results; not flagged)
 };
 extern DebugConfig g_debug;
 bool debug_nondefault();   // a result-affecting switch differs from its default

@@ -587,6 +587,33 @@ def test_detector_estep_vs_oracle(sbce, shape):
             assert np.allclose(S[i], S0, rtol=0, atol=1e-12)
 
 
+@pytest.mark.parametrize("shape", [(2, 2, 15, 20, 120, 64, -5), (2, 2, 15, 20, 60, 64, 33),
+                                   (1, 1, 6, 8, 40, 4, 0), (1, 8, 4, 8, 33, 16, 10),
+                                   (2, 8, 3, 12, 50, 16, 5), (2, 5, 2, 8, 17, 4, 20)])
+def test_detector_thread_kernel_bitwise_wave_kernel(sbce, shape):
+    """ZF / MMSE at n_tx <= 2 run one thread per symbol (BASELINE cfg 5); the one-wave-per-symbol
+    kernel (SBCE_PM_IMPL=wave) does the same arithmetic in the same order: m and S bitwise
+    equal, including low SNR (near-singular Gram) and ragged T_d."""
+    n_tx, n_rx, N, T_p, T_d, M, snr = shape
+    varn = float(sbce.signal_model.snr_to_varn(snr))
+    b = sbce.signal_model.synthetic_batch(3, n_tx, n_rx, N, T_p, T_d, M, varn, seed=37)
+    for kind in ("zf", "mmse"):
+        m, S = sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx, kind)
+        with sbce._lib.debug_env(SBCE_PM_IMPL="wave"):
+            mw, Sw = sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx,
+                                      kind)
+        assert np.array_equal(m, mw, equal_nan=True), kind
+        assert np.array_equal(S, Sw, equal_nan=True), kind
+        if n_tx <= 2 and snr >= 0:
+            from oracle.detectors import detector_moments
+            try:
+                m0, _ = detector_moments(b["theta0"][0], b["y_d"][0], b["psi_d"][0].T, None,
+                                         varn, n_tx, n_rx, kind, cons=b["cons"])
+            except IndexError:
+                continue          # the reference would raise; the device flags the trial
+            assert np.array_equal(m[0], m0)
+
+
 # ---------------------------------------------------------------- SER path
 def test_em_ml_ser_matches_reference(sbce):
     """log_max_SER.em: theta and the last iteration's decisions X_dest; device SER."""
