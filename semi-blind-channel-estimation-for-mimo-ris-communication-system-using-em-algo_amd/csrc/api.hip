@@ -17,7 +17,7 @@ DebugConfig g_debug;
 
 namespace {
 constexpr DebugConfig kDebugDefault = {false, false, false, false, 0, false, 128, false, false, false,
-                                       true, false};
+                                       true, false, 0, false};
 constexpr int kSphereBudgetMax = 256;      // estep.hip kBfsPmax
 
 void read_debug_env(DebugConfig& c) {
@@ -38,7 +38,9 @@ void read_debug_env(DebugConfig& c) {
     if ((v = env("SBCE_CHOL_IMPL"))) c.chol_valu = v[0] == 'v';
     if ((v = env("SBCE_ESTEP_PAIR"))) c.estep_nopair = v[0] == '0';
     if ((v = env("SBCE_CPLX3"))) c.cplx3 = v[0] != '0';
+    if ((v = env("SBCE_MSTEP_SMALL"))) c.mstep_nosmall = v[0] == '0';
     if ((v = env("SBCE_PM_IMPL"))) c.pm_wave = v[0] == 'w';
+    if ((v = env("SBCE_SMALL_STOP"))) c.small_stop = (v[0] >= '1' && v[0] <= '3') ? v[0] - '0' : 0;
 }
 
 __attribute__((constructor)) void load_debug_env() { read_debug_env(g_debug); }
@@ -52,6 +54,7 @@ bool debug_nondefault() {
            c.estep_nosphere != d.estep_nosphere || c.sphere_budget != d.sphere_budget ||
            c.backsub_general != d.backsub_general || c.chol_valu != d.chol_valu ||
            c.estep_nopair != d.estep_nopair || c.cplx3 != d.cplx3 ||
+           c.mstep_nosmall != d.mstep_nosmall || c.small_stop != d.small_stop ||
            (chol_debug_skip_mask() & 31);
 }
 
@@ -271,6 +274,8 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     // the Kronecker factors of the pilot regressors do not change across iterations
     const bool prefactor = rbuild_herm_supported(pb);
     if (prefactor && (rc = hip_rc(launch_pilot_factor(pb, ma, s)))) return rc;
+    // L <= 64: the whole M-step in one launch (BASELINE cfg 5: L = 32)
+    const bool small = mstep_small_supported(pb, solve_mode) && !(gauss && pb.NR == 1);
     for (int it = 0; it < iters; ++it) {
         if (p->x_sup) {
             if ((rc = hip_rc(launch_sup_shift_y(pb, ea.yd, ea.psid, ea.theta, (const cd*)p->x_sup,
@@ -283,11 +288,15 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
             ea.wide = it == 0;
             if ((rc = hip_rc(launch_estep(pb, ea, estep_mode, s)))) return rc;
         }
-        if ((rc = hip_rc(launch_mstep_build(pb, ma, s, prefactor)))) return rc;
-        // Gaussian prior, n_rx = 1: the reference's all-ones covariance term stays in A
-        // (MIMO_Gaussian_proposed.py:73-76): R += c 1 1^T
-        if (gauss && pb.NR == 1 && (rc = hip_rc(launch_gauss_rank1(pb, ma, s)))) return rc;
-        if ((rc = hip_rc(launch_chol_solve(pb, ma, s)))) return rc;
+        if (small) {
+            if ((rc = hip_rc(launch_mstep_small(pb, ma, false, s)))) return rc;
+        } else {
+            if ((rc = hip_rc(launch_mstep_build(pb, ma, s, prefactor)))) return rc;
+            // Gaussian prior, n_rx = 1: the reference's all-ones covariance term stays in A
+            // (MIMO_Gaussian_proposed.py:73-76): R += c 1 1^T
+            if (gauss && pb.NR == 1 && (rc = hip_rc(launch_gauss_rank1(pb, ma, s)))) return rc;
+            if ((rc = hip_rc(launch_chol_solve(pb, ma, s)))) return rc;
+        }
         if (p->llf &&
             (rc = hip_rc(launch_llf(pb, ma.theta, ma.yp, ma.up, ma.yd, ma.psid,
                                     (const cd*)p->x_d_true, p->llf, iters, it, ea.done, p->varn_t,
@@ -362,7 +371,12 @@ int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int 
     ma.rhs = (cd*)(ws + c.rhs); ma.theta = (cd*)p->theta; ma.status = p->status; ma.done = nullptr;
     ma.solve_mode = solve_mode; ma.nbatch = pb.B;
     set_large(ma, ws, c);
-    if ((rc = hip_rc(launch_mstep_build(pb, ma, s)))) return rc;
+    const bool small = mstep_small_supported(pb, solve_mode);
+    if (small) {
+        if ((rc = hip_rc(launch_mstep_small(pb, ma, r_out || rhs_out, s)))) return rc;
+    } else if ((rc = hip_rc(launch_mstep_build(pb, ma, s)))) {
+        return rc;
+    }
     if (r_out &&
         hipMemcpyAsync(r_out, ma.R, (size_t)pb.B * pb.L * pb.L * sizeof(cd), hipMemcpyDeviceToDevice,
                        s) != hipSuccess)
@@ -371,7 +385,7 @@ int sbce_mstep(const sbce_dims* d, const sbce_ptrs* p, const void* moments, int 
         hipMemcpyAsync(rhs_out, ma.rhs, (size_t)pb.B * pb.L * pb.NR * sizeof(cd),
                        hipMemcpyDeviceToDevice, s) != hipSuccess)
         return SBCE_EHIP;
-    return hip_rc(launch_chol_solve(pb, ma, s));
+    return small ? SBCE_OK : hip_rc(launch_chol_solve(pb, ma, s));
 }
 
 // Diagnostic, not part of include/sbce.h: HIP-event timing of the L <= 512 Cholesky's update /

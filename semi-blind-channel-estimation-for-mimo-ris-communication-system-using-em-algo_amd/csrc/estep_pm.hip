@@ -327,20 +327,128 @@ __global__ __launch_bounds__(64 * kPmWaves) void estep_pm_kernel(EstepArgs a, Pm
     }
 }
 
+// ---------------------------------------------------------------- nearest constellation point
+// The thread kernels' nearest-point search.  A square M-QAM table (K x K grid of real / imaginary
+// levels, any table order: grid_build checks it once per block, in parallel) is searched per axis: the best
+// and second-best level by |fl(z - l)| on each axis give the candidate (ix, iy) and its two
+// nearest rivals.  fl(z - s), cabs2 = fma(dx, dx, fl(dy dy)) are monotone in |dx| and |dy|, so
+// every other point's distance is >= a rival's: when both rivals are strictly farther, (ix, iy)
+// is the unique minimiser, i.e. what the first-minimum exhaustive scan in table order returns,
+// with the same distance value.  Otherwise (a tie, NaN, or not a square grid) the exhaustive scan
+// runs.  Bitwise the wave kernel's decisions either way.
+struct GridLds {
+    double lre[8], lim[8];
+    int idx[64];
+    int K;                                          // 0: not a square grid, exhaustive scans
+};
+
+// Every thread of the block calls it (blockDim >= M).  Thread s < M places point s: its level
+// index on each axis is (#points strictly below it) / K, valid when exactly K points share its
+// level and no other point equals it -- then the K x K cells are filled one-to-one.
+__device__ void grid_build(const cd* cons, int M, GridLds* g) {
+    const int tid = threadIdx.x;
+    int K = 0;
+    while (K * K < M) ++K;
+    const bool sq = K * K == M && K <= 8;
+    bool ok = true;
+    if (sq && tid < M) {
+        const cd v = cons[tid];
+        int lt_x = 0, eq_x = 0, lt_y = 0, eq_y = 0, same = 0;
+        for (int s = 0; s < M; ++s) {
+            const cd u = cons[s];
+            lt_x += u.x < v.x;
+            eq_x += u.x == v.x;
+            lt_y += u.y < v.y;
+            eq_y += u.y == v.y;
+            same += (u.x == v.x) && (u.y == v.y);
+        }
+        ok = eq_x == K && eq_y == K && same == 1 && lt_x % K == 0 && lt_y % K == 0;
+        if (ok) {
+            const int ir = lt_x / K, ii = lt_y / K;
+            g->lre[ir] = v.x;
+            g->lim[ii] = v.y;
+            g->idx[ir * K + ii] = tid;
+        }
+    }
+    const bool all = __syncthreads_and(ok ? 1 : 0) != 0;
+    if (tid == 0) g->K = (sq && all) ? K : 0;
+    __syncthreads();
+}
+
+__device__ __forceinline__ int nearest_scan(const cd* cons, int M, cd z, double& dbest) {
+    int sb = 0;
+    double db = cabs2(csub(z, cons[0]));
+    for (int s = 1; s < M; ++s) {
+        const double dd = cabs2(csub(z, cons[s]));
+        if (dd < db) { db = dd; sb = s; }
+    }
+    dbest = db;
+    return sb;
+}
+
+// the levels in registers (loaded once per thread), the cell -> table index map in LDS
+struct GridReg {
+    double lre[8], lim[8];
+    int K;
+};
+
+__device__ __forceinline__ GridReg grid_load(const GridLds& g) {
+    GridReg r;
+    r.K = g.K;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        r.lre[k] = k < r.K ? g.lre[k] : INFINITY;
+        r.lim[k] = k < r.K ? g.lim[k] : INFINITY;
+    }
+    return r;
+}
+
+__device__ __forceinline__ int nearest_point(const GridReg& gr, const GridLds& g, const cd* cons,
+                                             int M, cd z, double& dbest) {
+    const int K = gr.K;
+    if (K > 0) {
+        double bx = INFINITY, bx2 = INFINITY, by = INFINITY, by2 = INFINITY;
+        int ix = 0, ix2 = 0, iy = 0, iy2 = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k < K) {
+                const double dx = fabs(z.x - gr.lre[k]);
+                if (dx < bx) { bx2 = bx; ix2 = ix; bx = dx; ix = k; }
+                else if (dx < bx2) { bx2 = dx; ix2 = k; }
+                const double dy = fabs(z.y - gr.lim[k]);
+                if (dy < by) { by2 = by; iy2 = iy; by = dy; iy = k; }
+                else if (dy < by2) { by2 = dy; iy2 = k; }
+            }
+        }
+        const int s1 = g.idx[ix * K + iy];
+        const double v1 = cabs2(csub(z, cons[s1]));
+        const double va = cabs2(csub(z, cons[g.idx[ix2 * K + iy]]));
+        const double vb = cabs2(csub(z, cons[g.idx[ix * K + iy2]]));
+        if (va > v1 && vb > v1) {
+            dbest = v1;
+            return s1;
+        }
+    }
+    return nearest_scan(cons, M, z, dbest);
+}
+
 // ZF / MMSE hard decisions for n_tx <= 2 with ONE THREAD per symbol (64 symbols per wave side
-// by side) instead of one wave: the 2 x 2 Gram inverse, pinv and the nearest-point scans are a
-// few hundred scalar FP64 ops, which the wave form spreads over lanes at the price of an LDS
+// by side) instead of one wave: the 2 x 2 Gram inverse, pinv and the nearest-point searches
+// (nearest_point) are a few hundred scalar FP64 ops, which the wave form spreads over lanes at the price of an LDS
 // round trip and a wave barrier per step.  The arithmetic is the wave kernel's, operation for
 // operation (gram: cfmac over r; Gauss-Jordan on [G | I] reading row c and column c before the
 // step; GB and z in the same loop orders; strict-< scans), so the decisions and moments are
-// bitwise those of estep_pm_kernel<4/5> (test_gpu_em.py::test_small_detector_estep_bitwise).
+// bitwise those of estep_pm_kernel<4/5> (test_gpu_em.py::test_detector_thread_kernel_bitwise_wave_kernel).
 template <int NT, int NR, int MODE>
-__global__ __launch_bounds__(256) void estep_det_thread_kernel(EstepArgs a, PmConst c) {
+__global__ __launch_bounds__(64) void estep_det_thread_kernel(EstepArgs a, PmConst c) {
     static_assert(NT >= 1 && NT <= 2 && (MODE == 4 || MODE == 5), "n_tx <= 2 ZF / MMSE");
     constexpr int NO = NT * NR;
     __shared__ cd s_cons[64];
+    __shared__ GridLds s_grid;
     if ((int)threadIdx.x < c.M) s_cons[threadIdx.x] = a.cons[threadIdx.x];
     __syncthreads();
+    grid_build(s_cons, c.M, &s_grid);
+    const GridReg greg = grid_load(s_grid);
     const long nsym = (long)c.B * c.Td;
     const long gsym = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gsym >= nsym) return;
@@ -417,12 +525,8 @@ __global__ __launch_bounds__(256) void estep_det_thread_kernel(EstepArgs a, PmCo
         cd z = czero();
 #pragma unroll
         for (int r = 0; r < NR; ++r) z = cfma(z, GB[r], yv[r]);
-        int sb = 0;
-        double db = cabs2(csub(z, s_cons[0]));
-        for (int s = 1; s < c.M; ++s) {
-            const double dd = cabs2(csub(z, s_cons[s]));
-            if (dd < db) { db = dd; sb = s; }
-        }
+        double db;
+        const int sb = nearest_point(greg, s_grid, s_cons, c.M, z, db);
         dbest[q] = db;
         sbest[q] = sb;
     }
@@ -449,10 +553,207 @@ __global__ __launch_bounds__(256) void estep_det_thread_kernel(EstepArgs a, PmCo
     }
 }
 
+// PM / PM-soft list E-step for n_tx = 2 with a one-stream list (|A| = 1: partition_r < log2 M,
+// BASELINE cfg 5's r = 1 with 64-QAM) with ONE THREAD per symbol.  The wave kernel's steps in its
+// operation order: H_true / H_off, the greedy order from the 2 x 2 Gram inverse (Gauss-Jordan as
+// gj_inverse), G_B of the single B stream, then the M candidates a (x = [a, b], b the first
+// nearest point to z = G_B y - G_A a, nearest_point) and their distances; the wave kernel's
+// 64-lane xor-butterfly sum of the weights is the same pairwise tree over the candidate index
+// (lanes l and l + 32 first), and its moment sums run over the candidates in order, so m and S
+// are bitwise estep_pm_kernel<2/3>'s (test_gpu_em.py::test_pm_thread_kernel_bitwise_wave_kernel).
+template <int MODE, int NR>
+__global__ __launch_bounds__(64) void estep_pm_thread_kernel(EstepArgs a, PmConst c) {
+    static_assert(MODE == 2 || MODE == 3, "PM / PM-soft");
+    constexpr int NT = 2, NO = NT * NR;
+    __shared__ cd s_cons[64];
+    __shared__ GridLds s_grid;
+    __shared__ uint8_t s_sb[64 * 64];
+    if ((int)threadIdx.x < c.M) s_cons[threadIdx.x] = a.cons[threadIdx.x];
+    __syncthreads();
+    grid_build(s_cons, c.M, &s_grid);
+    const GridReg greg = grid_load(s_grid);
+    const long nsym = (long)c.B * c.Td;
+    const long gsym = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gsym >= nsym) return;
+    const int b = (int)(gsym / c.Td);
+    if (a.done && a.done[b]) return;
+    double inv_s2 = c.inv_s2;
+    if (a.varn_t) inv_s2 = trial_noise(a.varn_t[b]).inv_s2;   // per-trial noise variance (ABI 6)
+    const int P = c.P, JA = c.JA;
+
+    // ---- 1. H_true, H_off, y ----
+    cd Ht[NO], Ho[NO];
+    {
+        const cd* th = a.theta + (size_t)b * P * NO;
+        const cd* ps = a.psid + (size_t)gsym * P;
+#pragma unroll
+        for (int o = 0; o < NO; ++o) { Ht[o] = czero(); Ho[o] = th[o]; }
+        for (int p = 0; p < P; ++p) {
+            const cd psi = ps[p];
+#pragma unroll
+            for (int o = 0; o < NO; ++o) {
+                Ht[o] = cfma(Ht[o], psi, th[p * NO + o]);
+                if (p + 1 < P) Ho[o] = cfma(Ho[o], psi, th[(p + 1) * NO + o]);
+            }
+        }
+    }
+    cd yv[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) yv[r] = a.yd[(size_t)gsym * NR + r];
+
+    // ---- 2. greedy order: drop the stream with the largest diag((H^H H)^-1) first ----
+    int kmax = 0;
+    {
+        cd G[NT][NT], I[NT][NT];
+#pragma unroll
+        for (int u = 0; u < NT; ++u)
+#pragma unroll
+            for (int v = 0; v < NT; ++v) {
+                cd acc = czero();
+#pragma unroll
+                for (int r = 0; r < NR; ++r) acc = cfmac(acc, Ho[v * NR + r], Ho[u * NR + r]);
+                G[u][v] = acc;
+                I[u][v] = (u == v) ? cmk(1.0, 0.0) : czero();
+            }
+#pragma unroll
+        for (int cc = 0; cc < NT; ++cc) {
+            const cd piv = G[cc][cc];
+            const double den = cabs2(piv);
+            const cd inv = cmk(piv.x / den, -piv.y / den);
+            cd rg[NT], ri[NT], fi[NT];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) { rg[j] = G[cc][j]; ri[j] = I[cc][j]; }
+#pragma unroll
+            for (int i = 0; i < NT; ++i) fi[i] = G[i][cc];
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    const cd rsg = cmul(rg[j], inv), rsi = cmul(ri[j], inv);
+                    G[i][j] = (i == cc) ? rsg : csub(G[i][j], cmul(fi[i], rsg));
+                    I[i][j] = (i == cc) ? rsi : csub(I[i][j], cmul(fi[i], rsi));
+                }
+        }
+        // np.argmax over the complex diagonal: lexicographic (real, imag), first maximum
+        const cd v0 = I[0][0], v1 = I[1][1];
+        if (v1.x > v0.x || (v1.x == v0.x && v1.y > v0.y)) kmax = 1;
+    }
+    const int oa = kmax, ob = 1 - kmax;              // A = {ord[0]}, B = {ord[1]}
+
+    // ---- 3. G_B = (B^H B)^{-1} B^H (1 x NR), G_B y, G_B A ----
+    cd Gy = czero(), GA = czero();
+    {
+        cd HA[NR], HB[NR];                           // columns A, B of H_off (no dynamic indexing)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            HA[r] = csel(oa != 0, Ho[NR + r], Ho[r]);
+            HB[r] = csel(ob != 0, Ho[NR + r], Ho[r]);
+        }
+        cd g = czero();
+#pragma unroll
+        for (int r = 0; r < NR; ++r) g = cfmac(g, HB[r], HB[r]);
+        const double den = cabs2(g);
+        const cd inv = cmk(g.x / den, -g.y / den);
+        const cd gi = cmul(cmk(1.0, 0.0), inv);      // gj_inverse on the 1 x 1 [g | 1]
+        cd GB[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) GB[r] = cfma(czero(), gi, cconj(HB[r]));
+#pragma unroll
+        for (int r = 0; r < NR; ++r) Gy = cfma(Gy, GB[r], yv[r]);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) GA = cfma(GA, GB[r], HA[r]);
+    }
+
+    // ---- 4./5. candidates: x = [a, b] in concatenated order, distances ----
+    // three passes over the candidates (no per-candidate register arrays): b's index kept in LDS,
+    // the distance recomputed (the same operations, so the same value) where it is needed
+    uint8_t* sb_col = s_sb + threadIdx.x;              // [64 candidates][64 threads]
+    auto dist = [&](cd x0, cd x1) {
+        double dd = 0.0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            cd res = yv[r];
+            res = csub(res, cmul(Ht[0 * NR + r], x0));
+            res = csub(res, cmul(Ht[1 * NR + r], x1));
+            dd += cabs2(res);
+        }
+        return dd;
+    };
+    double dm = INFINITY;
+    for (int i = 0; i < JA; ++i) {
+        const cd x0 = s_cons[i];
+        cd z = Gy;
+        z = csub(z, cmul(GA, x0));
+        double db;
+        const int sb = nearest_point(greg, s_grid, s_cons, c.M, z, db);
+        sb_col[i * 64] = (uint8_t)sb;
+        if (MODE == 3) dm = fmin(dm, dist(x0, s_cons[sb]));
+    }
+    // weights: 1 (PM) or softmax(-d / varn^2); the wave kernel's 64-lane xor-butterfly sum is the
+    // pairwise tree over the candidates in bit-reversed order (lanes l, l + 32 first), summed here
+    // by a binary counter over six levels
+    double zs = 1.0;
+    if (MODE == 3) {
+        double st[6];
+#pragma unroll
+        for (int lev = 0; lev < 6; ++lev) st[lev] = 0.0;
+        for (int k = 0; k < 64; ++k) {
+            const int l = (int)(__builtin_bitreverse32((uint32_t)k) >> 26);
+            double v = 0.0;
+            if (l < JA) v = exp(-(dist(s_cons[l], s_cons[sb_col[l * 64]]) - dm) * inv_s2);
+            bool carry = true;
+#pragma unroll
+            for (int lev = 0; lev < 6; ++lev) {
+                if (carry) {
+                    if ((k >> lev) & 1) v = st[lev] + v;
+                    else { st[lev] = v; carry = false; }
+                }
+            }
+            if (k == 63) zs = v;
+        }
+    }
+
+    // ---- 6. moments, candidates in order ----
+    cd m0 = czero(), m1 = czero(), S00 = czero(), S01 = czero(), S10 = czero(), S11 = czero();
+    for (int i = 0; i < JA; ++i) {
+        const cd x0 = s_cons[i];
+        const cd x1 = s_cons[sb_col[i * 64]];
+        double w = 1.0;
+        if (MODE == 3) {
+            w = exp(-(dist(x0, x1) - dm) * inv_s2);
+            w /= zs;
+        }
+        S00 = caxpy(S00, w, cmulc(x0, x0));
+        S01 = caxpy(S01, w, cmulc(x0, x1));
+        S10 = caxpy(S10, w, cmulc(x1, x0));
+        S11 = caxpy(S11, w, cmulc(x1, x1));
+        m0 = caxpy(m0, w, x0);
+        m1 = caxpy(m1, w, x1);
+    }
+    cd* out = a.mom + (size_t)gsym * (NT + NT * NT);
+    out[0] = m0;
+    out[1] = m1;
+    out[2] = S00;
+    out[3] = S01;
+    out[4] = S10;
+    out[5] = S11;
+}
+
+template <int MODE>
+hipError_t launch_pm_thread_nr(int NR, dim3 g, hipStream_t s, const EstepArgs& a, const PmConst& c) {
+    switch (NR) {
+#define SBCE_PT(n) case n: hipLaunchKernelGGL((estep_pm_thread_kernel<MODE, n>), g, dim3(64), 0, s, a, c); break;
+        SBCE_PT(1) SBCE_PT(2) SBCE_PT(3) SBCE_PT(4) SBCE_PT(5) SBCE_PT(6) SBCE_PT(7) SBCE_PT(8)
+#undef SBCE_PT
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 template <int NT, int MODE>
 hipError_t launch_det_thread_nr(int NR, dim3 g, hipStream_t s, const EstepArgs& a, const PmConst& c) {
     switch (NR) {
-#define SBCE_DT(n) case n: hipLaunchKernelGGL((estep_det_thread_kernel<NT, n, MODE>), g, dim3(256), 0, s, a, c); break;
+#define SBCE_DT(n) case n: hipLaunchKernelGGL((estep_det_thread_kernel<NT, n, MODE>), g, dim3(64), 0, s, a, c); break;
         SBCE_DT(1) SBCE_DT(2) SBCE_DT(3) SBCE_DT(4) SBCE_DT(5) SBCE_DT(6) SBCE_DT(7) SBCE_DT(8)
 #undef SBCE_DT
         default: return hipErrorInvalidValue;
@@ -493,7 +794,7 @@ hipError_t launch_estep_pm(const Problem& pb, const EstepArgs& a, int mode, int 
     const long nsym = (long)pb.B * pb.Td;
     if ((mode == SBCE_ESTEP_ZF || mode == SBCE_ESTEP_MMSE) && pb.NT <= 2 && !g_debug.pm_wave) {
         // thread per symbol (BASELINE cfg 5: 2 x 2); bitwise the wave kernel's results
-        const long tb = (nsym + 255) / 256;
+        const long tb = (nsym + 63) / 64;
         if (tb == 0) return hipSuccess;
         const dim3 g((unsigned)tb);
         if (pb.NT == 1)
@@ -501,6 +802,15 @@ hipError_t launch_estep_pm(const Problem& pb, const EstepArgs& a, int mode, int 
                                          : launch_det_thread_nr<1, 5>(pb.NR, g, s, a, c);
         return mode == SBCE_ESTEP_ZF ? launch_det_thread_nr<2, 4>(pb.NR, g, s, a, c)
                                      : launch_det_thread_nr<2, 5>(pb.NR, g, s, a, c);
+    }
+    if ((mode == SBCE_ESTEP_PM || mode == SBCE_ESTEP_PM_SOFT) && pb.NT == 2 && c.NA == 1 &&
+        !g_debug.pm_wave) {
+        // thread per symbol, one-stream list (BASELINE cfg 5: 2 x 2, r = 1, 64-QAM)
+        const long tb = (nsym + 63) / 64;
+        if (tb == 0) return hipSuccess;
+        const dim3 g((unsigned)tb);
+        return mode == SBCE_ESTEP_PM ? launch_pm_thread_nr<2>(pb.NR, g, s, a, c)
+                                     : launch_pm_thread_nr<3>(pb.NR, g, s, a, c);
     }
     const size_t lds = (64 + (size_t)kPmWaves * PmLds::TOTAL) * sizeof(cd);
     const long blocks = (nsym + kPmWaves - 1) / kPmWaves;

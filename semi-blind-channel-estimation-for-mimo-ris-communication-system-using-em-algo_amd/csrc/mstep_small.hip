@@ -1,0 +1,302 @@
+// Small-L M-step (L = (N+1) n_tx <= 64, n_tx not in {4, 8}): the whole M-step of one trial in ONE
+// workgroup -- R and B^H built, factored and solved in registers, theta written.
+//
+// Reference: the M-step of "Proposed method/all_detectorsvsTd.py" (its five EMs, :62-96 etc.:
+// A = sum Z^H Z, b = sum Z^H y, np.linalg.solve) at BASELINE cfg 5's 2 x 2, N_RIS = 15 shape
+// (L = 32), in the reduced form of mstep.hip (R X = B^H, commutation_matrix.py:3-8).
+//
+// The batched path (rbuild_kernel, rhs_dma_kernel, diag_tol_kernel, panel_factor_kernel,
+// backsub4_kernel) spends five launches and four HBM round trips of R per iteration on a
+// 32 x 32 system, each launch a few microseconds of latency-bound work per trial.  Here each
+// thread owns a fixed set of R's entries and of B^H's from the build to the solve:
+//   1. every entry accumulated in rbuild_kernel's / rhs_kernel's operation order (pilot terms,
+//      then the data symbols in order; the symbols staged in LDS) -> bitwise their R and B^H;
+//   2. tol = 1e-14 max diag R (diag_tol_kernel); right-looking Cholesky with the forward
+//      substitution fused: per column ONE barrier, column c and y_c exchanged through a
+//      double-buffered LDS vector, every other update on the owner's registers;
+//   3. back substitution L^H x = y the same way (row c of L and x_c exchanged); theta = conj(x).
+// Pivot rule and status bits are the batched path's (chol.hip factor_diag): a pivot that is not
+// above tol is flagged (clamp_status); SBCE_SOLVE_CHOL clamps it to tol, CHOL_DROP drops the
+// direction (l_cc = 0, its unknowns 0).
+#include "sbce_internal.h"
+
+namespace sbce {
+
+namespace {
+
+constexpr int kSmallMaxL = 64;
+constexpr int kSmallThreads = 256;
+constexpr int kStageCd = 2048;                // staged symbols: <= 32 KB of complex doubles
+
+// Thread (ti, tj) = (tid / 16, tid % 16) owns the R elements (ti + 16 k1, tj + 16 k2), k1, k2 <
+// KB = ceil(L / 16), in registers from the build to the end of the solve; B^H / y entry
+// e = tid + 256 k (row e / NR, column e % NR) likewise.  Only column c (forward) or row c (back
+// substitution) of L and y_c / x_c cross threads, through a double-buffered LDS vector: one
+// barrier per column.
+template <int NR, int KB>
+__global__ __launch_bounds__(kSmallThreads) void mstep_small_kernel(MstepArgs a, int NT, int P,
+                                                                    int Tp, int Td, int L,
+                                                                    int write_sys, int stop) {
+    const int b = blockIdx.x;
+    if (a.done && a.done[b]) return;
+    constexpr int YK = (64 * NR + kSmallThreads - 1) / kSmallThreads;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cd* stg = reinterpret_cast<cd*>(smem);           // [kStageCd] staged symbols
+    cd* xb = stg + kStageCd;                         // [2][64 + 8] column / row + y_c exchange
+    double* dinv = reinterpret_cast<double*>(xb + 2 * (64 + 8));   // [64] 1 / l_cc (0: dropped)
+    double* red = dinv + 64;                                      // [4]
+    const int tid = threadIdx.x, ti = tid >> 4, tj = tid & 15;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int MS = NT + NT * NT;
+
+    // ---- 1. R and B^H in registers --------------------------------------------------------------
+    // element (i, j) is accumulated as rbuild_kernel's block pair (p, q), p >= q, entry (ia, ja):
+    // swapped (and conjugated at the end) when i's block is above j's
+    cd A[KB][KB];
+    int rr[KB][KB], cc[KB][KB];
+    int prr[KB][KB], pcc[KB][KB], sidx[KB][KB];   // rbuild's block pair and S_t entry
+    bool need[KB][KB], swp[KB][KB];
+#pragma unroll
+    for (int k1 = 0; k1 < KB; ++k1)
+#pragma unroll
+        for (int k2 = 0; k2 < KB; ++k2) {
+            const int i = ti + 16 * k1, j = tj + 16 * k2;
+            const bool valid = i < L && j < L;
+            swp[k1][k2] = valid && (i / NT) < (j / NT);
+            need[k1][k2] = valid && (i >= j || write_sys);
+            rr[k1][k2] = swp[k1][k2] ? j : i;
+            cc[k1][k2] = swp[k1][k2] ? i : j;
+            prr[k1][k2] = rr[k1][k2] / NT;
+            pcc[k1][k2] = cc[k1][k2] / NT;
+            sidx[k1][k2] = NT + (rr[k1][k2] - prr[k1][k2] * NT) * NT + (cc[k1][k2] - pcc[k1][k2] * NT);
+            A[k1][k2] = czero();
+        }
+    cd Y[YK];
+    int yl[YK], ypl[YK], yal[YK], yrr[YK];            // row, its block and stream, column
+#pragma unroll
+    for (int k = 0; k < YK; ++k) {
+        yl[k] = (tid + kSmallThreads * k) / NR;
+        yrr[k] = tid + kSmallThreads * k - yl[k] * NR;
+        ypl[k] = yl[k] / NT;
+        yal[k] = yl[k] - ypl[k] * NT;
+        Y[k] = czero();
+    }
+
+    // pilots, TPC symbols at a time: u_p [TPC][L], y_p [TPC][NR]
+    {
+        const int TPC = kStageCd / (L + NR) > 0 ? kStageCd / (L + NR) : 1;
+        const cd* up = a.up + (size_t)b * Tp * L;
+        const cd* yp = a.yp + (size_t)b * Tp * NR;
+        cd* su = stg;
+        cd* sp = stg + TPC * L;
+        for (int t0 = 0; t0 < Tp; t0 += TPC) {
+            const int tc = (Tp - t0) < TPC ? (Tp - t0) : TPC;
+            __syncthreads();
+            for (int e = tid; e < tc * L; e += kSmallThreads) su[e] = up[(size_t)t0 * L + e];
+            for (int e = tid; e < tc * NR; e += kSmallThreads) sp[e] = yp[(size_t)t0 * NR + e];
+            __syncthreads();
+            for (int tt = 0; tt < (stop == 3 ? 0 : tc); ++tt) {
+#pragma unroll
+                for (int k1 = 0; k1 < KB; ++k1)
+#pragma unroll
+                    for (int k2 = 0; k2 < KB; ++k2)
+                        if (need[k1][k2])
+                            A[k1][k2] = cfmac(A[k1][k2], su[tt * L + rr[k1][k2]], su[tt * L + cc[k1][k2]]);
+#pragma unroll
+                for (int k = 0; k < YK; ++k)
+                    if (yl[k] < L) Y[k] = cfmac(Y[k], su[tt * L + yl[k]], sp[tt * NR + yrr[k]]);
+            }
+        }
+    }
+    // data symbols, TC at a time: psi [TC][P], moments [TC][MS], y_d [TC][NR]
+    {
+        const int TC = kStageCd / (P + MS + NR) > 0 ? kStageCd / (P + MS + NR) : 1;
+        const cd* ps = a.psid + (size_t)b * Td * P;
+        const cd* mom = a.mom + (size_t)b * Td * MS;
+        const cd* yd = a.yd + (size_t)b * Td * NR;
+        cd* s_ps = stg;
+        cd* s_m = s_ps + TC * P;
+        cd* s_y = s_m + TC * MS;
+        for (int t0 = 0; t0 < Td; t0 += TC) {
+            const int tc = (Td - t0) < TC ? (Td - t0) : TC;
+            __syncthreads();
+            for (int e = tid; e < tc * P; e += kSmallThreads) s_ps[e] = ps[(size_t)t0 * P + e];
+            for (int e = tid; e < tc * MS; e += kSmallThreads) s_m[e] = mom[(size_t)t0 * MS + e];
+            for (int e = tid; e < tc * NR; e += kSmallThreads) s_y[e] = yd[(size_t)t0 * NR + e];
+            __syncthreads();
+            for (int tt = 0; tt < (stop == 3 ? 0 : tc); ++tt) {
+#pragma unroll
+                for (int k1 = 0; k1 < KB; ++k1)
+#pragma unroll
+                    for (int k2 = 0; k2 < KB; ++k2)
+                        if (need[k1][k2]) {
+                            const cd w = cmulc(s_ps[tt * P + prr[k1][k2]], s_ps[tt * P + pcc[k1][k2]]);
+                            A[k1][k2] = cfma(A[k1][k2], w, s_m[tt * MS + sidx[k1][k2]]);
+                        }
+#pragma unroll
+                for (int k = 0; k < YK; ++k)
+                    if (yl[k] < L) {
+                        const cd w = cmul(s_ps[tt * P + ypl[k]], s_m[tt * MS + yal[k]]);
+                        Y[k] = cfmac(Y[k], w, s_y[tt * NR + yrr[k]]);
+                    }
+            }
+        }
+    }
+#pragma unroll
+    for (int k1 = 0; k1 < KB; ++k1)
+#pragma unroll
+        for (int k2 = 0; k2 < KB; ++k2)
+            if (swp[k1][k2]) A[k1][k2] = cconj(A[k1][k2]);
+    if (write_sys) {                                 // sbce_mstep's r_out / rhs_out
+        cd* R = a.R + (size_t)b * L * L;
+#pragma unroll
+        for (int k1 = 0; k1 < KB; ++k1)
+#pragma unroll
+            for (int k2 = 0; k2 < KB; ++k2)
+                if (need[k1][k2]) R[(size_t)(ti + 16 * k1) * L + tj + 16 * k2] = A[k1][k2];
+        cd* rh = a.rhs + (size_t)b * L * NR;
+#pragma unroll
+        for (int k = 0; k < YK; ++k)
+            if (yl[k] < L) rh[tid + kSmallThreads * k] = Y[k];
+    }
+    if (stop == 1 || stop == 3) return;              // DIAGNOSTIC phase timing (results invalid)
+
+    // ---- 2. tol = 1e-14 max diag R (diag_tol_kernel); Cholesky + forward substitution ------------
+    double mx = 0.0;
+#pragma unroll
+    for (int k = 0; k < KB; ++k)
+        if (ti == tj && ti + 16 * k < L) mx = fmax(mx, A[k][k].x);
+    for (int off = 32; off >= 1; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+    if (lane == 0) red[wave] = mx;
+    __syncthreads();
+    const double tol = 1e-14 * fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    const bool chol = a.solve_mode == SBCE_SOLVE_CHOL;
+    bool anybad = false;
+#pragma unroll
+    for (int kc = 0; kc < KB; ++kc) {
+        for (int cl = 0; cl < 16; ++cl) {
+            const int c = 16 * kc + cl;
+            if (c >= L) break;
+            cd* col = xb + (c & 1) * (64 + 8);
+            if (tj == cl) {                          // column c (rows >= c), fully updated
+#pragma unroll
+                for (int k1 = 0; k1 < KB; ++k1) {
+                    const int i = ti + 16 * k1;
+                    if (i >= c && i < L) col[i] = A[k1][kc];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < YK; ++k)
+                if (yl[k] == c) col[64 + (tid + kSmallThreads * k - c * NR)] = Y[k];
+            __syncthreads();
+            const double dia = col[c].x;
+            const bool bad = !(dia > tol);
+            const bool drop = bad && !chol;
+            const double piv = sqrt(bad ? tol : dia);
+            const double inv = drop ? 0.0 : 1.0 / piv;
+            anybad |= bad;
+            if (tid == 0) dinv[c] = inv;
+            if (tj == cl) {
+#pragma unroll
+                for (int k1 = 0; k1 < KB; ++k1) {
+                    const int i = ti + 16 * k1;
+                    if (i == c) A[k1][kc] = cmk(drop ? 0.0 : piv, 0.0);
+                    else if (i > c && i < L) A[k1][kc] = cscale(A[k1][kc], inv);
+                }
+            }
+            cd li[KB], lj[KB];
+#pragma unroll
+            for (int k = 0; k < KB; ++k) {
+                li[k] = cscale(col[(ti + 16 * k) & 63], inv);
+                lj[k] = cscale(col[(tj + 16 * k) & 63], inv);
+            }
+#pragma unroll
+            for (int k1 = 0; k1 < KB; ++k1)
+#pragma unroll
+                for (int k2 = 0; k2 < KB; ++k2) {
+                    const int i = ti + 16 * k1, j = tj + 16 * k2;
+                    if (j > c && j <= i && i < L) A[k1][k2] = csub(A[k1][k2], cmulc(li[k1], lj[k2]));
+                }
+#pragma unroll
+            for (int k = 0; k < YK; ++k) {
+                const int r = tid + kSmallThreads * k - yl[k] * NR;
+                if (yl[k] == c) {
+                    Y[k] = cscale(Y[k], inv);
+                } else if (yl[k] > c && yl[k] < L) {
+                    Y[k] = csub(Y[k], cmul(cscale(col[yl[k]], inv), cscale(col[64 + r], inv)));
+                }
+            }
+        }
+    }
+    if (stop == 2) return;
+
+    // ---- 3. back substitution L^H x = y (y_i -= x_c conj(l_ci)), theta = conj(x) ------------------
+#pragma unroll
+    for (int kc = KB - 1; kc >= 0; --kc) {
+        for (int cl = 15; cl >= 0; --cl) {
+            const int c = 16 * kc + cl;
+            if (c >= L) continue;
+            cd* row = xb + (c & 1) * (64 + 8);
+            if (ti == cl) {                          // row c of L left of the diagonal
+#pragma unroll
+                for (int k2 = 0; k2 < KB; ++k2) {
+                    const int j = tj + 16 * k2;
+                    if (j < c) row[j] = A[kc][k2];
+                }
+            }
+            const double iv = dinv[c];
+#pragma unroll
+            for (int k = 0; k < YK; ++k)
+                if (yl[k] == c) {
+                    Y[k] = cscale(Y[k], iv);
+                    row[64 + (tid + kSmallThreads * k - c * NR)] = Y[k];
+                }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < YK; ++k) {
+                const int r = tid + kSmallThreads * k - yl[k] * NR;
+                if (yl[k] < c) Y[k] = csub(Y[k], cmulc(row[64 + r], row[yl[k]]));
+            }
+        }
+    }
+    cd* th = a.theta + (size_t)b * L * NR;
+#pragma unroll
+    for (int k = 0; k < YK; ++k)
+        if (yl[k] < L) th[tid + kSmallThreads * k] = cconj(Y[k]);
+    if (tid == 0 && a.status && anybad) a.status[b] |= a.clamp_status;
+}
+
+template <int KB>
+hipError_t launch_nr(const Problem& pb, const MstepArgs& a, size_t lds, int write_sys,
+                     hipStream_t s) {
+    switch (pb.NR) {
+#define SBCE_MS(n) case n: hipLaunchKernelGGL((mstep_small_kernel<n, KB>), dim3(pb.B), dim3(kSmallThreads), lds, s, a, pb.NT, pb.P, pb.Tp, pb.Td, pb.L, write_sys, g_debug.small_stop); break;
+        SBCE_MS(1) SBCE_MS(2) SBCE_MS(3) SBCE_MS(4) SBCE_MS(5) SBCE_MS(6) SBCE_MS(7) SBCE_MS(8)
+#undef SBCE_MS
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+bool mstep_small_supported(const Problem& pb, int solve_mode) {
+    return !g_debug.mstep_nosmall && !g_debug.chol_valu && chol_debug_skip_mask() == 0 &&
+           (solve_mode == SBCE_SOLVE_CHOL || solve_mode == SBCE_SOLVE_CHOL_DROP) &&
+           pb.L >= 1 && pb.L <= kSmallMaxL && pb.NR >= 1 && pb.NR <= 8 &&
+           !rbuild_herm_supported(pb);
+}
+
+hipError_t launch_mstep_small(const Problem& pb, const MstepArgs& a, bool write_sys, hipStream_t s) {
+    const size_t lds = (kStageCd + 2 * (64 + 8)) * sizeof(cd) + (64 + 4) * sizeof(double);
+    const int w = write_sys ? 1 : 0;
+    switch ((pb.L + 15) / 16) {
+        case 1: return launch_nr<1>(pb, a, lds, w, s);
+        case 2: return launch_nr<2>(pb, a, lds, w, s);
+        case 3: return launch_nr<3>(pb, a, lds, w, s);
+        case 4: return launch_nr<4>(pb, a, lds, w, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace sbce

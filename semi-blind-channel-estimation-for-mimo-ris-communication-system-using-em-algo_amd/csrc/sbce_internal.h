@@ -174,7 +174,13 @@ struct DebugConfig {
     bool chol_valu;      // SBCE_CHOL_IMPL=valu    VALU blocked Cholesky (L <= 1024)
     bool estep_nopair;   // SBCE_ESTEP_PAIR=0      no factorised-weight pass (estep_pair.hip)
     bool cplx3;          // SBCE_CPLX3=0           four real MFMAs per complex product (default: three, Gauss)
-    bool pm_wave;        // SBCE_PM_IMPL=wave      ZF/MMSE E-step one wave per symbol at n_tx <= 2 too
+    bool mstep_nosmall;  // SBCE_MSTEP_SMALL=0     L <= 64: the batched build + panel Cholesky instead of
+                         //                        the one-workgroup M-step (mstep_small.hip)
+    int small_stop;      // SBCE_SMALL_STOP=1|2|3  DIAGNOSTIC: the one-workgroup M-step stops after its
+                         //                        build (1) / factorisation (2) / symbol staging
+                         //                        without the build's arithmetic (3); results invalid
+    bool pm_wave;        // SBCE_PM_IMPL=wave      ZF/MMSE (n_tx <= 2) and PM (n_tx = 2, |A| = 1) E-steps
+                         //                        one wave per symbol too
                          //                        (bitwise the thread kernel's results; not flagged)
 };
 extern DebugConfig g_debug;
@@ -287,6 +293,11 @@ hipError_t launch_mstep_build(const Problem& pb, const MstepArgs& a, hipStream_t
                               bool pilots_factored = false);
 hipError_t launch_chol_solve(const Problem& pb, const MstepArgs& a, hipStream_t s);
 bool chol_supported(const Problem& pb);
+// L <= 64 (n_tx not 4, 8), CHOL / CHOL_DROP: build + solve of one trial in one workgroup
+// (mstep_small.hip); write_sys also stores R and B^H in a.R / a.rhs (sbce_mstep's outputs)
+bool mstep_small_supported(const Problem& pb, int solve_mode);
+hipError_t launch_mstep_small(const Problem& pb, const MstepArgs& a, bool write_sys, hipStream_t s);
+int chol_debug_skip_mask();
 constexpr int kLargeL = 512;   // L above this: tiled build + blocked right-looking Cholesky
 constexpr int kMaxL = 8192;    // largest supported L (R alone is 1 GiB per trial there)
 bool rbuild_herm_supported(const Problem& pb);   // MFMA build of the Hermitian R: NT in {4, 8}

@@ -482,6 +482,63 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape):
     assert rel(th_m, out["batched_bs1"][0]) < 1e-12
 
 
+@pytest.mark.parametrize("shape", [
+    # (n_tx, n_rx, N, T_p, T_d, M)      L = (N+1) n_tx <= 64: the one-workgroup M-step
+    (2, 2, 15, 20, 120, 64),            # BASELINE cfg 5 (L = 32)
+    (1, 3, 40, 8, 61, 4),               # L = 41, ragged everything
+    (3, 2, 20, 10, 50, 4),              # L = 63
+    (2, 8, 31, 20, 100, 16),            # L = 64, n_rx = 8
+    (1, 1, 0, 3, 2, 4),                 # L = 1
+    (2, 2, 15, 4, 5, 4),                # T_p + T_d < L: clamped / dropped pivots
+])
+@pytest.mark.parametrize("solve", ["chol", "drop"])
+def test_small_mstep_matches_batched_path(sbce, shape, solve):
+    """L <= 64 (n_tx <= 3): R and B^H built by mstep_small_kernel are bitwise the batched build's
+    (same per-element operation order); its in-LDS Cholesky solve agrees with the batched panel
+    Cholesky (SBCE_MSTEP_SMALL=0) and numpy.linalg.solve; the same trials are flagged."""
+    n_tx, n_rx, N, T_p, T_d, M = shape
+    b = sbce.signal_model.synthetic_batch(3, n_tx, n_rx, N, T_p, T_d, M, 0.1, seed=41)
+    x = b["x_d"]
+    S = x[..., :, None] * np.conj(x[..., None, :]) + 0.05 * np.eye(n_tx)
+    th, R, rhs, st = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], x, S,
+                                      0.1, solve=solve)
+    with sbce._lib.debug_env(SBCE_MSTEP_SMALL="0"):
+        th0, R0, rhs0, st0 = sbce.mstep_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"],
+                                              x, S, 0.1, solve=solve)
+    assert np.array_equal(R, R0) and np.array_equal(rhs, rhs0)
+    assert np.array_equal(st, st0 & ~8)              # bit 8: the debug switch itself
+    assert np.isfinite(th).all()
+    for i in range(3):
+        if st[i]:
+            continue                                 # clamped: a different rounding of garbage
+        X = np.linalg.solve(R[i], rhs[i])
+        cond = np.linalg.cond(R[i])
+        tol = max(1e-12, 1e-15 * cond)
+        assert rel(th[i], np.conj(X).reshape(-1)) < tol, cond
+        assert rel(th[i], th0[i]) < tol, cond
+    if T_p + n_tx * T_d < (N + 1) * n_tx:          # rank R <= T_p + n_tx T_d < L
+        assert st.all()
+
+
+def test_small_mstep_full_em_matches_batched_path(sbce):
+    """Five EM iterations at BASELINE cfg 5's shape (soft and PM-soft E-steps, per-trial noise
+    variances, the oracle early stop): one-workgroup M-step vs the batched path."""
+    varn = np.array([float(sbce.signal_model.snr_to_varn(s, 42.0)) for s in (0.0, 10.0, 20.0, 30.0)])
+    b = sbce.signal_model.synthetic_batch(4, 2, 2, 15, 20, 60, 64, 1.0, seed=43, pinv="scipy")
+    for mode in ("soft", "pm_soft"):
+        eng = sbce.EMEngine(b, varn, mode=mode, early_stop=True,
+                            partition_r=1 if mode == "pm_soft" else 0)
+        th = eng.run(5).cpu().numpy()
+        it = eng.iters_done.cpu().numpy()
+        with sbce._lib.debug_env(SBCE_MSTEP_SMALL="0"):
+            eng0 = sbce.EMEngine(b, varn, mode=mode, early_stop=True,
+                                 partition_r=1 if mode == "pm_soft" else 0)
+            th0 = eng0.run(5).cpu().numpy()
+            it0 = eng0.iters_done.cpu().numpy()
+        assert np.array_equal(it, it0), mode
+        assert rel(th, th0) < 1e-9, mode
+
+
 # ---------------------------------------------------------------- large-L M-step (L > 512)
 @pytest.mark.parametrize("shape", [
     # (n_tx, n_rx, N, T_p, T_d)       L = (N+1) n_tx
@@ -585,6 +642,27 @@ def test_detector_estep_vs_oracle(sbce, shape):
                 continue          # the reference would raise; the device flags the trial
             assert np.array_equal(m[i], m0)
             assert np.allclose(S[i], S0, rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("shape", [(2, 2, 15, 20, 120, 64, -5), (2, 2, 15, 20, 60, 64, 33),
+                                   (2, 1, 6, 8, 40, 4, 0), (2, 4, 4, 8, 33, 16, 10),
+                                   (2, 8, 3, 12, 50, 64, 20), (2, 3, 2, 8, 17, 4, 40)])
+def test_pm_thread_kernel_bitwise_wave_kernel(sbce, shape):
+    """PM / PM-soft at n_tx = 2 with a one-stream list (partition_r = 1 < log2 M, BASELINE cfg 5)
+    run one thread per symbol; the one-wave-per-symbol kernel (SBCE_PM_IMPL=wave) gives bitwise
+    the same m and S (greedy order, G_B, nearest points, butterfly weight sum, moment order)."""
+    n_tx, n_rx, N, T_p, T_d, M, snr = shape
+    varn = float(sbce.signal_model.snr_to_varn(snr))
+    b = sbce.signal_model.synthetic_batch(3, n_tx, n_rx, N, T_p, T_d, M, varn, seed=47)
+    for kind in ("pm", "pm_soft"):
+        m, S = sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx, kind,
+                                partition_r=1)
+        with sbce._lib.debug_env(SBCE_PM_IMPL="wave"):
+            mw, Sw = sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx,
+                                      kind, partition_r=1)
+        assert np.array_equal(m, mw, equal_nan=True), kind
+        assert np.array_equal(S, Sw, equal_nan=True), kind
+        assert np.isfinite(m).all(), kind
 
 
 @pytest.mark.parametrize("shape", [(2, 2, 15, 20, 120, 64, -5), (2, 2, 15, 20, 60, 64, 33),

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""GPU busy time of a rocprofv3 --kernel-trace run (rocpd SQLite output): the span from the
+first kernel start to the last kernel end, the union of all kernel intervals (time the GPU ran
+at least one kernel), per-stream busy time, and the idle gaps -- whether a multi-stream run is
+bound by the kernels or by the host's launch rate.
+
+  python tools/trace_timeline.py gpurun_out/<tag>/trace [--last-frac 0.5]
+"""
+import glob
+import os
+import sqlite3
+import sys
+
+
+def main():
+    d = sys.argv[1]
+    frac = float(sys.argv[sys.argv.index("--last-frac") + 1]) if "--last-frac" in sys.argv else 1.0
+    dbs = glob.glob(os.path.join(d, "**", "*.db"), recursive=True)
+    if not dbs:
+        raise SystemExit(f"no rocpd database under {d}")
+    con = sqlite3.connect(dbs[0])
+    cols = [c[1] for c in con.execute("pragma table_info(kernels)").fetchall()]
+    print("columns:", cols)
+    sc = next((c for c in ("stream_id", "stream", "queue_id", "queue") if c in cols), None)
+    rows = con.execute(f"select start, end, {sc or 0}, name from kernels order by start").fetchall()
+    t0, t1 = rows[0][0], max(r[1] for r in rows)
+    cut = t1 - (t1 - t0) * frac                       # the last `frac` of the run (timed steps)
+    rows = [r for r in rows if r[0] >= cut]
+    t0 = rows[0][0]
+    span = t1 - t0
+    busy, cur_s, cur_e = 0, None, None
+    gaps = []
+    for s, e, _, _ in rows:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+                gaps.append(s - cur_e)
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    busy += cur_e - cur_s
+    per = {}
+    for s, e, q, _ in rows:
+        per[q] = per.get(q, 0) + (e - s)
+    ksum = sum(r[1] - r[0] for r in rows)
+    print(f"kernels {len(rows)}  span {span / 1e6:.2f} ms  union busy {busy / 1e6:.2f} ms "
+          f"({100 * busy / span:.1f}%)  sum of kernel time {ksum / 1e6:.2f} ms "
+          f"(mean concurrency while busy {ksum / max(busy, 1):.2f})")
+    for q, t in sorted(per.items(), key=lambda x: -x[1]):
+        print(f"  stream {q}: {t / 1e6:.2f} ms")
+    gaps.sort()
+    if gaps:
+        tot = sum(gaps)
+        print(f"idle gaps {len(gaps)}: total {tot / 1e6:.2f} ms, median {gaps[len(gaps) // 2] / 1e3:.1f} us, "
+              f"max {gaps[-1] / 1e3:.1f} us")
+
+
+if __name__ == "__main__":
+    main()
