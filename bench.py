@@ -400,6 +400,9 @@ def parse_args(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="cfg5: only the roofline launches (the largest T_d point's E-steps and "
+                         "M-step), no grid steps -- for the PMC passes of tools/profile_cfg5.sh")
     ap.add_argument("--streams", type=int, default=None,
                     help="sub-batches on concurrent HIP streams per GPU (default: 3 at cfg1, else 1)")
     ap.add_argument("--rccl-init", choices=["lazy", "eager"], default="lazy",
@@ -544,6 +547,60 @@ def grid_cpu_baseline(g, seed, td=60, snr=15.0):
                       f"threads={threads or 'default'}), {dt:.2f} s"}
 
 
+def grid_roofline(args, g, engines, k_last, torch):
+    """cfg5 roofline: every detector's E-step and the M-step at the largest T_d point (the grid's
+    costliest launches; the SNR axis batched, B = trials x 20), timed alone with HIP events on the
+    launch stream at theta = h (the converged regime the oracle early stop leaves most trials in).
+    The dominant launch (the exact soft E-step) is priced at its data-independent enumeration work,
+    estep_flops_per_trial_iter: T_d M^n_tx (4 n_rx + 2) flop per trial, against the FP64 peak (the
+    tree / BFS passes run on the FP64 VALU, the tile sweep on FP64 MFMA: 78.6 TF/s either way)."""
+    n_tx, n_rx, N, M = g["n_tx"], g["n_rx"], g["N"], g["M"]
+    P = N + 1
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for _ in range(args.kernel_reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / args.kernel_reps
+
+    phases, B, T_d, soft_eng = {}, None, None, None
+    for di, k, js, eng in engines:
+        det = g["detectors"][di]
+        if k != k_last or f"estep_{det}" in phases:
+            continue
+        eng.theta.copy_(eng.h)
+        phases[f"estep_{det}"] = timed(eng.estep)
+        B, T_d = eng.B, eng.T_d
+        if det == "soft":
+            soft_eng = eng
+    if soft_eng is not None:
+        phases["mstep"] = timed(soft_eng.mstep)
+    pmc = load_pmc_traffic(args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}_latest.json"))
+    pmc_ok = bool(pmc and pmc.get("config") == args.config and pmc.get("trials") == B)
+    ms = phases.get("estep_soft")
+    flops = estep_flops_per_trial_iter(n_tx, n_rx, T_d, M) * B
+    algo = estep_bytes_per_trial_iter(n_tx, n_rx, P, T_d) * B
+    traffic = phase_traffic(pmc, ESTEP_KERNELS, ESTEP_KERNELS) if pmc_ok else None
+    ach = flops / (ms * 1e-3) / 1e12 if ms else None
+    roof = {"bound": "mfma", "pipe": "FP64 (VALU tree / BFS passes + MFMA tile sweep)",
+            "phase": "exact soft E-step (the grid's dominant launch)", "kernels": ESTEP_KERNELS,
+            "point": {"T_d": T_d, "trials": B, "theta": "h (converged regime)"},
+            "ms": ms, "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": ach / FP64_PEAK_TFLOPS if ach else None, "flops_per_launch": flops,
+            "flops_note": "data-independent enumeration work T_d M^n_tx (4 n_rx + 2) per trial; "
+                          "the pruned search issues less",
+            "traffic": traffic, "algorithmic_bytes": algo,
+            "traffic_ratio": traffic / algo if traffic else None,
+            "hbm_frac_algorithmic": algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS if ms else None}
+    return {"roofline": roof, "phases": {k: v for k, v in phases.items()}}
+
+
 def grid_main(args, ranks, pkg):
     """--config cfg5: one step = the whole SNR x T_d grid, five detector EMs per point, `trials`
     Monte-Carlo trials per point on every rank.  Calls are spread over 3 HIP streams.  value =
@@ -558,6 +615,8 @@ def grid_main(args, ranks, pkg):
     n_tx, n_rx, N, T_p, M, B, iters = (g[k] for k in ("n_tx", "n_rx", "N", "T_p", "M", "trials",
                                                         "iters"))
     T_D, SNR, dets = g["T_d"], g["SNR"], g["detectors"]
+    if args.roofline_only:
+        T_D = T_D[-1:]
     varns = [float(v) for v in pkg.signal_model.snr_to_varn(SNR, g["power"])]
     ns, nt, nd = len(SNR), len(T_D), len(dets)
     engines = []                     # (detector index, T_d index, SNR indices, engine)
@@ -594,6 +653,12 @@ def grid_main(args, ranks, pkg):
         for st in streams:
             cur.wait_stream(st)
 
+    if args.roofline_only:
+        roof = grid_roofline(args, g, engines, len(T_D) - 1, torch)
+        if rank == 0:
+            print(json.dumps({"roofline_only": args.config, "roofline": roof}), flush=True)
+        ranks.close()
+        return
     for _ in range(args.warmup):
         step()
     ranks.barrier()
@@ -621,6 +686,7 @@ def grid_main(args, ranks, pkg):
     mean = a[..., 0] / a[..., 1]
     executed = float(acc[-1].item())
     flagged = sum(int((eng.status != 0).sum().item()) for _, _, _, eng in engines)
+    roof = grid_roofline(args, g, engines, len(T_D) - 1, torch)   # overwrites theta: after NMSE
     line = {
         "metric": metric_name(n_tx, N, T_p, f"{T_D[0]}..{T_D[-1]}") + " (SNR x T_d grid, five EMs)",
         "value": executed * args.steps / elapsed,
@@ -644,6 +710,8 @@ def grid_main(args, ranks, pkg):
         "nmse_grid_mean": {det: float(np.mean(mean[di])) for di, det in enumerate(dets)},
         "nmse_at_max_td": {det: [float(v) for v in mean[di, -1]] for di, det in enumerate(dets)},
         "status_flagged_trials": flagged,
+        "roofline": roof["roofline"],
+        "phases_at_max_td": roof["phases"],
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = grid_cpu_baseline(g, args.seed)
