@@ -48,6 +48,31 @@ def main():
           f"(mean concurrency while busy {ksum / max(busy, 1):.2f})")
     for q, t in sorted(per.items(), key=lambda x: -x[1]):
         print(f"  stream {q}: {t / 1e6:.2f} ms")
+    # segments separated by idle gaps > 2 ms (the bench's steps vs its setup / timing phases)
+    seg, segs = [rows[0]], []
+    cur_e = rows[0][1]
+    for r in rows[1:]:
+        if r[0] - cur_e > 2e6:
+            segs.append(seg)
+            seg = []
+        seg.append(r)
+        cur_e = max(cur_e, r[1])
+    segs.append(seg)
+    for sg in segs:
+        a0, a1 = sg[0][0], max(r[1] for r in sg)
+        ks = sum(r[1] - r[0] for r in sg)
+        ub, cs, ce = 0, None, None
+        for s_, e_, _, _ in sg:
+            if ce is None or s_ > ce:
+                if ce is not None:
+                    ub += ce - cs
+                cs, ce = s_, e_
+            else:
+                ce = max(ce, e_)
+        ub += ce - cs
+        qs = len(set(r[2] for r in sg))
+        print(f"  segment {(a0 - t0) / 1e6:9.2f} ms +{(a1 - a0) / 1e6:8.2f} ms: {len(sg):5d} kernels on {qs} "
+              f"streams, busy {100 * ub / max(a1 - a0, 1):5.1f}%, concurrency {ks / max(ub, 1):.2f}")
     gaps.sort()
     if gaps:
         tot = sum(gaps)
