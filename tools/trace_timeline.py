@@ -73,6 +73,15 @@ def main():
         qs = len(set(r[2] for r in sg))
         print(f"  segment {(a0 - t0) / 1e6:9.2f} ms +{(a1 - a0) / 1e6:8.2f} ms: {len(sg):5d} kernels on {qs} "
               f"streams, busy {100 * ub / max(a1 - a0, 1):5.1f}%, concurrency {ks / max(ub, 1):.2f}")
+    if "--dump" in sys.argv:                     # N kernels from the middle of the longest segment
+        n = int(sys.argv[sys.argv.index("--dump") + 1])
+        sg = max(segs, key=lambda x: max(r[1] for r in x) - x[0][0])
+        mid = len(sg) // 2
+        w = sg[max(0, mid - n // 2): mid + n // 2]
+        base = w[0][0]
+        for s_, e_, q, nm in w:
+            short = nm.replace("(anonymous namespace)::", "").replace("void sbce::", "")[:48]
+            print(f"    {(s_ - base) / 1e3:9.1f} {(e_ - base) / 1e3:9.1f} us  q{q}  {short}")
     gaps.sort()
     if gaps:
         tot = sum(gaps)
