@@ -17,7 +17,7 @@ DebugConfig g_debug;
 
 namespace {
 constexpr DebugConfig kDebugDefault = {false, false, false, false, 0, false, 128, false, false, false,
-                                       true, false, 0, false};
+                                       true, false, false, 0, false};
 constexpr int kSphereBudgetMax = 256;      // estep.hip kBfsPmax
 
 void read_debug_env(DebugConfig& c) {
@@ -38,7 +38,7 @@ void read_debug_env(DebugConfig& c) {
     if ((v = env("SBCE_CHOL_IMPL"))) c.chol_valu = v[0] == 'v';
     if ((v = env("SBCE_ESTEP_PAIR"))) c.estep_nopair = v[0] == '0';
     if ((v = env("SBCE_CPLX3"))) c.cplx3 = v[0] != '0';
-    if ((v = env("SBCE_MSTEP_SMALL"))) c.mstep_nosmall = v[0] == '0';
+    if ((v = env("SBCE_MSTEP_SMALL"))) { c.mstep_nosmall = v[0] == '0'; c.small_valu = v[0] == 'v'; }
     if ((v = env("SBCE_PM_IMPL"))) c.pm_wave = v[0] == 'w';
     if ((v = env("SBCE_SMALL_STOP"))) c.small_stop = (v[0] >= '1' && v[0] <= '3') ? v[0] - '0' : 0;
 }
@@ -55,6 +55,7 @@ bool debug_nondefault() {
            c.backsub_general != d.backsub_general || c.chol_valu != d.chol_valu ||
            c.estep_nopair != d.estep_nopair || c.cplx3 != d.cplx3 ||
            c.mstep_nosmall != d.mstep_nosmall || c.small_stop != d.small_stop ||
+           c.small_valu != d.small_valu ||
            (chol_debug_skip_mask() & 31);
 }
 

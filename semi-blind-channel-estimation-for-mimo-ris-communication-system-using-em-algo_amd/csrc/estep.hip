@@ -1544,6 +1544,47 @@ __device__ __forceinline__ double pair_screen(const cd (&H)[NT][NR], const cd (&
     }
 }
 
+// NT = 2, square QAM (estep_pair.hip estep_fact2_kernel): D = (sum of the eight log-table maxima)
+// - l(x_c), both times 1/s2, with x_c the prep candidate (a real hypothesis: l(x_c) <= max l).  The
+// 1-D tables' maxima over the constellation's real / imaginary parts, the bilinear ones at the
+// corners of the level box.  The factorised pass represents every weight within e^-50 of the
+// largest as a normal double when D <= kPairDmax.
+template <int NR>
+__device__ __forceinline__ double fact2_bound(const cd (&H)[2][NR], const cd (&y)[NR], int xidx,
+                                              const cd* cons, int M, double inv_s2) {
+    cd z0 = czero(), z1 = czero(), g = czero();
+    double g00 = 0.0, g11 = 0.0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        z0 = cfmac(z0, y[r], H[0][r]);
+        z1 = cfmac(z1, y[r], H[1][r]);
+        g = cfmac(g, H[1][r], H[0][r]);
+        g00 += cabs2(H[0][r]);
+        g11 += cabs2(H[1][r]);
+    }
+    double fa0 = -INFINITY, fb0 = -INFINITY, fa1 = -INFINITY, fb1 = -INFINITY;
+    double amin = INFINITY, amax = -INFINITY, bmin = INFINITY, bmax = -INFINITY;
+    for (int s = 0; s < M; ++s) {
+        const double av = cons[s].x, bv = cons[s].y;
+        fa0 = fmax(fa0, 2.0 * av * z0.x - g00 * av * av);
+        fb0 = fmax(fb0, 2.0 * bv * z0.y - g00 * bv * bv);
+        fa1 = fmax(fa1, 2.0 * av * z1.x - g11 * av * av);
+        fb1 = fmax(fb1, 2.0 * bv * z1.y - g11 * bv * bv);
+        amin = fmin(amin, av); amax = fmax(amax, av);
+        bmin = fmin(bmin, bv); bmax = fmax(bmax, bv);
+    }
+    auto corner = [](double k, double u0, double u1, double v0, double v1) {
+        return fmax(fmax(k * u0 * v0, k * u0 * v1), fmax(k * u1 * v0, k * u1 * v1));
+    };
+    const double tmax = corner(-2.0 * g.x, amin, amax, amin, amax) + corner(2.0 * g.y, amin, amax, bmin, bmax) +
+                        corner(-2.0 * g.y, bmin, bmax, amin, amax) + corner(-2.0 * g.x, bmin, bmax, bmin, bmax);
+    const cd x0 = cons[xidx & 255], x1 = cons[(xidx >> 8) & 255];
+    const double lc = 2.0 * (x0.x * z0.x + x0.y * z0.y) - g00 * cabs2(x0) + 2.0 * (x1.x * z1.x + x1.y * z1.y) -
+                      g11 * cabs2(x1) -
+                      2.0 * (x0.x * x1.x * g.x - x0.x * x1.y * g.y + x0.y * x1.x * g.y + x0.y * x1.y * g.x);
+    return (fa0 + fb0 + fa1 + fb1 + tmax - lc) * inv_s2;
+}
+
 // Column-tile bounds (column_tile_bounds) and, for NT = 4, the row-tile bound vectors of
 // one symbol into its prep record `out`.
 template <int NT, int NR>
@@ -1812,6 +1853,7 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
         c.reg = tn.reg; c.thr_d = tn.thr_d; c.inv_s2 = tn.inv_s2;
     }
     bool single = false;
+    double f2d = INFINITY;            // NT = 2: the factorised pass's range bound (fact2_bound)
     if (live) {
     cd Lm[NT][NT], zf[NT];
     double piv[NT], dinv[NT], d0, sc, screen, gsum;
@@ -1836,9 +1878,10 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
         out[0] = d0;
         out[1] = sc;
         screen = pair_screen<NT, NR>(H, y, xidx, cons, gsum);
+        if constexpr (NT == 2) f2d = c.pair ? fact2_bound<NR>(H, y, xidx, cons, c.M, c.inv_s2) : INFINITY;
         // computed here, while H and y are live anyway (left to the compiler, the computation
         // sinks to the record store at the end and keeps H_eff live across the whole kernel)
-        asm volatile("" : "+v"(screen), "+v"(gsum));
+        asm volatile("" : "+v"(screen), "+v"(gsum), "+v"(f2d));
         // reliability of stream q: g_q = [(G + reg I)^-1]_qq = sum_k |(L^-1)_kq|^2
         cd W[NT][NT];
         double g[NT];
@@ -1987,11 +2030,25 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
             ++k;
         }
     }   // live
-    // the other live symbols go to the enumeration's list: one atomic per wave
-    const bool enumer = live && !single;
+    // NT = 2 soft: a symbol the factorised pass can represent goes to its list (counter 3); the
+    // other live symbols go to the enumeration's list: one atomic per wave and list
+    const bool f2 = NT == 2 && live && !single && f2d <= kPairDmax;
+    const bool enumer = live && !single && !f2;
     const int lane = threadIdx.x & 63;
-    const unsigned long long bal = __ballot(enumer);
     int32_t* cnt = a.list + nsym;
+    if (NT == 2) {
+        const unsigned long long bf = __ballot(f2);
+        if (bf) {
+            const int first = __builtin_ctzll(bf);
+            int base = 0;
+            if (lane == first) base = atomicAdd(cnt + 3, __builtin_popcountll(bf));
+            base = __shfl(base, first);
+            if (f2)
+                a.list[2 * nsym + 2 * kEstepListCnt + base + __builtin_popcountll(bf & ((1ull << lane) - 1ull))] =
+                    (int32_t)gsym;
+        }
+    }
+    const unsigned long long bal = __ballot(enumer);
     if (bal) {
         const int first = __builtin_ctzll(bal);
         int base = 0;

@@ -323,11 +323,209 @@ __global__ __launch_bounds__(64 * kPairWaves) __attribute__((amdgpu_waves_per_eu
     flush();
 }
 
+
+// ---------------------------------------------------------------- n_tx = 2, square M-QAM
+// The same idea for two streams (BASELINE cfg 5: 2 x 2, 64-QAM, J = 4096 hypotheses).  With
+// x_a = a_a + i b_a on a K x K level grid, z_a = h_a^H y, g_aa = ||h_a||^2, g = h_0^H h_1,
+//   l(x) s2 + ||y||^2 = [2 a0 Re z0 - g00 a0^2] + [2 b0 Im z0 - g00 b0^2] + (same for x1)
+//                     - 2 [a0 a1 Re g - a0 b1 Im g + b0 a1 Im g + b0 b1 Re g],
+// four 1-D tables and four K x K tables, each exponentiated after subtracting its maximum.  The
+// bilinear part couples {a0, b0} only with {a1, b1}, so for fixed (a0, b0) the sum over (a1, b1)
+// is a PRODUCT of a sum over a1 and a sum over b1:
+//   Z = sum_{a0,b0} F(a0) G(b0) U(a0,b0) V(a0,b0),  U = sum_a1 F1(a1) T1(a0,a1) T3(b0,a1),
+//   V = sum_b1 G1(b1) T2(a0,b1) T4(b0,b1),
+// and every moment E[x_a], E[x_a conj(x_b)] takes a1- / b1-weighted versions of U and V.  One
+// WAVE per symbol, lane = (a0, b0): 288 exponentials and ~100 VALU ops per lane plus eleven wave
+// sums instead of 4096 distances and exponentials.  Range as above: the largest weight is
+// >= exp(-D), D = (sum of the eight table maxima) - l(x_c); the tree pass routes a symbol here
+// only when its D (estep.hip fact2_bound) is within kPairDmax, and a symbol whose sum Z still
+// leaves the normal range joins the sweep's list.
+constexpr int kF2Waves = 4;
+
+template <int NR>
+__global__ __launch_bounds__(64 * kF2Waves) void estep_fact2_kernel(EstepArgs a, PairConst c, int M) {
+    constexpr int NT = 2, MS = NT + NT * NT;
+    __shared__ cd s_cons[64];
+    __shared__ GridLds s_grid;
+    __shared__ double s_tab[kF2Waves][4 * 8 + 4 * 64];   // F0 G0 F1 G1 [8], T1 T2 T3 T4 [8][8]
+    __shared__ int32_t s_fail[kF2Waves][64];
+    if ((int)threadIdx.x < M) s_cons[threadIdx.x] = a.cons[threadIdx.x];
+    __syncthreads();
+    grid_build(s_cons, M, &s_grid);
+    const int K = s_grid.K;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const long nsym = (long)c.B * c.Td;
+    int32_t* cnt = a.list + nsym;                    // [0] the sweep's list, [3] this pass's
+    const int32_t* plist = a.list + 2 * nsym + 2 * kEstepListCnt;
+    const int nwork = __builtin_amdgcn_readfirstlane(cnt[3]);
+    double* tab = s_tab[wave];
+    double* F0 = tab;
+    double* G0 = tab + 8;
+    double* F1 = tab + 16;
+    double* G1 = tab + 24;
+    double* T1 = tab + 32;                           // [a0][a1]
+    double* T2 = T1 + 64;                            // [a0][b1]
+    double* T3 = T2 + 64;                            // [b0][a1]
+    double* T4 = T3 + 64;                            // [b0][b1]
+    const int nwaves = gridDim.x * kF2Waves;
+    int gi = blockIdx.x * kF2Waves + wave;
+    int32_t* s_f = s_fail[wave];
+    int nf = 0;
+    auto flush = [&]() {
+        if (nf == 0) return;
+        int base = 0;
+        if (lane == 0) base = atomicAdd(cnt, nf);
+        base = __shfl(base, 0);
+        if (lane < nf) a.list[base + lane] = s_f[lane];
+        nf = 0;
+        wave_sync();
+    };
+    auto wmax = [](double v) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v = fmax(v, shfl_xor_d(v, off));
+        return v;
+    };
+    auto wsum = [](double v) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += shfl_xor_d(v, off);
+        return v;
+    };
+    // symbols by a static stride (every symbol costs the same: no work grabbing), the next one's
+    // index, channel and observation loaded while the current one is computed
+    auto fetch = [&](int k, long& gs, cd (&hh)[2 * NR], cd (&yy)[NR]) {
+        gs = k < nwork ? (long)plist[k] : -1;
+        if (gs >= 0) {
+            const double* rec = a.prep + (size_t)gs * c.stride;
+#pragma unroll
+            for (int e = 0; e < 2 * NR; ++e) hh[e] = cmk(rec[4 + 2 * e], rec[5 + 2 * e]);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) yy[r] = a.yd[(size_t)gs * NR + r];
+        }
+    };
+    long gnext;
+    cd hnext[2 * NR], ynext[NR];
+    fetch(gi, gnext, hnext, ynext);
+    for (; gi < nwork; gi += nwaves) {
+        const long gsym = gnext;
+        cd hc[2 * NR], yc[NR];
+#pragma unroll
+        for (int e = 0; e < 2 * NR; ++e) hc[e] = hnext[e];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) yc[r] = ynext[r];
+        fetch(gi + nwaves, gnext, hnext, ynext);
+        const int b = (int)(gsym / c.Td);
+        if (a.done && a.done[b]) continue;
+        if (K == 0) {                                // not a square grid: the sweep weighs it
+            if (lane == 0) s_f[nf] = (int32_t)gsym;
+            ++nf;
+            if (nf == 64) flush();
+            continue;
+        }
+        const double is2 = a.varn_t ? uniform_d(trial_noise(a.varn_t[b]).inv_s2) : c.inv_s2;
+        cd z0 = czero(), z1 = czero(), g = czero();
+        double g00 = 0.0, g11 = 0.0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const cd h0 = hc[r], h1 = hc[NR + r], yr = yc[r];
+            z0 = cfmac(z0, yr, h0);                  // h_0^H y
+            z1 = cfmac(z1, yr, h1);
+            g = cfmac(g, h1, h0);                    // h_0^H h_1
+            g00 += cabs2(h0);
+            g11 += cabs2(h1);
+        }
+        // ---- log tables (times s2), their maxima, the exponentials into LDS ----
+        const int i = lane >> 3, j = lane & 7;       // lane = (row i, column j) of a K x K table
+        const bool on1 = lane < 4 * K, on2 = i < K && j < K;
+        double v1 = -INFINITY;                       // 1-D table entry: table lane / K, level lane % K
+        const int t1 = on1 ? lane / K : 0, k1 = on1 ? lane - t1 * K : 0;
+        if (on1) {
+            const double lv = (t1 & 1) ? s_grid.lim[k1] : s_grid.lre[k1];
+            const double zz = t1 == 0 ? z0.x : (t1 == 1 ? z0.y : (t1 == 2 ? z1.x : z1.y));
+            const double gg = t1 < 2 ? g00 : g11;
+            v1 = (2.0 * lv * zz - gg * lv * lv) * is2;
+        }
+        double w1 = -INFINITY, w2 = -INFINITY, w3 = -INFINITY, w4 = -INFINITY;
+        if (on2) {
+            const double ai = s_grid.lre[i], bi = s_grid.lim[i], aj = s_grid.lre[j], bj = s_grid.lim[j];
+            w1 = -2.0 * g.x * ai * aj * is2;         // T1(a0 = a_i, a1 = a_j)
+            w2 = 2.0 * g.y * ai * bj * is2;          // T2(a0 = a_i, b1 = b_j)
+            w3 = -2.0 * g.y * bi * aj * is2;         // T3(b0 = b_i, a1 = a_j)
+            w4 = -2.0 * g.x * bi * bj * is2;         // T4(b0 = b_i, b1 = b_j)
+        }
+        double m1[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) m1[t] = wmax((on1 && t1 == t) ? v1 : -INFINITY);
+        const double mT1 = wmax(w1), mT2 = wmax(w2), mT3 = wmax(w3), mT4 = wmax(w4);
+        // D = (sum of the maxima) - l(x_c) with x_c the best hypothesis on the diagonal of the
+        // lanes' own (a0, b0) x (a1 = a0, b1 = b0) grid is not needed: the tree pass bounded it;
+        // the sum Z below is checked for the normal range instead
+        wave_sync();                                 // the previous symbol's table reads are done
+        if (on1) tab[8 * t1 + k1] = exp(v1 - m1[t1]);
+        if (on2) {
+            T1[i * 8 + j] = exp(w1 - mT1);
+            T2[i * 8 + j] = exp(w2 - mT2);
+            T3[i * 8 + j] = exp(w3 - mT3);
+            T4[i * 8 + j] = exp(w4 - mT4);
+        }
+        wave_sync();
+        // ---- lane (a0 = level i, b0 = level j): the a1 and b1 sums ----
+        double P = 0.0, Pa1 = 0.0, Pb1 = 0.0, P11 = 0.0;
+        double a0 = 0.0, b0 = 0.0;
+        if (on2) {
+            a0 = s_grid.lre[i];
+            b0 = s_grid.lim[j];
+            double U = 0.0, U1 = 0.0, U2 = 0.0, V = 0.0, V1 = 0.0, V2 = 0.0;
+            for (int k = 0; k < K; ++k) {
+                const double a1 = s_grid.lre[k], b1 = s_grid.lim[k];
+                const double eu = F1[k] * T1[i * 8 + k] * T3[j * 8 + k];
+                U += eu;
+                U1 = fma(a1, eu, U1);
+                U2 = fma(a1 * a1, eu, U2);
+                const double ev = G1[k] * T2[i * 8 + k] * T4[j * 8 + k];
+                V += ev;
+                V1 = fma(b1, ev, V1);
+                V2 = fma(b1 * b1, ev, V2);
+            }
+            const double w = F0[i] * G0[j];
+            P = w * U * V;
+            Pa1 = w * U1 * V;
+            Pb1 = w * U * V1;
+            P11 = w * fma(U2, V, U * V2);
+        }
+        const double Z = wsum(P);
+        const double Sa0 = wsum(a0 * P), Sb0 = wsum(b0 * P), S00 = wsum(fma(a0, a0, b0 * b0) * P);
+        const double Sa1 = wsum(Pa1), Sb1 = wsum(Pb1), S11 = wsum(P11);
+        const double Sa0a1 = wsum(a0 * Pa1), Sb0b1 = wsum(b0 * Pb1);
+        const double Sb0a1 = wsum(b0 * Pa1), Sa0b1 = wsum(a0 * Pb1);
+        if (!(Z > 1e-250) || !(Z < 1e250)) {         // outside the represented range: to the sweep
+            if (lane == 0) s_f[nf] = (int32_t)gsym;
+            ++nf;
+            if (nf == 64) flush();
+            continue;
+        }
+        const double iz = 1.0 / Z;
+        cd* out = a.mom + (size_t)gsym * MS;
+        if (lane == 0) {
+            out[0] = cmk(Sa0 * iz, Sb0 * iz);
+            out[1] = cmk(Sa1 * iz, Sb1 * iz);
+            out[2] = cmk(S00 * iz, 0.0);
+            const cd s01 = cmk((Sa0a1 + Sb0b1) * iz, (Sb0a1 - Sa0b1) * iz);   // E[x0 conj(x1)]
+            out[3] = s01;
+            out[4] = cconj(s01);
+            out[5] = cmk(S11 * iz, 0.0);
+        }
+        if (c.count && lane == 0) atomicAdd(&g_estep_pair, 1ull);
+    }
+    flush();
+}
+
 }  // namespace
 
 bool estep_pair_supported(const Problem& pb, int mode) {
-    return mode == SBCE_ESTEP_SOFT && pb.NT == 4 && pb.M == 16 && pb.NR >= 4 && pb.NR <= 8 &&
-           !g_debug.estep_nopair;
+    if (mode != SBCE_ESTEP_SOFT || g_debug.estep_nopair) return false;
+    if (pb.NT == 2) return pb.M >= 4 && pb.M <= 64 && pb.NR >= 2 && pb.NR <= 8;   // estep_fact2_kernel
+    return pb.NT == 4 && pb.M == 16 && pb.NR >= 4 && pb.NR <= 8;
 }
 
 // a.list: this pass's list (EstepArgs::list, counters 3 and 4, zeroed by the caller); the
@@ -343,6 +541,19 @@ hipError_t launch_estep_pair(const Problem& pb, const EstepArgs& a, int stride, 
     long blocks = (nsym + kPairWaves - 1) / kPairWaves;
     if (blocks > 768) blocks = 768;                  // 3 blocks per CU are resident (LDS, VGPRs)
     const dim3 grid((unsigned)blocks), blk(64 * kPairWaves);
+    if (pb.NT == 2) {
+        long fb = (nsym + 8 * kF2Waves - 1) / (8 * kF2Waves);   // >= 8 symbols per wave
+        if (fb > 2048) fb = 2048;
+        if (fb < 1) fb = 1;
+        const dim3 fgrid((unsigned)fb);
+        switch (pb.NR) {
+#define SBCE_F2(n) case n: hipLaunchKernelGGL((estep_fact2_kernel<n>), fgrid, dim3(64 * kF2Waves), 0, s, a, c, pb.M); break;
+            SBCE_F2(2) SBCE_F2(3) SBCE_F2(4) SBCE_F2(5) SBCE_F2(6) SBCE_F2(7) SBCE_F2(8)
+#undef SBCE_F2
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (pb.NR) {
         case 4: hipLaunchKernelGGL((estep_pair_kernel<4>), grid, blk, 0, s, a, c); break;
         case 5: hipLaunchKernelGGL((estep_pair_kernel<5>), grid, blk, 0, s, a, c); break;

@@ -336,45 +336,6 @@ __global__ __launch_bounds__(64 * kPmWaves) void estep_pm_kernel(EstepArgs a, Pm
 // is the unique minimiser, i.e. what the first-minimum exhaustive scan in table order returns,
 // with the same distance value.  Otherwise (a tie, NaN, or not a square grid) the exhaustive scan
 // runs.  Bitwise the wave kernel's decisions either way.
-struct GridLds {
-    double lre[8], lim[8];
-    int idx[64];
-    int K;                                          // 0: not a square grid, exhaustive scans
-};
-
-// Every thread of the block calls it (blockDim >= M).  Thread s < M places point s: its level
-// index on each axis is (#points strictly below it) / K, valid when exactly K points share its
-// level and no other point equals it -- then the K x K cells are filled one-to-one.
-__device__ void grid_build(const cd* cons, int M, GridLds* g) {
-    const int tid = threadIdx.x;
-    int K = 0;
-    while (K * K < M) ++K;
-    const bool sq = K * K == M && K <= 8;
-    bool ok = true;
-    if (sq && tid < M) {
-        const cd v = cons[tid];
-        int lt_x = 0, eq_x = 0, lt_y = 0, eq_y = 0, same = 0;
-        for (int s = 0; s < M; ++s) {
-            const cd u = cons[s];
-            lt_x += u.x < v.x;
-            eq_x += u.x == v.x;
-            lt_y += u.y < v.y;
-            eq_y += u.y == v.y;
-            same += (u.x == v.x) && (u.y == v.y);
-        }
-        ok = eq_x == K && eq_y == K && same == 1 && lt_x % K == 0 && lt_y % K == 0;
-        if (ok) {
-            const int ir = lt_x / K, ii = lt_y / K;
-            g->lre[ir] = v.x;
-            g->lim[ii] = v.y;
-            g->idx[ir * K + ii] = tid;
-        }
-    }
-    const bool all = __syncthreads_and(ok ? 1 : 0) != 0;
-    if (tid == 0) g->K = (sq && all) ? K : 0;
-    __syncthreads();
-}
-
 __device__ __forceinline__ int nearest_scan(const cd* cons, int M, cd z, double& dbest) {
     int sb = 0;
     double db = cabs2(csub(z, cons[0]));

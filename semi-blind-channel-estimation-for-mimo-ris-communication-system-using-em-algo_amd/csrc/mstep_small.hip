@@ -28,21 +28,140 @@ constexpr int kSmallMaxL = 64;
 constexpr int kSmallThreads = 256;
 constexpr int kStageCd = 2048;                // staged symbols: <= 32 KB of complex doubles
 
+// ---- MFMA build (P <= 16: every (i, j) block of R is ONE 16 x 16 complex tile) ----
+// R_ij[p][q] = sum_t a_t[p] conj(b_t[q]) with a = psi_t[p] S_t[i][j] (data) or u_t[p n_tx + i]
+// (pilots), b = psi_t[q] (data) or u_t[q n_tx + j] (pilots): four real v_mfma_f64_16x16x4f64 per
+// block and k-step of 4 symbols, lane (li, lk) feeding symbol t0 + lk at index li of both operands
+// (four consecutive psi rows per load).  B^H rides along as an (L x T) x (T x n_rx) product on row
+// tiles of 16.  The NT(NT+1)/2 blocks and NT row tiles are spread over the 4 waves; the next
+// k-step's operands are loaded before the current MFMAs.  Results to LDS (R: [L][LD], B^H: [L][NR]).
+typedef double d4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void cmfma(d4v& cre, d4v& cim, cd x, cd y) {   // C += x * y
+    cre = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, y.x, cre, 0, 0, 0);
+    cre = __builtin_amdgcn_mfma_f64_16x16x4f64(-x.y, y.y, cre, 0, 0, 0);
+    cim = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, y.y, cim, 0, 0, 0);
+    cim = __builtin_amdgcn_mfma_f64_16x16x4f64(x.y, y.x, cim, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ cd pick(const cd (&v)[N], int i) {   // v[i] without dynamic indexing
+    cd r = v[0];
+#pragma unroll
+    for (int k = 1; k < N; ++k) r = csel(i == k, v[k], r);
+    return r;
+}
+
+template <int NT, int NR>
+__device__ __forceinline__ void mfma_build(const MstepArgs& a, int b, int P, int Tp, int Td, int L,
+                                           int LD, cd* sR, cd* sY, int wave, int lane) {
+    constexpr int NBLK = NT * (NT + 1) / 2, LT = NT, NIT = NBLK + LT, IPW = (NIT + 3) / 4;
+    constexpr int MS = NT + NT * NT;
+    const int li = lane & 15, lk = lane >> 4;
+    int bi[IPW], bj[IPW], tq[IPW];                    // item: block (bi, bj) or B^H row tile tq
+    d4v cre[IPW], cim[IPW];
+#pragma unroll
+    for (int s = 0; s < IPW; ++s) {
+        const int it = wave + 4 * s;
+        bi[s] = 0; bj[s] = 0; tq[s] = -1;
+        if (it < NBLK) {
+            int i = 0;
+            while ((i + 1) * (i + 2) / 2 <= it) ++i;
+            bi[s] = i;
+            bj[s] = it - i * (i + 1) / 2;
+        } else {
+            tq[s] = it - NBLK;                       // >= LT: no item
+        }
+        cre[s] = d4v{0.0, 0.0, 0.0, 0.0};
+        cim[s] = cre[s];
+    }
+    const cd* up = a.up + (size_t)b * Tp * L;
+    const cd* yp = a.yp + (size_t)b * Tp * NR;
+    for (int t0 = 0; t0 < Tp; t0 += 4) {
+        const int t = t0 + lk;
+        const bool on = t < Tp;
+        cd u[NT];
+#pragma unroll
+        for (int i = 0; i < NT; ++i) u[i] = (on && li < P) ? up[(size_t)t * L + li * NT + i] : czero();
+        const cd yc = (on && li < NR) ? cconj(yp[(size_t)t * NR + li]) : czero();
+#pragma unroll
+        for (int s = 0; s < IPW; ++s) {
+            if (tq[s] < 0) {
+                cmfma(cre[s], cim[s], pick(u, bi[s]), cconj(pick(u, bj[s])));
+            } else if (tq[s] < LT) {
+                const int l = 16 * tq[s] + li;
+                const cd ul = (on && l < L) ? up[(size_t)t * L + l] : czero();
+                cmfma(cre[s], cim[s], ul, yc);
+            }
+        }
+    }
+    const cd* ps = a.psid + (size_t)b * Td * P;
+    const cd* mom = a.mom + (size_t)b * Td * MS;
+    const cd* yd = a.yd + (size_t)b * Td * NR;
+    cd psi_n = czero(), yc_n = czero(), sv_n[MS];
+    auto load = [&](int t0) {
+        const int t = t0 + lk;
+        const bool on = t < Td;
+        psi_n = (on && li < P) ? ps[(size_t)t * P + li] : czero();
+#pragma unroll
+        for (int e = 0; e < MS; ++e) sv_n[e] = on ? mom[(size_t)t * MS + e] : czero();
+        yc_n = (on && li < NR) ? cconj(yd[(size_t)t * NR + li]) : czero();
+    };
+    if (Td > 0) load(0);
+    for (int t0 = 0; t0 < Td; t0 += 4) {
+        const cd psi = psi_n, yc = yc_n;
+        cd sv[MS];
+#pragma unroll
+        for (int e = 0; e < MS; ++e) sv[e] = sv_n[e];
+        if (t0 + 4 < Td) load(t0 + 4);
+#pragma unroll
+        for (int s = 0; s < IPW; ++s) {
+            if (tq[s] < 0) {
+                cmfma(cre[s], cim[s], cmul(psi, pick(sv, NT + bi[s] * NT + bj[s])), cconj(psi));
+            } else if (tq[s] < LT) {
+                const int l = 16 * tq[s] + li;
+                const int pl = l / NT, al = l - pl * NT;
+                // psi_t[l / NT] from the lane of this symbol's group that holds it
+                const cd pv = cmk(__shfl(psi.x, (lane & 48) | (pl & 15)), __shfl(psi.y, (lane & 48) | (pl & 15)));
+                cmfma(cre[s], cim[s], l < L ? cmul(pv, pick(sv, al)) : czero(), yc);
+            }
+        }
+    }
+    // lane holds column li, rows lk + 4v of each of its tiles
+#pragma unroll
+    for (int s = 0; s < IPW; ++s) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int p = lk + 4 * v;
+            const cd c = cmk(cre[s][v], cim[s][v]);
+            if (tq[s] < 0) {
+                if (p < P && li < P) {
+                    sR[(p * NT + bi[s]) * LD + li * NT + bj[s]] = c;
+                    if (bi[s] != bj[s]) sR[(li * NT + bj[s]) * LD + p * NT + bi[s]] = cconj(c);
+                }
+            } else if (tq[s] < LT) {
+                const int l = 16 * tq[s] + p;
+                if (l < L && li < NR) sY[l * NR + li] = c;
+            }
+        }
+    }
+}
+
 // Thread (ti, tj) = (tid / 16, tid % 16) owns the R elements (ti + 16 k1, tj + 16 k2), k1, k2 <
 // KB = ceil(L / 16), in registers from the build to the end of the solve; B^H / y entry
 // e = tid + 256 k (row e / NR, column e % NR) likewise.  Only column c (forward) or row c (back
 // substitution) of L and y_c / x_c cross threads, through a double-buffered LDS vector: one
 // barrier per column.
-template <int NR, int KB>
+template <int NR, int KB, int MNT>
 __global__ __launch_bounds__(kSmallThreads) void mstep_small_kernel(MstepArgs a, int NT, int P,
                                                                     int Tp, int Td, int L,
-                                                                    int write_sys, int stop) {
+                                                                    int write_sys, int stop, int sg) {
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
     constexpr int YK = (64 * NR + kSmallThreads - 1) / kSmallThreads;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    cd* stg = reinterpret_cast<cd*>(smem);           // [kStageCd] staged symbols
-    cd* xb = stg + kStageCd;                         // [2][64 + 8] column / row + y_c exchange
+    cd* stg = reinterpret_cast<cd*>(smem);           // [sg] staged symbols / the MFMA build's R, B^H
+    cd* xb = stg + sg;                               // [2][64 + 8] column / row + y_c exchange
     double* dinv = reinterpret_cast<double*>(xb + 2 * (64 + 8));   // [64] 1 / l_cc (0: dropped)
     double* red = dinv + 64;                                      // [4]
     const int tid = threadIdx.x, ti = tid >> 4, tj = tid & 15;
@@ -82,71 +201,85 @@ __global__ __launch_bounds__(kSmallThreads) void mstep_small_kernel(MstepArgs a,
         Y[k] = czero();
     }
 
-    // pilots, TPC symbols at a time: u_p [TPC][L], y_p [TPC][NR]
-    {
-        const int TPC = kStageCd / (L + NR) > 0 ? kStageCd / (L + NR) : 1;
-        const cd* up = a.up + (size_t)b * Tp * L;
-        const cd* yp = a.yp + (size_t)b * Tp * NR;
-        cd* su = stg;
-        cd* sp = stg + TPC * L;
-        for (int t0 = 0; t0 < Tp; t0 += TPC) {
-            const int tc = (Tp - t0) < TPC ? (Tp - t0) : TPC;
-            __syncthreads();
-            for (int e = tid; e < tc * L; e += kSmallThreads) su[e] = up[(size_t)t0 * L + e];
-            for (int e = tid; e < tc * NR; e += kSmallThreads) sp[e] = yp[(size_t)t0 * NR + e];
-            __syncthreads();
-            for (int tt = 0; tt < (stop == 3 ? 0 : tc); ++tt) {
+    if constexpr (MNT > 0) {
+        const int LD = L + 1;
+        mfma_build<MNT, NR>(a, b, P, Tp, Td, L, LD, stg, stg + L * LD, wave, lane);
+        __syncthreads();
 #pragma unroll
-                for (int k1 = 0; k1 < KB; ++k1)
+        for (int k1 = 0; k1 < KB; ++k1)
 #pragma unroll
-                    for (int k2 = 0; k2 < KB; ++k2)
-                        if (need[k1][k2])
-                            A[k1][k2] = cfmac(A[k1][k2], su[tt * L + rr[k1][k2]], su[tt * L + cc[k1][k2]]);
+            for (int k2 = 0; k2 < KB; ++k2)
+                if (need[k1][k2]) A[k1][k2] = stg[(ti + 16 * k1) * LD + tj + 16 * k2];
 #pragma unroll
-                for (int k = 0; k < YK; ++k)
-                    if (yl[k] < L) Y[k] = cfmac(Y[k], su[tt * L + yl[k]], sp[tt * NR + yrr[k]]);
+        for (int k = 0; k < YK; ++k)
+            if (yl[k] < L) Y[k] = stg[L * LD + tid + kSmallThreads * k];
+    } else {
+        // pilots, TPC symbols at a time: u_p [TPC][L], y_p [TPC][NR]
+        {
+            const int TPC = sg / (L + NR) > 0 ? sg / (L + NR) : 1;
+            const cd* up = a.up + (size_t)b * Tp * L;
+            const cd* yp = a.yp + (size_t)b * Tp * NR;
+            cd* su = stg;
+            cd* sp = stg + TPC * L;
+            for (int t0 = 0; t0 < Tp; t0 += TPC) {
+                const int tc = (Tp - t0) < TPC ? (Tp - t0) : TPC;
+                __syncthreads();
+                for (int e = tid; e < tc * L; e += kSmallThreads) su[e] = up[(size_t)t0 * L + e];
+                for (int e = tid; e < tc * NR; e += kSmallThreads) sp[e] = yp[(size_t)t0 * NR + e];
+                __syncthreads();
+                for (int tt = 0; tt < (stop == 3 ? 0 : tc); ++tt) {
+    #pragma unroll
+                    for (int k1 = 0; k1 < KB; ++k1)
+    #pragma unroll
+                        for (int k2 = 0; k2 < KB; ++k2)
+                            if (need[k1][k2])
+                                A[k1][k2] = cfmac(A[k1][k2], su[tt * L + rr[k1][k2]], su[tt * L + cc[k1][k2]]);
+    #pragma unroll
+                    for (int k = 0; k < YK; ++k)
+                        if (yl[k] < L) Y[k] = cfmac(Y[k], su[tt * L + yl[k]], sp[tt * NR + yrr[k]]);
+                }
             }
         }
-    }
-    // data symbols, TC at a time: psi [TC][P], moments [TC][MS], y_d [TC][NR]
-    {
-        const int TC = kStageCd / (P + MS + NR) > 0 ? kStageCd / (P + MS + NR) : 1;
-        const cd* ps = a.psid + (size_t)b * Td * P;
-        const cd* mom = a.mom + (size_t)b * Td * MS;
-        const cd* yd = a.yd + (size_t)b * Td * NR;
-        cd* s_ps = stg;
-        cd* s_m = s_ps + TC * P;
-        cd* s_y = s_m + TC * MS;
-        for (int t0 = 0; t0 < Td; t0 += TC) {
-            const int tc = (Td - t0) < TC ? (Td - t0) : TC;
-            __syncthreads();
-            for (int e = tid; e < tc * P; e += kSmallThreads) s_ps[e] = ps[(size_t)t0 * P + e];
-            for (int e = tid; e < tc * MS; e += kSmallThreads) s_m[e] = mom[(size_t)t0 * MS + e];
-            for (int e = tid; e < tc * NR; e += kSmallThreads) s_y[e] = yd[(size_t)t0 * NR + e];
-            __syncthreads();
-            for (int tt = 0; tt < (stop == 3 ? 0 : tc); ++tt) {
-#pragma unroll
-                for (int k1 = 0; k1 < KB; ++k1)
-#pragma unroll
-                    for (int k2 = 0; k2 < KB; ++k2)
-                        if (need[k1][k2]) {
-                            const cd w = cmulc(s_ps[tt * P + prr[k1][k2]], s_ps[tt * P + pcc[k1][k2]]);
-                            A[k1][k2] = cfma(A[k1][k2], w, s_m[tt * MS + sidx[k1][k2]]);
+        // data symbols, TC at a time: psi [TC][P], moments [TC][MS], y_d [TC][NR]
+        {
+            const int TC = sg / (P + MS + NR) > 0 ? sg / (P + MS + NR) : 1;
+            const cd* ps = a.psid + (size_t)b * Td * P;
+            const cd* mom = a.mom + (size_t)b * Td * MS;
+            const cd* yd = a.yd + (size_t)b * Td * NR;
+            cd* s_ps = stg;
+            cd* s_m = s_ps + TC * P;
+            cd* s_y = s_m + TC * MS;
+            for (int t0 = 0; t0 < Td; t0 += TC) {
+                const int tc = (Td - t0) < TC ? (Td - t0) : TC;
+                __syncthreads();
+                for (int e = tid; e < tc * P; e += kSmallThreads) s_ps[e] = ps[(size_t)t0 * P + e];
+                for (int e = tid; e < tc * MS; e += kSmallThreads) s_m[e] = mom[(size_t)t0 * MS + e];
+                for (int e = tid; e < tc * NR; e += kSmallThreads) s_y[e] = yd[(size_t)t0 * NR + e];
+                __syncthreads();
+                for (int tt = 0; tt < (stop == 3 ? 0 : tc); ++tt) {
+    #pragma unroll
+                    for (int k1 = 0; k1 < KB; ++k1)
+    #pragma unroll
+                        for (int k2 = 0; k2 < KB; ++k2)
+                            if (need[k1][k2]) {
+                                const cd w = cmulc(s_ps[tt * P + prr[k1][k2]], s_ps[tt * P + pcc[k1][k2]]);
+                                A[k1][k2] = cfma(A[k1][k2], w, s_m[tt * MS + sidx[k1][k2]]);
+                            }
+    #pragma unroll
+                    for (int k = 0; k < YK; ++k)
+                        if (yl[k] < L) {
+                            const cd w = cmul(s_ps[tt * P + ypl[k]], s_m[tt * MS + yal[k]]);
+                            Y[k] = cfmac(Y[k], w, s_y[tt * NR + yrr[k]]);
                         }
-#pragma unroll
-                for (int k = 0; k < YK; ++k)
-                    if (yl[k] < L) {
-                        const cd w = cmul(s_ps[tt * P + ypl[k]], s_m[tt * MS + yal[k]]);
-                        Y[k] = cfmac(Y[k], w, s_y[tt * NR + yrr[k]]);
-                    }
+                }
             }
         }
+    #pragma unroll
+        for (int k1 = 0; k1 < KB; ++k1)
+    #pragma unroll
+            for (int k2 = 0; k2 < KB; ++k2)
+                if (swp[k1][k2]) A[k1][k2] = cconj(A[k1][k2]);
     }
-#pragma unroll
-    for (int k1 = 0; k1 < KB; ++k1)
-#pragma unroll
-        for (int k2 = 0; k2 < KB; ++k2)
-            if (swp[k1][k2]) A[k1][k2] = cconj(A[k1][k2]);
     if (write_sys) {                                 // sbce_mstep's r_out / rhs_out
         cd* R = a.R + (size_t)b * L * L;
 #pragma unroll
@@ -266,11 +399,11 @@ __global__ __launch_bounds__(kSmallThreads) void mstep_small_kernel(MstepArgs a,
     if (tid == 0 && a.status && anybad) a.status[b] |= a.clamp_status;
 }
 
-template <int KB>
-hipError_t launch_nr(const Problem& pb, const MstepArgs& a, size_t lds, int write_sys,
+template <int KB, int MNT>
+hipError_t launch_nr(const Problem& pb, const MstepArgs& a, size_t lds, int write_sys, int sg,
                      hipStream_t s) {
     switch (pb.NR) {
-#define SBCE_MS(n) case n: hipLaunchKernelGGL((mstep_small_kernel<n, KB>), dim3(pb.B), dim3(kSmallThreads), lds, s, a, pb.NT, pb.P, pb.Tp, pb.Td, pb.L, write_sys, g_debug.small_stop); break;
+#define SBCE_MS(n) case n: hipLaunchKernelGGL((mstep_small_kernel<n, KB, MNT>), dim3(pb.B), dim3(kSmallThreads), lds, s, a, pb.NT, pb.P, pb.Tp, pb.Td, pb.L, write_sys, g_debug.small_stop, sg); break;
         SBCE_MS(1) SBCE_MS(2) SBCE_MS(3) SBCE_MS(4) SBCE_MS(5) SBCE_MS(6) SBCE_MS(7) SBCE_MS(8)
 #undef SBCE_MS
         default: return hipErrorInvalidValue;
@@ -288,13 +421,29 @@ bool mstep_small_supported(const Problem& pb, int solve_mode) {
 }
 
 hipError_t launch_mstep_small(const Problem& pb, const MstepArgs& a, bool write_sys, hipStream_t s) {
-    const size_t lds = (kStageCd + 2 * (64 + 8)) * sizeof(cd) + (64 + 4) * sizeof(double);
     const int w = write_sys ? 1 : 0;
-    switch ((pb.L + 15) / 16) {
-        case 1: return launch_nr<1>(pb, a, lds, w, s);
-        case 2: return launch_nr<2>(pb, a, lds, w, s);
-        case 3: return launch_nr<3>(pb, a, lds, w, s);
-        case 4: return launch_nr<4>(pb, a, lds, w, s);
+    const int KB = (pb.L + 15) / 16;
+    // P <= 16 (BASELINE cfg 5): the MFMA build, R and B^H through LDS; else the VALU build
+    const bool mf = pb.P <= 16 && pb.NT <= 3 && !g_debug.small_valu && g_debug.small_stop == 0;
+    int sg = kStageCd;
+    if (mf && pb.L * (pb.L + 1) + pb.L * pb.NR > sg) sg = pb.L * (pb.L + 1) + pb.L * pb.NR;
+    const size_t lds = ((size_t)sg + 2 * (64 + 8)) * sizeof(cd) + (64 + 4) * sizeof(double);
+    if (mf) {
+        switch (pb.NT * 8 + KB) {
+            case 1 * 8 + 1: return launch_nr<1, 1>(pb, a, lds, w, sg, s);
+            case 2 * 8 + 1: return launch_nr<1, 2>(pb, a, lds, w, sg, s);
+            case 2 * 8 + 2: return launch_nr<2, 2>(pb, a, lds, w, sg, s);
+            case 3 * 8 + 1: return launch_nr<1, 3>(pb, a, lds, w, sg, s);
+            case 3 * 8 + 2: return launch_nr<2, 3>(pb, a, lds, w, sg, s);
+            case 3 * 8 + 3: return launch_nr<3, 3>(pb, a, lds, w, sg, s);
+        }
+        return hipErrorInvalidValue;
+    }
+    switch (KB) {
+        case 1: return launch_nr<1, 0>(pb, a, lds, w, sg, s);
+        case 2: return launch_nr<2, 0>(pb, a, lds, w, sg, s);
+        case 3: return launch_nr<3, 0>(pb, a, lds, w, sg, s);
+        case 4: return launch_nr<4, 0>(pb, a, lds, w, sg, s);
     }
     return hipErrorInvalidValue;
 }

@@ -176,6 +176,7 @@ struct DebugConfig {
     bool cplx3;          // SBCE_CPLX3=0           four real MFMAs per complex product (default: three, Gauss)
     bool mstep_nosmall;  // SBCE_MSTEP_SMALL=0     L <= 64: the batched build + panel Cholesky instead of
                          //                        the one-workgroup M-step (mstep_small.hip)
+    bool small_valu;     // SBCE_MSTEP_SMALL=v     the 256-thread VALU-build kernel also at P <= 16
     int small_stop;      // SBCE_SMALL_STOP=1|2|3  DIAGNOSTIC: the one-workgroup M-step stops after its
                          //                        build (1) / factorisation (2) / symbol staging
                          //                        without the build's arithmetic (3); results invalid
@@ -231,6 +232,48 @@ __device__ __forceinline__ TrialNoise trial_noise(double v) {
     n.s2 = v * v;
     return n;
 }
+// A square M-QAM table as a K x K grid of real / imaginary levels (any table order), built once per
+// block by grid_build (estep_pm.hip's nearest-point search, estep_pair.hip's NT = 2 factorised
+// pass); K = 0: the table is not such a grid.
+struct GridLds {
+    double lre[8], lim[8];
+    int idx[64];
+    int K;                                          // 0: not a square grid, exhaustive scans
+};
+
+// Every thread of the block calls it (blockDim >= M).  Thread s < M places point s: its level
+// index on each axis is (#points strictly below it) / K, valid when exactly K points share its
+// level and no other point equals it -- then the K x K cells are filled one-to-one.
+__device__ inline void grid_build(const cd* cons, int M, GridLds* g) {
+    const int tid = threadIdx.x;
+    int K = 0;
+    while (K * K < M) ++K;
+    const bool sq = K * K == M && K <= 8;
+    bool ok = true;
+    if (sq && tid < M) {
+        const cd v = cons[tid];
+        int lt_x = 0, eq_x = 0, lt_y = 0, eq_y = 0, same = 0;
+        for (int s = 0; s < M; ++s) {
+            const cd u = cons[s];
+            lt_x += u.x < v.x;
+            eq_x += u.x == v.x;
+            lt_y += u.y < v.y;
+            eq_y += u.y == v.y;
+            same += (u.x == v.x) && (u.y == v.y);
+        }
+        ok = eq_x == K && eq_y == K && same == 1 && lt_x % K == 0 && lt_y % K == 0;
+        if (ok) {
+            const int ir = lt_x / K, ii = lt_y / K;
+            g->lre[ir] = v.x;
+            g->lim[ii] = v.y;
+            g->idx[ir * K + ii] = tid;
+        }
+    }
+    const bool all = __syncthreads_and(ok ? 1 : 0) != 0;
+    if (tid == 0) g->K = (sq && all) ? K : 0;
+    __syncthreads();
+}
+
 constexpr int kTreeRecDoubles = 32;   // (word 31: the factorised-weight pass's screen)
 constexpr int kEstepListCnt = 16;      // int32 counters after the sweep's list
 // the factorised-weight pass (estep_pair.hip) takes a symbol whose range D is at most this

@@ -83,3 +83,40 @@ def test_pair_estep_full_em_low_snr_vs_oracle(sbce):
     th0 = em_reduced(b["y_d"][0], b["y_p"][0], b["u_p"][0], b["psi_d"][0].T, aps, varn, 2,
                      b["theta0"][0])
     assert rel(r["theta"][0], th0) < 1e-10
+
+
+def _run_nt(sbce, b, th, varn, pair, n_tx):
+    lib = sbce._lib.load()
+    with sbce._lib.debug_env(SBCE_ESTEP_PAIR=pair, SBCE_ESTEP_COUNT="1"):
+        lib.sbce_debug_estep_pair(None, 1)
+        m, S = sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], th, varn, n_tx)
+        npair = ctypes.c_ulonglong(0)
+        lib.sbce_debug_estep_pair(ctypes.byref(npair), 0)
+    return m, S, npair.value
+
+
+@pytest.mark.parametrize("n_rx,M,snr", [(2, 64, -5), (2, 64, 5), (2, 64, 15), (2, 64, 30),
+                                        (3, 16, 0), (2, 4, -5), (4, 64, 10), (8, 16, 20)])
+def test_fact2_estep_nt2_matches_sweep_and_oracle(sbce, n_rx, M, snr):
+    """n_tx = 2 (BASELINE cfg 5: 2 x 2, N_RIS = 15, 64-QAM): the tree pass routes every symbol it
+    does not resolve alone and whose factor range D is representable to the factorised pass
+    (estep_fact2_kernel, four 1-D and four K x K log tables, the (a1, b1) sum split into an a1 and
+    a b1 sum); its moments equal the enumeration / sweep path's (SBCE_ESTEP_PAIR=0) and the
+    oracle's enumeration of all M^2 hypotheses to 1e-11 max|c|^2."""
+    power = {4: 2.0, 16: 10.0, 64: 42.0}[M]          # the square QAM's mean symbol energy
+    varn = float(sbce.signal_model.snr_to_varn(snr, power))
+    b = sbce.signal_model.synthetic_batch(3, 2, n_rx, 15, 20, 60, M, varn, seed=60 + snr + n_rx,
+                                          pinv="scipy")
+    scale = np.abs(b["cons"]).max() ** 2
+    aps = sbce.qam.all_possible_symbols(b["cons"], 2)
+    for th in (b["theta0"], b["h"] + 0.05 * b["theta0"] / np.abs(b["theta0"]).max()):
+        m1, S1, npair = _run_nt(sbce, b, th, varn, "1", 2)
+        m0, S0, npair0 = _run_nt(sbce, b, th, varn, "0", 2)
+        assert npair0 == 0
+        if snr <= 5 and M >= 16:                   # (4-QAM, J = 16: the VALU E-step, no sphere pass)
+            assert npair > 0
+        assert np.abs(m1 - m0).max() < 1e-11 * scale, (snr, np.abs(m1 - m0).max())
+        assert np.abs(S1 - S0).max() < 1e-11 * scale, (snr, np.abs(S1 - S0).max())
+        mo, So, _, _ = estep_moments(th[0], b["y_d"][0], b["psi_d"][0].T, aps, varn)
+        assert np.abs(m1[0] - mo).max() < 1e-11 * scale
+        assert np.abs(S1[0] - So).max() < 1e-11 * scale

@@ -30,7 +30,8 @@ def timed(fn, reps=10):
 
 def main():
     td = int(sys.argv[1]) if len(sys.argv) > 1 else 120
-    arms = [("default", {})] + [(a, dict(kv.split("=") for kv in a.split(","))) for a in sys.argv[2:]]
+    arms = [("default", {})] + [(a, dict(kv.split("=") for kv in a.split(","))) for a in sys.argv[2:]
+                                if a != "count"]
     snr = np.arange(-5, 35, 2.0)
     varn = pkg.signal_model.snr_to_varn(snr, 42.0)
     pts = [pkg.signal_model.synthetic_batch(64, 2, 2, 15, 20, td, 64, float(v), seed=7 + j,
@@ -38,6 +39,9 @@ def main():
     batch = {k: np.concatenate([p[k] for p in pts]) for k in ("y_d", "y_p", "psi_d", "u_p", "theta0", "h")}
     batch["cons"] = pts[0]["cons"]
     vt = np.repeat(varn, 64)
+    count = "count" in sys.argv
+    if count:
+        arms = [(n, e) for n, e in arms if n != "count"]
     for name, env in arms:
         with pkg._lib.debug_env(**env):
             out = []
@@ -47,6 +51,27 @@ def main():
                 out.append(f"{det} {timed(eng.estep):7.1f}")
             out.append(f"mstep {timed(eng.mstep):7.1f}")
             print(f"{name:24s} T_d={td} B={eng.B} us: " + "  ".join(out), flush=True)
+    if count:                      # where the exact soft E-step's symbols were resolved, per SNR
+        import ctypes
+        lib = pkg._lib.load()
+        eng = pkg.EMEngine(batch, vt, mode="soft")
+        eng.run(1)
+        sph = (ctypes.c_ulonglong * 3)()
+        npair, nmf = ctypes.c_ulonglong(0), ctypes.c_ulonglong(0)
+        with pkg._lib.debug_env(SBCE_ESTEP_COUNT="1"):
+            lib.sbce_debug_estep_sphere(None, 1)
+            lib.sbce_debug_estep_pair(None, 1)
+            lib.sbce_debug_estep_mfma(None, 1)
+            eng.estep()
+            torch.cuda.synchronize()
+            lib.sbce_debug_estep_sphere(sph, 0)
+            lib.sbce_debug_estep_pair(ctypes.byref(npair), 0)
+            lib.sbce_debug_estep_mfma(ctypes.byref(nmf), 0)
+        nsym = float(eng.B * td)
+        print(f"soft E-step symbols: single path {sph[2] / nsym:.3f}, enumerated {sph[0] / nsym:.3f}, "
+              f"factorised {npair.value / nsym:.3f}, swept {(sph[1] - npair.value) / nsym:.3f}; "
+              f"sweep MFMAs {nmf.value} ({nmf.value / max(sph[1] - npair.value, 1):.0f} per swept symbol)",
+              flush=True)
 
 
 if __name__ == "__main__":
