@@ -32,9 +32,9 @@ constexpr int kStageCd = 2048;                // staged symbols: <= 32 KB of com
 // R_ij[p][q] = sum_t a_t[p] conj(b_t[q]) with a = psi_t[p] S_t[i][j] (data) or u_t[p n_tx + i]
 // (pilots), b = psi_t[q] (data) or u_t[q n_tx + j] (pilots): four real v_mfma_f64_16x16x4f64 per
 // block and k-step of 4 symbols, lane (li, lk) feeding symbol t0 + lk at index li of both operands
-// (four consecutive psi rows per load).  B^H rides along as an (L x T) x (T x n_rx) product on row
-// tiles of 16.  The NT(NT+1)/2 blocks and NT row tiles are spread over the 4 waves; the next
-// k-step's operands are loaded before the current MFMAs.  Results to LDS (R: [L][LD], B^H: [L][NR]).
+// (the symbols staged in LDS by chunks, all loads of a chunk in flight at once).  B^H rides along
+// as an (L x T) x (T x n_rx) product on row tiles of 16.  The NT(NT+1)/2 blocks and NT row tiles
+// are spread over the 4 waves.  Results to LDS (R: [L][LD], B^H: [L][NR]) over the staging area.
 typedef double d4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void cmfma(d4v& cre, d4v& cim, cd x, cd y) {   // C += x * y
@@ -54,10 +54,10 @@ __device__ __forceinline__ cd pick(const cd (&v)[N], int i) {   // v[i] without 
 
 template <int NT, int NR>
 __device__ __forceinline__ void mfma_build(const MstepArgs& a, int b, int P, int Tp, int Td, int L,
-                                           int LD, cd* sR, cd* sY, int wave, int lane) {
+                                           int LD, cd* stg, int sg, int tid) {
     constexpr int NBLK = NT * (NT + 1) / 2, LT = NT, NIT = NBLK + LT, IPW = (NIT + 3) / 4;
     constexpr int MS = NT + NT * NT;
-    const int li = lane & 15, lk = lane >> 4;
+    const int lane = tid & 63, wave = tid >> 6, li = lane & 15, lk = lane >> 4;
     int bi[IPW], bj[IPW], tq[IPW];                    // item: block (bi, bj) or B^H row tile tq
     d4v cre[IPW], cim[IPW];
 #pragma unroll
@@ -75,58 +75,81 @@ __device__ __forceinline__ void mfma_build(const MstepArgs& a, int b, int P, int
         cre[s] = d4v{0.0, 0.0, 0.0, 0.0};
         cim[s] = cre[s];
     }
-    const cd* up = a.up + (size_t)b * Tp * L;
-    const cd* yp = a.yp + (size_t)b * Tp * NR;
-    for (int t0 = 0; t0 < Tp; t0 += 4) {
-        const int t = t0 + lk;
-        const bool on = t < Tp;
-        cd u[NT];
+    // pilots, TPC symbols (a multiple of 4) per LDS chunk: u_p [TPC][L], y_p [TPC][NR]
+    {
+        int TPC = (sg / (L + NR)) & ~3;
+        if (TPC < 4) TPC = 4;
+        const cd* up = a.up + (size_t)b * Tp * L;
+        const cd* yp = a.yp + (size_t)b * Tp * NR;
+        cd* su = stg;
+        cd* sp = stg + TPC * L;
+        for (int c0 = 0; c0 < Tp; c0 += TPC) {
+            const int tc = (Tp - c0) < TPC ? (Tp - c0) : TPC;
+            __syncthreads();
+            for (int e = tid; e < tc * L; e += kSmallThreads) su[e] = up[(size_t)c0 * L + e];
+            for (int e = tid; e < tc * NR; e += kSmallThreads) sp[e] = yp[(size_t)c0 * NR + e];
+            __syncthreads();
+            for (int t0 = 0; t0 < tc; t0 += 4) {
+                const int t = t0 + lk;
+                const bool on = t < tc;
+                cd u[NT];
 #pragma unroll
-        for (int i = 0; i < NT; ++i) u[i] = (on && li < P) ? up[(size_t)t * L + li * NT + i] : czero();
-        const cd yc = (on && li < NR) ? cconj(yp[(size_t)t * NR + li]) : czero();
+                for (int i = 0; i < NT; ++i) u[i] = (on && li < P) ? su[t * L + li * NT + i] : czero();
+                const cd yc = (on && li < NR) ? cconj(sp[t * NR + li]) : czero();
 #pragma unroll
-        for (int s = 0; s < IPW; ++s) {
-            if (tq[s] < 0) {
-                cmfma(cre[s], cim[s], pick(u, bi[s]), cconj(pick(u, bj[s])));
-            } else if (tq[s] < LT) {
-                const int l = 16 * tq[s] + li;
-                const cd ul = (on && l < L) ? up[(size_t)t * L + l] : czero();
-                cmfma(cre[s], cim[s], ul, yc);
+                for (int s = 0; s < IPW; ++s) {
+                    if (tq[s] < 0) {
+                        cmfma(cre[s], cim[s], pick(u, bi[s]), cconj(pick(u, bj[s])));
+                    } else if (tq[s] < LT) {
+                        const int l = 16 * tq[s] + li;
+                        cmfma(cre[s], cim[s], (on && l < L) ? su[t * L + l] : czero(), yc);
+                    }
+                }
             }
         }
     }
-    const cd* ps = a.psid + (size_t)b * Td * P;
-    const cd* mom = a.mom + (size_t)b * Td * MS;
-    const cd* yd = a.yd + (size_t)b * Td * NR;
-    cd psi_n = czero(), yc_n = czero(), sv_n[MS];
-    auto load = [&](int t0) {
-        const int t = t0 + lk;
-        const bool on = t < Td;
-        psi_n = (on && li < P) ? ps[(size_t)t * P + li] : czero();
+    // data symbols, TC (a multiple of 4) per LDS chunk: psi [TC][P], moments [TC][MS], y_d [TC][NR]
+    {
+        int TC = (sg / (P + MS + NR)) & ~3;
+        if (TC < 4) TC = 4;
+        const cd* ps = a.psid + (size_t)b * Td * P;
+        const cd* mom = a.mom + (size_t)b * Td * MS;
+        const cd* yd = a.yd + (size_t)b * Td * NR;
+        cd* s_ps = stg;
+        cd* s_m = s_ps + TC * P;
+        cd* s_y = s_m + TC * MS;
+        for (int c0 = 0; c0 < Td; c0 += TC) {
+            const int tc = (Td - c0) < TC ? (Td - c0) : TC;
+            __syncthreads();
+            for (int e = tid; e < tc * P; e += kSmallThreads) s_ps[e] = ps[(size_t)c0 * P + e];
+            for (int e = tid; e < tc * MS; e += kSmallThreads) s_m[e] = mom[(size_t)c0 * MS + e];
+            for (int e = tid; e < tc * NR; e += kSmallThreads) s_y[e] = yd[(size_t)c0 * NR + e];
+            __syncthreads();
+            for (int t0 = 0; t0 < tc; t0 += 4) {
+                const int t = t0 + lk;
+                const bool on = t < tc;
+                const cd psi = (on && li < P) ? s_ps[t * P + li] : czero();
+                const cd yc = (on && li < NR) ? cconj(s_y[t * NR + li]) : czero();
+                cd sv[MS];
 #pragma unroll
-        for (int e = 0; e < MS; ++e) sv_n[e] = on ? mom[(size_t)t * MS + e] : czero();
-        yc_n = (on && li < NR) ? cconj(yd[(size_t)t * NR + li]) : czero();
-    };
-    if (Td > 0) load(0);
-    for (int t0 = 0; t0 < Td; t0 += 4) {
-        const cd psi = psi_n, yc = yc_n;
-        cd sv[MS];
+                for (int e = 0; e < MS; ++e) sv[e] = on ? s_m[t * MS + e] : czero();
 #pragma unroll
-        for (int e = 0; e < MS; ++e) sv[e] = sv_n[e];
-        if (t0 + 4 < Td) load(t0 + 4);
-#pragma unroll
-        for (int s = 0; s < IPW; ++s) {
-            if (tq[s] < 0) {
-                cmfma(cre[s], cim[s], cmul(psi, pick(sv, NT + bi[s] * NT + bj[s])), cconj(psi));
-            } else if (tq[s] < LT) {
-                const int l = 16 * tq[s] + li;
-                const int pl = l / NT, al = l - pl * NT;
-                // psi_t[l / NT] from the lane of this symbol's group that holds it
-                const cd pv = cmk(__shfl(psi.x, (lane & 48) | (pl & 15)), __shfl(psi.y, (lane & 48) | (pl & 15)));
-                cmfma(cre[s], cim[s], l < L ? cmul(pv, pick(sv, al)) : czero(), yc);
+                for (int s = 0; s < IPW; ++s) {
+                    if (tq[s] < 0) {
+                        cmfma(cre[s], cim[s], cmul(psi, pick(sv, NT + bi[s] * NT + bj[s])), cconj(psi));
+                    } else if (tq[s] < LT) {
+                        const int l = 16 * tq[s] + li;
+                        const int pl = l / NT, al = l - pl * NT;
+                        const cd pv = (on && l < L) ? s_ps[t * P + pl] : czero();
+                        cmfma(cre[s], cim[s], cmul(pv, pick(sv, al)), yc);
+                    }
+                }
             }
         }
     }
+    __syncthreads();                                 // every wave is done with the staged symbols
+    cd* sR = stg;
+    cd* sY = stg + L * LD;
     // lane holds column li, rows lk + 4v of each of its tiles
 #pragma unroll
     for (int s = 0; s < IPW; ++s) {
@@ -203,7 +226,7 @@ __global__ __launch_bounds__(kSmallThreads) void mstep_small_kernel(MstepArgs a,
 
     if constexpr (MNT > 0) {
         const int LD = L + 1;
-        mfma_build<MNT, NR>(a, b, P, Tp, Td, L, LD, stg, stg + L * LD, wave, lane);
+        mfma_build<MNT, NR>(a, b, P, Tp, Td, L, LD, stg, sg, tid);
         __syncthreads();
 #pragma unroll
         for (int k1 = 0; k1 < KB; ++k1)
