@@ -1878,7 +1878,8 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
         out[0] = d0;
         out[1] = sc;
         screen = pair_screen<NT, NR>(H, y, xidx, cons, gsum);
-        if constexpr (NT == 2) f2d = c.pair ? fact2_bound<NR>(H, y, xidx, cons, c.M, c.inv_s2) : INFINITY;
+        if constexpr (NT == 2)          // hard: every unresolved symbol (no exponentials, no range)
+            f2d = c.pair ? (c.hard ? 0.0 : fact2_bound<NR>(H, y, xidx, cons, c.M, c.inv_s2)) : INFINITY;
         // computed here, while H and y are live anyway (left to the compiler, the computation
         // sinks to the record store at the end and keeps H_eff live across the whole kernel)
         asm volatile("" : "+v"(screen), "+v"(gsum), "+v"(f2d));
@@ -2547,7 +2548,7 @@ hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStre
                 // wide posteriors of the cfg-1 geometry: the factorised-weight pass resolves the
                 // symbols the enumeration routed to it and lists the ones it cannot represent
                 // for the tile bounds and the sweep
-                if (e == hipSuccess && pc.pair) e = launch_estep_pair(pb, as, mc.prep_stride, mc.count, s);
+                if (e == hipSuccess && pc.pair) e = launch_estep_pair(pb, as, mc.prep_stride, mc.count, mode, s);
                 if (e == hipSuccess) {
                     switch (pb.NT * 16 + pb.NR) {
 #define SBCE_BND(nt, nr) case nt * 16 + nr: \

@@ -520,17 +520,140 @@ __global__ __launch_bounds__(64 * kF2Waves) void estep_fact2_kernel(EstepArgs a,
     flush();
 }
 
+
+// ---------------------------------------------------------------- n_tx = 2, hard decision
+// The log-max E-step (argmin over the M^2 hypotheses of ||y - h_0 x_0 - h_1 x_1||^2, first table
+// index on ties: ML_detecctor.py:65-75) for n_tx = 2 on a square M-QAM grid: lane = x_0 (its table
+// index), r = y - h_0 x_0, and the best x_1 for that x_0 minimises g_11 |x_1 - z|^2 + const,
+// z = h_1^H r / g_11 -- separable per axis.  The per-axis best and second-best levels give the
+// candidate and its two rivals; their distances are computed the direct way, and the candidate is
+// taken when both rivals are farther by more than the distances' rounding (else the lane scans all
+// M points).  Then the wave's first minimum in table order (x_0 slow, x_1 fast).  The tree pass
+// routes every symbol it does not resolve alone here (no range limit: no exponentials).
+template <int NR>
+__global__ __launch_bounds__(64 * kF2Waves) void estep_hard2_kernel(EstepArgs a, PairConst c, int M) {
+    constexpr int MS = 6;
+    __shared__ cd s_cons[64];
+    __shared__ GridLds s_grid;
+    if ((int)threadIdx.x < M) s_cons[threadIdx.x] = a.cons[threadIdx.x];
+    __syncthreads();
+    grid_build(s_cons, M, &s_grid);
+    const int K = s_grid.K;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const long nsym = (long)c.B * c.Td;
+    const int32_t* cnt = a.list + nsym;
+    const int32_t* plist = a.list + 2 * nsym + 2 * kEstepListCnt;
+    const int nwork = __builtin_amdgcn_readfirstlane(cnt[3]);
+    const int nwaves = gridDim.x * kF2Waves;
+    double lre[8], lim[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        lre[k] = k < K ? s_grid.lre[k] : INFINITY;
+        lim[k] = k < K ? s_grid.lim[k] : INFINITY;
+    }
+    for (int gi = blockIdx.x * kF2Waves + wave; gi < nwork; gi += nwaves) {
+        const long gsym = plist[gi];
+        const int b = (int)(gsym / c.Td);
+        if (a.done && a.done[b]) continue;
+        const double* rec = a.prep + (size_t)gsym * c.stride;
+        cd h0[NR], h1[NR], r[NR];
+        double g11 = 0.0, scale = 0.0;
+        const bool on = lane < M;
+        const cd x0 = s_cons[on ? lane : 0];
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+            h0[q] = cmk(rec[4 + 2 * q], rec[5 + 2 * q]);
+            h1[q] = cmk(rec[4 + 2 * (NR + q)], rec[5 + 2 * (NR + q)]);
+            r[q] = csub(a.yd[(size_t)gsym * NR + q], cmul(h0[q], x0));
+            g11 += cabs2(h1[q]);
+            scale += cabs2(r[q]);
+        }
+        auto dist = [&](int s1) {
+            const cd x1 = s_cons[s1];
+            double d = 0.0;
+#pragma unroll
+            for (int q = 0; q < NR; ++q) d += cabs2(csub(r[q], cmul(h1[q], x1)));
+            return d;
+        };
+        int best = 0;
+        double dbest = INFINITY;
+        bool scan = K == 0 || !(g11 > 0.0);
+        if (!scan) {
+            cd z = czero();
+#pragma unroll
+            for (int q = 0; q < NR; ++q) z = cfmac(z, r[q], h1[q]);     // h_1^H r
+            z = cscale(z, 1.0 / g11);
+            double bx = INFINITY, bx2 = INFINITY, by = INFINITY, by2 = INFINITY;
+            int ix = 0, ix2 = 0, iy = 0, iy2 = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const double dx = fabs(z.x - lre[k]);
+                if (dx < bx) { bx2 = bx; ix2 = ix; bx = dx; ix = k; }
+                else if (dx < bx2) { bx2 = dx; ix2 = k; }
+                const double dy = fabs(z.y - lim[k]);
+                if (dy < by) { by2 = by; iy2 = iy; by = dy; iy = k; }
+                else if (dy < by2) { by2 = dy; iy2 = k; }
+            }
+            const int s1 = s_grid.idx[ix * K + iy];
+            const double v1 = dist(s1);
+            // rounding of a distance: a few ulps of the terms it sums
+            double cm2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (k < K) cm2 = fmax(cm2, fma(lre[k], lre[k], lim[k] * lim[k]));
+            const double mg = 64.0 * 2.2e-16 * (scale + 4.0 * g11 * cm2);
+            const bool ra = K < 2 || dist(s_grid.idx[ix2 * K + iy]) > v1 + mg;
+            const bool rb = K < 2 || dist(s_grid.idx[ix * K + iy2]) > v1 + mg;
+            if (ra && rb) { best = s1; dbest = v1; }
+            else scan = true;
+        }
+        if (scan) {                                  // every point, first minimum in table order
+            dbest = dist(0);
+            best = 0;
+            for (int s1 = 1; s1 < M; ++s1) {
+                const double d = dist(s1);
+                if (d < dbest) { dbest = d; best = s1; }
+            }
+        }
+        // first minimum over the lanes (x_0 in table order)
+        double dm = on ? dbest : INFINITY;
+        int li = on ? lane : 64;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double od = shfl_xor_d(dm, off);
+            const int ol = __shfl_xor(li, off);
+            if (od < dm || (od == dm && ol < li)) { dm = od; li = ol; }
+        }
+        const int i1 = __shfl(best, li & 63);
+        if (lane == 0) {
+            const cd xa = s_cons[li & 63], xb = s_cons[i1];
+            cd* out = a.mom + (size_t)gsym * MS;
+            out[0] = xa;
+            out[1] = xb;
+            out[2] = cmulc(xa, xa);
+            out[3] = cmulc(xa, xb);
+            out[4] = cmulc(xb, xa);
+            out[5] = cmulc(xb, xb);
+        }
+        if (c.count && lane == 0) atomicAdd(&g_estep_pair, 1ull);
+    }
+}
+
 }  // namespace
 
 bool estep_pair_supported(const Problem& pb, int mode) {
-    if (mode != SBCE_ESTEP_SOFT || g_debug.estep_nopair) return false;
-    if (pb.NT == 2) return pb.M >= 4 && pb.M <= 64 && pb.NR >= 2 && pb.NR <= 8;   // estep_fact2_kernel
+    if (g_debug.estep_nopair) return false;
+    if (pb.NT == 2)                                 // estep_fact2_kernel / estep_hard2_kernel
+        return (mode == SBCE_ESTEP_SOFT || mode == SBCE_ESTEP_HARD) && pb.M >= 4 && pb.M <= 64 &&
+               pb.NR >= 2 && pb.NR <= 8;
+    if (mode != SBCE_ESTEP_SOFT) return false;
     return pb.NT == 4 && pb.M == 16 && pb.NR >= 4 && pb.NR <= 8;
 }
 
 // a.list: this pass's list (EstepArgs::list, counters 3 and 4, zeroed by the caller); the
 // symbols it cannot represent join the sweep's list (counter 0)
-hipError_t launch_estep_pair(const Problem& pb, const EstepArgs& a, int stride, int count,
+hipError_t launch_estep_pair(const Problem& pb, const EstepArgs& a, int stride, int count, int mode,
                              hipStream_t s) {
     PairConst c;
     c.B = pb.B; c.Td = pb.Td; c.stride = stride;
@@ -546,6 +669,15 @@ hipError_t launch_estep_pair(const Problem& pb, const EstepArgs& a, int stride, 
         if (fb > 2048) fb = 2048;
         if (fb < 1) fb = 1;
         const dim3 fgrid((unsigned)fb);
+        if (mode == SBCE_ESTEP_HARD) {
+            switch (pb.NR) {
+#define SBCE_H2(n) case n: hipLaunchKernelGGL((estep_hard2_kernel<n>), fgrid, dim3(64 * kF2Waves), 0, s, a, c, pb.M); break;
+                SBCE_H2(2) SBCE_H2(3) SBCE_H2(4) SBCE_H2(5) SBCE_H2(6) SBCE_H2(7) SBCE_H2(8)
+#undef SBCE_H2
+                default: return hipErrorInvalidValue;
+            }
+            return hipGetLastError();
+        }
         switch (pb.NR) {
 #define SBCE_F2(n) case n: hipLaunchKernelGGL((estep_fact2_kernel<n>), fgrid, dim3(64 * kF2Waves), 0, s, a, c, pb.M); break;
             SBCE_F2(2) SBCE_F2(3) SBCE_F2(4) SBCE_F2(5) SBCE_F2(6) SBCE_F2(7) SBCE_F2(8)

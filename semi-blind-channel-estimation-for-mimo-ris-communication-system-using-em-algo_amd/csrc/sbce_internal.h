@@ -383,7 +383,7 @@ hipError_t estep_debug_mfma(unsigned long long* out, int reset);   // SBCE_ESTEP
 hipError_t estep_debug_sphere(unsigned long long* out3, int reset);   // [enumerated, listed, single path]
 // factorised-weight soft E-step (estep_pair.hip) for the sphere pass's listed symbols
 bool estep_pair_supported(const Problem& pb, int mode);
-hipError_t launch_estep_pair(const Problem& pb, const EstepArgs& a, int stride, int count,
+hipError_t launch_estep_pair(const Problem& pb, const EstepArgs& a, int stride, int count, int mode,
                              hipStream_t s);
 hipError_t estep_debug_pair(unsigned long long* out, int reset);      // SBCE_ESTEP_COUNT=1
 hipError_t launch_gauss_rank1(const Problem& pb, const MstepArgs& a, hipStream_t s);

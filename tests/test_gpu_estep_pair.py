@@ -120,3 +120,32 @@ def test_fact2_estep_nt2_matches_sweep_and_oracle(sbce, n_rx, M, snr):
         mo, So, _, _ = estep_moments(th[0], b["y_d"][0], b["psi_d"][0].T, aps, varn)
         assert np.abs(m1[0] - mo).max() < 1e-11 * scale
         assert np.abs(S1[0] - So).max() < 1e-11 * scale
+
+
+@pytest.mark.parametrize("n_rx,M,snr", [(2, 64, -5), (2, 64, 10), (2, 64, 30), (3, 16, 0),
+                                        (4, 64, 20), (8, 16, 5)])
+def test_hard2_estep_nt2_matches_enumeration_and_oracle(sbce, n_rx, M, snr):
+    """n_tx = 2 log-max E-step (estep_hard2_kernel: lane = x_0, the best x_1 per axis with a
+    rounding-guarded rival check, first minimum in table order): decisions identical to the
+    enumeration path (SBCE_ESTEP_PAIR=0) and to the oracle's argmin over all M^2 hypotheses."""
+    power = {4: 2.0, 16: 10.0, 64: 42.0}[M]
+    varn = float(sbce.signal_model.snr_to_varn(snr, power))
+    b = sbce.signal_model.synthetic_batch(3, 2, n_rx, 15, 20, 60, M, varn, seed=80 + snr + n_rx,
+                                          pinv="scipy")
+    aps = sbce.qam.all_possible_symbols(b["cons"], 2)
+    lib = sbce._lib.load()
+    for th in (b["theta0"], b["h"] + 0.05 * b["theta0"] / np.abs(b["theta0"]).max()):
+        out = {}
+        for pair in ("1", "0"):
+            with sbce._lib.debug_env(SBCE_ESTEP_PAIR=pair, SBCE_ESTEP_COUNT="1"):
+                lib.sbce_debug_estep_pair(None, 1)
+                m, S = sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], th, varn, 2, "hard")
+                npair = ctypes.c_ulonglong(0)
+                lib.sbce_debug_estep_pair(ctypes.byref(npair), 0)
+            out[pair] = (m, S, npair.value)
+        assert out["0"][2] == 0 and out["1"][2] > 0
+        assert np.array_equal(out["1"][0], out["0"][0])
+        assert np.array_equal(out["1"][1], out["0"][1])
+        for i in range(3):
+            mo, So, _, _ = estep_moments(th[i], b["y_d"][i], b["psi_d"][i].T, aps, varn, "hard")
+            assert np.array_equal(out["1"][0][i], mo)
