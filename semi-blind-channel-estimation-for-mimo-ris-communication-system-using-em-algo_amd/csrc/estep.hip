@@ -2033,7 +2033,10 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
     }   // live
     // NT = 2 soft: a symbol the factorised pass can represent goes to its list (counter 3); the
     // other live symbols go to the enumeration's list: one atomic per wave and list
-    const bool f2 = NT == 2 && live && !single && f2d <= kPairDmax;
+    // (soft: D within range -> the factorised tables; else the narrow-posterior path, flagged by
+    // the entry's sign bit; hard: f2d = 0, every unresolved symbol)
+    const bool f2 = NT == 2 && c.pair && live && !single;
+    const bool wide = f2d <= kPairDmax;
     const bool enumer = live && !single && !f2;
     const int lane = threadIdx.x & 63;
     int32_t* cnt = a.list + nsym;
@@ -2046,7 +2049,7 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
             base = __shfl(base, first);
             if (f2)
                 a.list[2 * nsym + 2 * kEstepListCnt + base + __builtin_popcountll(bf & ((1ull << lane) - 1ull))] =
-                    (int32_t)gsym;
+                    wide ? (int32_t)gsym : (int32_t)((uint32_t)gsym | 0x80000000u);
         }
     }
     const unsigned long long bal = __ballot(enumer);

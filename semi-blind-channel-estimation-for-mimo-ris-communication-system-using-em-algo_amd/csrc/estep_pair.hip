@@ -38,6 +38,7 @@ typedef double d4v __attribute__((ext_vector_type(4)));
 struct PairConst {
     int B, Td, stride;     // prep record doubles per symbol
     double inv_s2;
+    double thr_d;          // NT = 2 soft2 symbols: weights below e^-50 of the best are skipped
     int count;             // SBCE_ESTEP_COUNT=1: count the resolved symbols
 };
 
@@ -394,20 +395,22 @@ __global__ __launch_bounds__(64 * kF2Waves) void estep_fact2_kernel(EstepArgs a,
     // symbols by a static stride (every symbol costs the same: no work grabbing), the next one's
     // index, channel and observation loaded while the current one is computed
     auto fetch = [&](int k, long& gs, cd (&hh)[2 * NR], cd (&yy)[NR]) {
-        gs = k < nwork ? (long)plist[k] : -1;
-        if (gs >= 0) {
-            const double* rec = a.prep + (size_t)gs * c.stride;
+        gs = k < nwork ? (long)plist[k] : 0;         // (a negative entry: soft2, see below)
+        if (k < nwork) {
+            const long g0 = gs & 0x7fffffffL;
+            const double* rec = a.prep + (size_t)g0 * c.stride;
 #pragma unroll
             for (int e = 0; e < 2 * NR; ++e) hh[e] = cmk(rec[4 + 2 * e], rec[5 + 2 * e]);
 #pragma unroll
-            for (int r = 0; r < NR; ++r) yy[r] = a.yd[(size_t)gs * NR + r];
+            for (int r = 0; r < NR; ++r) yy[r] = a.yd[(size_t)g0 * NR + r];
         }
     };
     long gnext;
     cd hnext[2 * NR], ynext[NR];
     fetch(gi, gnext, hnext, ynext);
     for (; gi < nwork; gi += nwaves) {
-        const long gsym = gnext;
+        const bool soft2 = gnext < 0;                // sign bit: a symbol whose range D is too wide
+        const long gsym = gnext & 0x7fffffffL;
         cd hc[2 * NR], yc[NR];
 #pragma unroll
         for (int e = 0; e < 2 * NR; ++e) hc[e] = hnext[e];
@@ -423,6 +426,7 @@ __global__ __launch_bounds__(64 * kF2Waves) void estep_fact2_kernel(EstepArgs a,
             continue;
         }
         const double is2 = a.varn_t ? uniform_d(trial_noise(a.varn_t[b]).inv_s2) : c.inv_s2;
+        if (soft2) continue;                         // estep_soft2_kernel's
         cd z0 = czero(), z1 = czero(), g = czero();
         double g00 = 0.0, g11 = 0.0;
 #pragma unroll
@@ -520,6 +524,177 @@ __global__ __launch_bounds__(64 * kF2Waves) void estep_fact2_kernel(EstepArgs a,
     flush();
 }
 
+
+// Narrow posteriors of n_tx = 2 (the tree pass's entries with the sign bit: range D above the
+// factorised tables' limit): lane = x_0, r = y - h_0 x_0; d(x_1) = g_11 |x_1 - z|^2 + (||r||^2 -
+// g_11 |z|^2), z = h_1^H r / g_11, so the lane's best x_1 is the per-axis nearest level pair (taken
+// when both per-axis rivals are farther by more than the distances' rounding, else every point is
+// scanned), d_min the wave minimum, and the x_1 within thr = 50 varn^2 of d_min (the sweep's e^-50
+// skip) lie in a box of half-width sqrt((d_min + thr - c_0) / g_11) around z; each is checked
+// directly and weighted exp(-(d - d_min) / s2).
+template <int NR>
+__global__ __launch_bounds__(64 * kF2Waves) void estep_soft2_kernel(EstepArgs a, PairConst c, int M) {
+    constexpr int MS = 6;
+    __shared__ cd s_cons[64];
+    __shared__ GridLds s_grid;
+    __shared__ int32_t s_fail[kF2Waves][64];
+    if ((int)threadIdx.x < M) s_cons[threadIdx.x] = a.cons[threadIdx.x];
+    __syncthreads();
+    grid_build(s_cons, M, &s_grid);
+    const int K = s_grid.K;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const long nsym = (long)c.B * c.Td;
+    int32_t* cnt = a.list + nsym;
+    const int32_t* plist = a.list + 2 * nsym + 2 * kEstepListCnt;
+    const int nwork = __builtin_amdgcn_readfirstlane(cnt[3]);
+    const int nwaves = gridDim.x * kF2Waves;
+    int32_t* s_f = s_fail[wave];
+    int nf = 0;
+    auto flush = [&]() {
+        if (nf == 0) return;
+        int base = 0;
+        if (lane == 0) base = atomicAdd(cnt, nf);
+        base = __shfl(base, 0);
+        if (lane < nf) a.list[base + lane] = s_f[lane];
+        nf = 0;
+        wave_sync();
+    };
+    auto wmax = [](double v) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v = fmax(v, shfl_xor_d(v, off));
+        return v;
+    };
+    auto wsum = [](double v) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += shfl_xor_d(v, off);
+        return v;
+    };
+    double lre[8], lim[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        lre[k] = k < K ? s_grid.lre[k] : INFINITY;
+        lim[k] = k < K ? s_grid.lim[k] : INFINITY;
+    }
+    for (int gi = blockIdx.x * kF2Waves + wave; gi < nwork; gi += nwaves) {
+        const int32_t ent = plist[gi];
+        if (ent >= 0) continue;                      // the factorised tables' symbol
+        const long gsym = (long)(ent & 0x7fffffff);
+        const int b = (int)(gsym / c.Td);
+        if (a.done && a.done[b]) continue;
+        if (K == 0) {                                // not a square grid: the sweep weighs it
+            if (lane == 0) s_f[nf] = (int32_t)gsym;
+            ++nf;
+            if (nf == 64) flush();
+            continue;
+        }
+        const double is2 = a.varn_t ? uniform_d(trial_noise(a.varn_t[b]).inv_s2) : c.inv_s2;
+        const double* rec = a.prep + (size_t)gsym * c.stride;
+        cd hc[2 * NR], yc[NR];
+#pragma unroll
+        for (int e = 0; e < 2 * NR; ++e) hc[e] = cmk(rec[4 + 2 * e], rec[5 + 2 * e]);
+#pragma unroll
+        for (int q = 0; q < NR; ++q) yc[q] = a.yd[(size_t)gsym * NR + q];
+        // ---- narrow posterior: lane = x_0, the x_1 within e^-50 of the best hypothesis ----
+        const double thr = a.varn_t ? uniform_d(trial_noise(a.varn_t[b]).thr_d) : c.thr_d;
+        const bool on = lane < M;
+        const cd x0 = s_cons[on ? lane : 0];
+        cd r[NR], h1[NR];
+        double g11 = 0.0, scale = 0.0;
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+            h1[q] = hc[NR + q];
+            r[q] = csub(yc[q], cmul(hc[q], x0));
+            g11 += cabs2(h1[q]);
+            scale += cabs2(r[q]);
+        }
+        auto dist = [&](int s1) {
+            const cd x1 = s_cons[s1];
+            double d = 0.0;
+#pragma unroll
+            for (int q = 0; q < NR; ++q) d += cabs2(csub(r[q], cmul(h1[q], x1)));
+            return d;
+        };
+        cd z = czero();
+#pragma unroll
+        for (int q = 0; q < NR; ++q) z = cfmac(z, r[q], h1[q]);    // h_1^H r
+        const bool deg = !(g11 > 0.0);
+        z = deg ? czero() : cscale(z, 1.0 / g11);
+        // the lane's best x_1 (exact: every point when the per-axis candidate is not clear)
+        double dbest = INFINITY;
+        {
+            double bx = INFINITY, bx2 = INFINITY, by = INFINITY, by2 = INFINITY;
+            int ix = 0, ix2 = 0, iy = 0, iy2 = 0;
+            double cm2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const double dx = fabs(z.x - lre[k]);
+                if (dx < bx) { bx2 = bx; ix2 = ix; bx = dx; ix = k; }
+                else if (dx < bx2) { bx2 = dx; ix2 = k; }
+                const double dy = fabs(z.y - lim[k]);
+                if (dy < by) { by2 = by; iy2 = iy; by = dy; iy = k; }
+                else if (dy < by2) { by2 = dy; iy2 = k; }
+                if (k < K) cm2 = fmax(cm2, fma(lre[k], lre[k], lim[k] * lim[k]));
+            }
+            const double mg = 64.0 * 2.2e-16 * (scale + 4.0 * g11 * cm2);
+            const double v1 = dist(s_grid.idx[ix * K + iy]);
+            const bool clear = !deg && K >= 2 && dist(s_grid.idx[ix2 * K + iy]) > v1 + mg &&
+                               dist(s_grid.idx[ix * K + iy2]) > v1 + mg;
+            if (clear) {
+                dbest = v1;
+            } else {
+                for (int s1 = 0; s1 < M; ++s1) dbest = fmin(dbest, dist(s1));
+            }
+        }
+        const double dmin = wmax(on ? -dbest : -INFINITY) * -1.0;
+        // d(x_1) = g11 |x_1 - z|^2 + (||r||^2 - g11 |z|^2): the points within thr of dmin lie in
+        // a box of half-width rho around z (widened for rounding); each is checked directly
+        double Zl = 0.0, Q1 = 0.0;
+        cd X1 = czero();
+        if (on) {
+            const double c0 = scale - g11 * cabs2(z);
+            const double rho2 = deg ? INFINITY : (dmin + thr - c0) / g11;
+            const double rho = rho2 > 0.0 ? sqrt(rho2) * (1.0 + 1e-7) + 1e-9 * sqrt(1.0 + cabs2(z)) : -1.0;
+            for (int kx = 0; kx < K; ++kx) {
+                if (!(fabs(lre[kx] - z.x) <= rho)) continue;
+                for (int ky = 0; ky < K; ++ky) {
+                    if (!(fabs(lim[ky] - z.y) <= rho)) continue;
+                    const int s1 = s_grid.idx[kx * K + ky];
+                    const double d = dist(s1);
+                    if (d - dmin > thr) continue;
+                    const double w = exp(-(d - dmin) * is2);
+                    const cd x1 = s_cons[s1];
+                    Zl += w;
+                    X1 = caxpy(X1, w, x1);
+                    Q1 = fma(w, cabs2(x1), Q1);
+                }
+            }
+        }
+        const double Z = wsum(Zl);
+        const double m0r = wsum(Zl * x0.x), m0i = wsum(Zl * x0.y), S00 = wsum(Zl * cabs2(x0));
+        const double m1r = wsum(X1.x), m1i = wsum(X1.y), S11 = wsum(Q1);
+        const cd s01l = cmulc(x0, X1);                                 // x_0 conj(sum w x_1)
+        const double s01r = wsum(s01l.x), s01i = wsum(s01l.y);
+        if (!(Z > 0.0)) {                        // (cannot happen: the best hypothesis has w = 1)
+            if (lane == 0) s_f[nf] = (int32_t)gsym;
+            ++nf;
+            if (nf == 64) flush();
+            continue;
+        }
+        const double iz = 1.0 / Z;
+        if (lane == 0) {
+            cd* out = a.mom + (size_t)gsym * MS;
+            out[0] = cmk(m0r * iz, m0i * iz);
+            out[1] = cmk(m1r * iz, m1i * iz);
+            out[2] = cmk(S00 * iz, 0.0);
+            out[3] = cmk(s01r * iz, s01i * iz);
+            out[4] = cmk(s01r * iz, -s01i * iz);
+            out[5] = cmk(S11 * iz, 0.0);
+        }
+        if (c.count && lane == 0) atomicAdd(&g_estep_pair, 1ull);
+    }
+    flush();
+}
 
 // ---------------------------------------------------------------- n_tx = 2, hard decision
 // The log-max E-step (argmin over the M^2 hypotheses of ||y - h_0 x_0 - h_1 x_1||^2, first table
@@ -658,6 +833,7 @@ hipError_t launch_estep_pair(const Problem& pb, const EstepArgs& a, int stride, 
     PairConst c;
     c.B = pb.B; c.Td = pb.Td; c.stride = stride;
     c.inv_s2 = 1.0 / (pb.varn * pb.varn);
+    c.thr_d = 50.0 * pb.varn * pb.varn;              // estep.hip kSkipThr varn^2 (TrialNoise::thr_d)
     c.count = count;
     // waves grab listed symbols until the list is exhausted: a grid that fills the chip
     const long nsym = (long)pb.B * pb.Td;
@@ -679,7 +855,8 @@ hipError_t launch_estep_pair(const Problem& pb, const EstepArgs& a, int stride, 
             return hipGetLastError();
         }
         switch (pb.NR) {
-#define SBCE_F2(n) case n: hipLaunchKernelGGL((estep_fact2_kernel<n>), fgrid, dim3(64 * kF2Waves), 0, s, a, c, pb.M); break;
+#define SBCE_F2(n) case n: hipLaunchKernelGGL((estep_fact2_kernel<n>), fgrid, dim3(64 * kF2Waves), 0, s, a, c, pb.M); \
+                           hipLaunchKernelGGL((estep_soft2_kernel<n>), fgrid, dim3(64 * kF2Waves), 0, s, a, c, pb.M); break;
             SBCE_F2(2) SBCE_F2(3) SBCE_F2(4) SBCE_F2(5) SBCE_F2(6) SBCE_F2(7) SBCE_F2(8)
 #undef SBCE_F2
             default: return hipErrorInvalidValue;

@@ -99,10 +99,11 @@ def _run_nt(sbce, b, th, varn, pair, n_tx):
                                         (3, 16, 0), (2, 4, -5), (4, 64, 10), (8, 16, 20)])
 def test_fact2_estep_nt2_matches_sweep_and_oracle(sbce, n_rx, M, snr):
     """n_tx = 2 (BASELINE cfg 5: 2 x 2, N_RIS = 15, 64-QAM): the tree pass routes every symbol it
-    does not resolve alone and whose factor range D is representable to the factorised pass
-    (estep_fact2_kernel, four 1-D and four K x K log tables, the (a1, b1) sum split into an a1 and
-    a b1 sum); its moments equal the enumeration / sweep path's (SBCE_ESTEP_PAIR=0) and the
-    oracle's enumeration of all M^2 hypotheses to 1e-11 max|c|^2."""
+    does not resolve alone to estep_fact2_kernel -- the factorised tables (four 1-D and four K x K
+    log tables, the (a1, b1) sum split into an a1 and a b1 sum) when the range D is representable,
+    else the narrow-posterior path (lane = x0, the x1 within e^-50 in a box around h1^H r / g11);
+    its moments equal the enumeration / sweep path's (SBCE_ESTEP_PAIR=0) and the oracle's
+    enumeration of all M^2 hypotheses to 1e-11 max|c|^2, from -5 to 30 dB."""
     power = {4: 2.0, 16: 10.0, 64: 42.0}[M]          # the square QAM's mean symbol energy
     varn = float(sbce.signal_model.snr_to_varn(snr, power))
     b = sbce.signal_model.synthetic_batch(3, 2, n_rx, 15, 20, 60, M, varn, seed=60 + snr + n_rx,
