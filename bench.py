@@ -79,7 +79,7 @@ def metric_name(n_tx, N, T_p, T_d):
 
 # kernels of one E-step / M-step launch sequence (rocprofv3 names, tools/pmc_summary.py keys)
 ESTEP_KERNELS = ["estep_tree_kernel", "estep_bfs_kernel", "estep_pair_kernel", "estep_bounds_kernel", "estep_prep_kernel",
-                 "estep_mfma_kernel_occ3", "estep_mfma_kernel"]
+                 "estep_mfma_kernel"]
 MSTEP_KERNELS = ["pilot_factor_kernel", "pilot_rhs_kernel", "rbuild_herm_kernel", "rbuild_kernel", "rhs_lds_kernel",
                  "rhs_dma_kernel", "rhs_kernel", "diag_tol_kernel", "panel_update2_kernel",
                  "panel_factor_kernel", "backsub_kernel", "backsub4_kernel"]

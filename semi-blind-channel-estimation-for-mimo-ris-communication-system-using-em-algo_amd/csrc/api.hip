@@ -16,7 +16,7 @@ namespace sbce {
 DebugConfig g_debug;
 
 namespace {
-constexpr DebugConfig kDebugDefault = {false, false, false, false, 0, false, 128, false, false, false,
+constexpr DebugConfig kDebugDefault = {false, false, false, false, false, 128, false, false, false,
                                        true, false, false, 0, false};
 constexpr int kSphereBudgetMax = 256;      // estep.hip kBfsPmax
 
@@ -28,7 +28,6 @@ void read_debug_env(DebugConfig& c) {
     if ((v = env("SBCE_ESTEP_PRUNE"))) c.estep_noprune = v[0] == '0';
     if ((v = env("SBCE_ESTEP_COUNT"))) c.estep_count = v[0] == '1';
     if ((v = env("SBCE_ESTEP_F32"))) c.estep_nof32 = v[0] == '0';
-    if ((v = env("SBCE_ESTEP_OCC"))) c.estep_occ = (v[0] == '2' || v[0] == '3') ? v[0] : 0;
     if ((v = env("SBCE_ESTEP_SPHERE"))) c.estep_nosphere = v[0] == '0';
     if ((v = env("SBCE_SPHERE_BUDGET"))) {
         const int bu = atoi(v);
@@ -50,7 +49,7 @@ bool debug_nondefault() {
     const DebugConfig& c = g_debug;
     const DebugConfig& d = kDebugDefault;
     return c.estep_valu != d.estep_valu || c.estep_noprune != d.estep_noprune ||
-           c.estep_nof32 != d.estep_nof32 || c.estep_occ != d.estep_occ ||
+           c.estep_nof32 != d.estep_nof32 ||
            c.estep_nosphere != d.estep_nosphere || c.sphere_budget != d.sphere_budget ||
            c.backsub_general != d.backsub_general || c.chol_valu != d.chol_valu ||
            c.estep_nopair != d.estep_nopair || c.cplx3 != d.cplx3 ||
@@ -286,7 +285,6 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
             if ((rc = hip_rc(launch_sup_shift_mom(pb, ea.mom, (const cd*)p->x_sup, ea.done, s))))
                 return rc;
         } else {
-            ea.wide = it == 0;
             if ((rc = hip_rc(launch_estep(pb, ea, estep_mode, s)))) return rc;
         }
         if (small) {

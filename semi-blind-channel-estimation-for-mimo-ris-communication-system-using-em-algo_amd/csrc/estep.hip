@@ -2006,6 +2006,9 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
             }
         }
     }
+    // the tree record: only the enumeration reads it (not the single-path symbols, nor the
+    // n_tx = 2 symbols of the factorised passes)
+    if (!single && !(NT == 2 && c.pair)) {
     int packed = ok ? (1 << 16) : 0;
 #pragma unroll
     for (int q = 0; q < NT; ++q) packed |= q << (4 * lev[q]);   // level l holds stream perm[l]
@@ -2030,6 +2033,7 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
             rec[5 + 3 * NT + 2 * k] = Lm[i][j].y;
             ++k;
         }
+    }   // enumerated
     }   // live
     // NT = 2 soft: a symbol the factorised pass can represent goes to its list (counter 3); the
     // other live symbols go to the enumeration's list: one atomic per wave and list
@@ -2283,14 +2287,6 @@ template <int NT, int NR, int MODE, int TU, bool V16 = false>
 __global__ __launch_bounds__(128) void estep_mfma_kernel(EstepArgs a, MfmaConst c) {
     estep_mfma_body<NT, NR, MODE, TU, V16>(a, c);
 }
-// Same kernel held to 168 VGPRs (3 waves per SIMD); the few spills this costs at
-// n_rx <= 4 sit in the per-column-tile code, outside the MFMA group loop.
-template <int NT, int NR, int MODE, int TU, bool V16 = false>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) void
-estep_mfma_kernel_occ3(EstepArgs a, MfmaConst c) {
-    estep_mfma_body<NT, NR, MODE, TU, V16>(a, c);
-}
-
 bool make_mfma(const Problem& pb, MfmaConst& c, size_t& lds, long& blocks) {
     if (pb.NT < 2 || pb.NT > 4 || pb.NR < 1 || pb.NR > 8) return false;
     if (pb.M < 2 || pb.M > 64 || (pb.M & (pb.M - 1))) return false;
@@ -2337,21 +2333,6 @@ hipError_t dispatch_mfma_mode(const MfmaConst& c, size_t lds, long blocks, const
         if (c.JA != 256 || c.JB != 256 || c.chunk != 256 || c.nkt_pad != 16 ||
             c.prep_stride != 4 + 2 * NT * NR + 16 + 6 * NR)
             return hipErrorInvalidValue;
-        if constexpr (NR <= 4) {
-            // the 168-VGPR build (3 waves/SIMD) for the wide iteration-0 posteriors, the uncapped
-            // one (206 VGPRs, no spills) otherwise: converged E-step 0.566 -> 0.539 ms, iteration 0
-            // 5.17 vs 5.58 ms (profiles/r04/estep_f32_ab_20db.log); SBCE_ESTEP_OCC=2/3 forces one
-            const bool capped = g_debug.estep_occ == '3' || (g_debug.estep_occ != '2' && a.wide);
-            if (capped) {
-                if (mode == SBCE_ESTEP_HARD)
-                    hipLaunchKernelGGL((estep_mfma_kernel_occ3<NT, NR, SBCE_ESTEP_HARD, 4, true>),
-                                       dim3((unsigned)blocks), dim3(64 * kMfmaWaves), lds, s, a, c);
-                else
-                    hipLaunchKernelGGL((estep_mfma_kernel_occ3<NT, NR, SBCE_ESTEP_SOFT, 4, true>),
-                                       dim3((unsigned)blocks), dim3(64 * kMfmaWaves), lds, s, a, c);
-                return hipGetLastError();
-            }
-        }
         if (mode == SBCE_ESTEP_HARD)
             hipLaunchKernelGGL((estep_mfma_kernel<NT, NR, SBCE_ESTEP_HARD, 4, true>),
                                dim3((unsigned)blocks), dim3(64 * kMfmaWaves), lds, s, a, c);

@@ -166,8 +166,6 @@ struct DebugConfig {
     bool estep_noprune;  // SBCE_ESTEP_PRUNE=0     no column-tile bounds
     bool estep_count;    // SBCE_ESTEP_COUNT=1     device counters (results unchanged)
     bool estep_nof32;    // SBCE_ESTEP_F32=0       no FP32 screen of the sweep's tile groups
-    char estep_occ;      // SBCE_ESTEP_OCC         0 auto (the 168-VGPR sweep at EM iteration 0 only),
-                         //                        '2' never, '3' always
     bool estep_nosphere; // SBCE_ESTEP_SPHERE=0    tile sweep only
     int sphere_budget;   // SBCE_SPHERE_BUDGET     path list cap per level (default 128)
     bool backsub_general;// SBCE_BACKSUB=1         the general back substitution at every shape
@@ -212,9 +210,6 @@ struct EstepArgs {
                        // symbols the enumeration left to the factorised-weight pass;
                        // null: no sphere
     double* tree;      // [B*Td][32] the sphere pass's per-symbol search-tree records
-    // launch hint: theta is the pilot-only theta_0 (EM iteration 0), whose wide posteriors make
-    // the sweep exp-path heavy -- it then runs the 168-VGPR (three waves per SIMD) build
-    int wide = 0;
     const double* varn_t = nullptr;   // [B] per-trial noise variances (sbce_ptrs.varn_t), or null
 };
 

@@ -296,21 +296,6 @@ def test_sphere_estep_cfg1_geometry(sbce, snr):
         assert np.array_equal(mh1, mh0)
 
 
-def test_em_sweep_build_choice_is_bitwise_neutral(sbce):
-    """sbce_em runs the 168-VGPR sweep build at iteration 0 and the uncapped one afterwards
-    (EstepArgs::wide); both are the same code under a different register budget, so the EM's
-    theta is bitwise the same with either forced for every iteration (SBCE_ESTEP_OCC=3 / 2)."""
-    varn = float(sbce.signal_model.snr_to_varn(20.0))
-    b = sbce.signal_model.synthetic_batch(6, 4, 4, 64, 16, 256, 16, varn, seed=77)   # cfg1 shape
-    out = {}
-    for occ in ("a", "2", "3"):
-        with sbce._lib.debug_env(SBCE_ESTEP_OCC=occ):
-            out[occ] = sbce.em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, 4,
-                                     b["theta0"])["theta"]
-    assert np.isfinite(out["a"]).all()
-    assert np.array_equal(out["a"], out["2"]) and np.array_equal(out["a"], out["3"])
-
-
 @pytest.mark.parametrize("snr", [30, 20, 10, 0, -5])
 def test_estep_fp32_screen_is_bitwise_neutral(sbce, snr):
     """The sweep's FP32 screen of its tile groups (V16 geometry: n_tx = 4, 16-QAM) only skips
