@@ -692,12 +692,21 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     const long nwork = listed ? (long)__builtin_amdgcn_readfirstlane(cnt[0]) : nsym;
     const bool prep = a.prep != nullptr;
     auto sym_of = [&](long gi) -> long { return listed ? (long)a.list[gi] : gi; };
+    // listed: a wave's first entry is its global wave index (no atomic -- with a short or empty
+    // list most waves exit at once; 4096 same-address atomics of an empty list cost ~50 us),
+    // the later ones come from the counter, which starts past the first round
+    bool first = true;
     for (;;) {
     long chunk_id;
     if (listed) {
-        int v = 0;
-        if (lane == 0) v = atomicAdd(cnt + 1, 1);
-        chunk_id = __builtin_amdgcn_readfirstlane(__shfl(v, 0));
+        if (first) {
+            chunk_id = (long)blockIdx.x * kMfmaWaves + wave;
+        } else {
+            int v = 0;
+            if (lane == 0) v = atomicAdd(cnt + 1, 1);
+            chunk_id = (long)gridDim.x * kMfmaWaves + __builtin_amdgcn_readfirstlane(__shfl(v, 0));
+        }
+        first = false;
     } else {
         chunk_id = (long)blockIdx.x * kMfmaWaves + wave;
     }
