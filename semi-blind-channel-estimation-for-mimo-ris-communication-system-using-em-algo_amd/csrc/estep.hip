@@ -2044,35 +2044,42 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
         }
     }   // enumerated
     }   // live
-    // NT = 2 soft: a symbol the factorised pass can represent goes to its list (counter 3); the
-    // other live symbols go to the enumeration's list: one atomic per wave and list
-    // (soft: D within range -> the factorised tables; else the narrow-posterior path, flagged by
-    // the entry's sign bit; hard: f2d = 0, every unresolved symbol)
     const bool f2 = NT == 2 && c.pair && live && !single;
     const bool wide = f2d <= kPairDmax;
     const bool enumer = live && !single && !f2;
     const int lane = threadIdx.x & 63;
     int32_t* cnt = a.list + nsym;
-    if (NT == 2) {
-        const unsigned long long bf = __ballot(f2);
-        if (bf) {
-            const int first = __builtin_ctzll(bf);
-            int base = 0;
-            if (lane == first) base = atomicAdd(cnt + 3, __builtin_popcountll(bf));
-            base = __shfl(base, first);
-            if (f2)
-                a.list[2 * nsym + 2 * kEstepListCnt + base + __builtin_popcountll(bf & ((1ull << lane) - 1ull))] =
-                    wide ? (int32_t)gsym : (int32_t)((uint32_t)gsym | 0x80000000u);
-        }
+    // one atomic per BLOCK and list (4096 per-wave same-address atomics serialise at the L2):
+    // the waves' counts through LDS, thread l reserves list l's block range
+    __shared__ int s_n[2][4];
+    __shared__ int s_b[2];
+    const int wv = threadIdx.x >> 6;
+    const unsigned long long bf = __ballot(f2), be = __ballot(enumer);
+    if (lane == 0) {
+        s_n[0][wv] = __builtin_popcountll(bf);
+        s_n[1][wv] = __builtin_popcountll(be);
     }
-    const unsigned long long bal = __ballot(enumer);
-    if (bal) {
-        const int first = __builtin_ctzll(bal);
-        int base = 0;
-        if (lane == first) base = atomicAdd(cnt + 2, __builtin_popcountll(bal));
-        base = __shfl(base, first);
-        if (enumer)
-            cnt[kEstepListCnt + base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = (int32_t)gsym;
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const int l = threadIdx.x;
+        const int tot = s_n[l][0] + s_n[l][1] + s_n[l][2] + s_n[l][3];
+        s_b[l] = tot ? atomicAdd(cnt + (l ? 2 : 3), tot) : 0;
+    }
+    __syncthreads();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    if (f2 || enumer) {
+        const int l = f2 ? 0 : 1;
+        int base = s_b[l] + __builtin_popcountll((f2 ? bf : be) & lt);
+        for (int w = 0; w < wv; ++w) base += s_n[l][w];
+        // NT = 2 soft: a symbol the factorised pass can represent goes to its list (counter 3)
+        // (D within range -> the factorised tables; else the narrow-posterior path, flagged by
+        // the entry's sign bit; hard: f2d = 0, every unresolved symbol); the other live
+        // symbols go to the enumeration's list (counter 2)
+        if (f2)
+            a.list[2 * nsym + 2 * kEstepListCnt + base] =
+                wide ? (int32_t)gsym : (int32_t)((uint32_t)gsym | 0x80000000u);
+        else
+            cnt[kEstepListCnt + base] = (int32_t)gsym;
     }
     if (c.count) {
         const unsigned long long one = __ballot(single);
