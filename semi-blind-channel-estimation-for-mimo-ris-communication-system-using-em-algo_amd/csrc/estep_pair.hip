@@ -382,16 +382,8 @@ __global__ __launch_bounds__(64 * kF2Waves) void estep_fact2_kernel(EstepArgs a,
         nf = 0;
         wave_sync();
     };
-    auto wmax = [](double v) {
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) v = fmax(v, shfl_xor_d(v, off));
-        return v;
-    };
-    auto wsum = [](double v) {
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) v += shfl_xor_d(v, off);
-        return v;
-    };
+    auto wmax = [](double v) { return wave_max_dpp(v); };
+    auto wsum = [](double v) { return wave_sum_dpp(v); };
     // symbols by a static stride (every symbol costs the same: no work grabbing), the next one's
     // index, channel and observation loaded while the current one is computed
     auto fetch = [&](int k, long& gs, cd (&hh)[2 * NR], cd (&yy)[NR]) {
@@ -560,16 +552,8 @@ __global__ __launch_bounds__(64 * kF2Waves) void estep_soft2_kernel(EstepArgs a,
         nf = 0;
         wave_sync();
     };
-    auto wmax = [](double v) {
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) v = fmax(v, shfl_xor_d(v, off));
-        return v;
-    };
-    auto wsum = [](double v) {
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) v += shfl_xor_d(v, off);
-        return v;
-    };
+    auto wmax = [](double v) { return wave_max_dpp(v); };
+    auto wsum = [](double v) { return wave_sum_dpp(v); };
     double lre[8], lim[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {

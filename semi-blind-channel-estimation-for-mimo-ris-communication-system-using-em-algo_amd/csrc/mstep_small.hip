@@ -27,6 +27,7 @@ namespace {
 constexpr int kSmallMaxL = 64;
 constexpr int kSmallThreads = 256;
 constexpr int kStageCd = 2048;                // staged symbols: <= 32 KB of complex doubles
+constexpr int kStageMf = 1024;                // the MFMA build's symbol chunks
 
 // ---- MFMA build (P <= 16: every (i, j) block of R is ONE 16 x 16 complex tile) ----
 // R_ij[p][q] = sum_t a_t[p] conj(b_t[q]) with a = psi_t[p] S_t[i][j] (data) or u_t[p n_tx + i]
@@ -176,9 +177,8 @@ __device__ __forceinline__ void mfma_build(const MstepArgs& a, int b, int P, int
 // substitution) of L and y_c / x_c cross threads, through a double-buffered LDS vector: one
 // barrier per column.
 template <int NR, int KB, int MNT>
-__global__ __launch_bounds__(kSmallThreads) void mstep_small_kernel(MstepArgs a, int NT, int P,
-                                                                    int Tp, int Td, int L,
-                                                                    int write_sys, int stop, int sg) {
+__device__ __forceinline__ void mstep_small_body(const MstepArgs& a, int NT, int P, int Tp, int Td,
+                                                 int L, int write_sys, int stop, int sg) {
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
     constexpr int YK = (64 * NR + kSmallThreads - 1) / kSmallThreads;
@@ -422,11 +422,30 @@ __global__ __launch_bounds__(kSmallThreads) void mstep_small_kernel(MstepArgs a,
     if (tid == 0 && a.status && anybad) a.status[b] |= a.clamp_status;
 }
 
+template <int NR, int KB, int MNT>
+__global__ __launch_bounds__(kSmallThreads) void mstep_small_kernel(MstepArgs a, int NT, int P,
+                                                                    int Tp, int Td, int L,
+                                                                    int write_sys, int stop, int sg) {
+    mstep_small_body<NR, KB, MNT>(a, NT, P, Tp, Td, L, write_sys, stop, sg);
+}
+// n_tx <= 2 MFMA build (BASELINE cfg 5: L = 32, 1280 trials) held to 96 VGPRs (no spills) and
+// ~21 KB of LDS: five workgroups per CU, so 1280 trials run in one round instead of two
+template <int NR, int KB, int MNT>
+__global__ __launch_bounds__(kSmallThreads) __attribute__((amdgpu_waves_per_eu(5))) void
+mstep_small5_kernel(MstepArgs a, int NT, int P, int Tp, int Td, int L, int write_sys, int stop, int sg) {
+    mstep_small_body<NR, KB, MNT>(a, NT, P, Tp, Td, L, write_sys, stop, sg);
+}
+
 template <int KB, int MNT>
 hipError_t launch_nr(const Problem& pb, const MstepArgs& a, size_t lds, int write_sys, int sg,
                      hipStream_t s) {
     switch (pb.NR) {
-#define SBCE_MS(n) case n: hipLaunchKernelGGL((mstep_small_kernel<n, KB, MNT>), dim3(pb.B), dim3(kSmallThreads), lds, s, a, pb.NT, pb.P, pb.Tp, pb.Td, pb.L, write_sys, g_debug.small_stop, sg); break;
+#define SBCE_MS(n) case n: \
+    if constexpr (MNT == 2 && n <= 4) \
+        hipLaunchKernelGGL((mstep_small5_kernel<n, KB, MNT>), dim3(pb.B), dim3(kSmallThreads), lds, s, a, pb.NT, pb.P, pb.Tp, pb.Td, pb.L, write_sys, g_debug.small_stop, sg); \
+    else \
+        hipLaunchKernelGGL((mstep_small_kernel<n, KB, MNT>), dim3(pb.B), dim3(kSmallThreads), lds, s, a, pb.NT, pb.P, pb.Tp, pb.Td, pb.L, write_sys, g_debug.small_stop, sg); \
+    break;
         SBCE_MS(1) SBCE_MS(2) SBCE_MS(3) SBCE_MS(4) SBCE_MS(5) SBCE_MS(6) SBCE_MS(7) SBCE_MS(8)
 #undef SBCE_MS
         default: return hipErrorInvalidValue;
@@ -448,7 +467,9 @@ hipError_t launch_mstep_small(const Problem& pb, const MstepArgs& a, bool write_
     const int KB = (pb.L + 15) / 16;
     // P <= 16 (BASELINE cfg 5): the MFMA build, R and B^H through LDS; else the VALU build
     const bool mf = pb.P <= 16 && pb.NT <= 3 && !g_debug.small_valu && g_debug.small_stop == 0;
-    int sg = kStageCd;
+    // the MFMA build's staging area also holds its R / B^H result; its symbol chunks are kept to
+    // 1024 complex values (five workgroups per CU at cfg 5)
+    int sg = mf ? kStageMf : kStageCd;
     if (mf && pb.L * (pb.L + 1) + pb.L * pb.NR > sg) sg = pb.L * (pb.L + 1) + pb.L * pb.NR;
     const size_t lds = ((size_t)sg + 2 * (64 + 8)) * sizeof(cd) + (64 + 4) * sizeof(double);
     if (mf) {
