@@ -1052,8 +1052,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                     s_al32[s0 * 16 + col] = (float)al;     // natural order: f32 C/D rows 4 rq + q
                     am = fmax(am, al);
                 }
-                for (int off = 32; off >= 1; off >>= 1) am = fmax(am, shfl_xor_d(am, off));
-                amax = am;
+                amax = wave_max_dpp(am);
                 wave_sync();
                 table_ready = true;
             }
@@ -1161,7 +1160,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
                 cm += gam;
                 if (__any(cm < mshift)) {
                     double mn = fmin(cm, mshift);
-                    for (int off = 32; off >= 1; off >>= 1) mn = fmin(mn, shfl_xor_d(mn, off));
+                    mn = wave_min_dpp(mn);
                     const double f = fexp_neg((mn - mshift) * inv_s2);
                     mshift = mn;
                     // V16: ck, mu are formed at the column tile's end; the stream-3 totals
@@ -1270,11 +1269,7 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     constexpr int MS = NT + NT * NT;
     cd* out = a.mom + (size_t)gsym * MS;
     if (MODE == SBCE_ESTEP_HARD) {
-        for (int off = 32; off >= 1; off >>= 1) {
-            const double od = shfl_xor_d(best_d, off);
-            const int oj = __shfl_xor(best_j, off);
-            if (od < best_d || (od == best_d && oj < best_j)) { best_d = od; best_j = oj; }
-        }
+        wave_argmin_dpp(best_d, best_j);
         if (lane == 0) {
             cd x[NT];
 #pragma unroll

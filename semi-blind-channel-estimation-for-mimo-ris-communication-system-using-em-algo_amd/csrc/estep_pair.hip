@@ -778,13 +778,8 @@ __global__ __launch_bounds__(64 * kF2Waves) void estep_hard2_kernel(EstepArgs a,
         // first minimum over the lanes (x_0 in table order)
         double dm = on ? dbest : INFINITY;
         int li = on ? lane : 64;
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const double od = shfl_xor_d(dm, off);
-            const int ol = __shfl_xor(li, off);
-            if (od < dm || (od == dm && ol < li)) { dm = od; li = ol; }
-        }
-        const int i1 = __shfl(best, li & 63);
+        wave_argmin_dpp(dm, li);                     // wave-uniform (dm, li)
+        const int i1 = __builtin_amdgcn_readlane(best, li & 63);
         if (lane == 0) {
             const cd xa = s_cons[li & 63], xb = s_cons[i1];
             cd* out = a.mom + (size_t)gsym * MS;

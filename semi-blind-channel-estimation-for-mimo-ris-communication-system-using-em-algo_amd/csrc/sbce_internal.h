@@ -139,6 +139,37 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
     v += dpp_d<0x140>(v);
     return (lane_d(v, 0) + lane_d(v, 16)) + (lane_d(v, 32) + lane_d(v, 48));
 }
+// First minimum of (d, i) over the wave (smallest d, ties to the smallest i), by the same
+// DPP / readlane steps; exact comparisons, so the result is that of any reduction order.
+template <int CTRL>
+__device__ __forceinline__ void argmin_step(double& d, int& i) {
+    const double od = dpp_d<CTRL>(d);
+    const int oi = __builtin_amdgcn_update_dpp(0, i, CTRL, 0xF, 0xF, false);
+    if (od < d || (od == d && oi < i)) { d = od; i = oi; }
+}
+__device__ __forceinline__ void wave_argmin_dpp(double& d, int& i) {
+    argmin_step<0xB1>(d, i);
+    argmin_step<0x4E>(d, i);
+    argmin_step<0x141>(d, i);
+    argmin_step<0x140>(d, i);
+    double bd = lane_d(d, 0);
+    int bi = __builtin_amdgcn_readlane(i, 0);
+#pragma unroll
+    for (int r = 16; r < 64; r += 16) {
+        const double od = lane_d(d, r);
+        const int oi = __builtin_amdgcn_readlane(i, r);
+        if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+    }
+    d = bd;
+    i = bi;
+}
+__device__ __forceinline__ double wave_min_dpp(double v) {
+    v = fmin(v, dpp_d<0xB1>(v));
+    v = fmin(v, dpp_d<0x4E>(v));
+    v = fmin(v, dpp_d<0x141>(v));
+    v = fmin(v, dpp_d<0x140>(v));
+    return fmin(fmin(lane_d(v, 0), lane_d(v, 16)), fmin(lane_d(v, 32), lane_d(v, 48)));
+}
 __device__ __forceinline__ double wave_max_dpp(double v) {
     v = fmax(v, dpp_d<0xB1>(v));
     v = fmax(v, dpp_d<0x4E>(v));
