@@ -662,6 +662,9 @@ __device__ __forceinline__ void estep_mfma_body(const EstepArgs& a, const MfmaCo
     constexpr int NPB = NB * (NB - 1) / 2;
     static_assert(NA >= 1 && NA <= 2 && NB <= 2, "mfma E-step: 2 <= n_tx <= 4");
 
+    // listed sweep: a block whose first wave has no list entry has no work at all (an empty
+    // list is common: the launch then costs only its dispatch)
+    if (a.list && (long)blockIdx.x * kMfmaWaves >= (long)a.list[(long)c.B * c.Td]) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     cd* s_cons = reinterpret_cast<cd*>(smem);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: SGPR addresses
@@ -1799,9 +1802,10 @@ __global__ __launch_bounds__(256) void estep_prep_kernel(EstepArgs a, PrepConst 
 // are in their prep records already).  Grid over all symbols; threads past the list exit.
 template <int NT, int NR>
 __global__ __launch_bounds__(256) void estep_bounds_kernel(EstepArgs a, PrepConst c) {
-    const cd* cons = stage_cons(a.cons, c.M);
     const long nsym = (long)c.B * c.Td;
     const long n = a.list[nsym];
+    if ((long)blockIdx.x * blockDim.x >= n) return;  // the whole block is past the list
+    const cd* cons = stage_cons(a.cons, c.M);
     const long gi = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gi >= n) return;
     const long gsym = a.list[gi];
@@ -2049,7 +2053,7 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
     __shared__ int s_n[2][4];
     __shared__ int s_b[2];
     const int wv = threadIdx.x >> 6;
-    const unsigned long long bf = __ballot(f2), be = __ballot(enumer);
+    const unsigned long long bf = __ballot(f2 && wide), be = __ballot(enumer || (f2 && !wide));
     if (lane == 0) {
         s_n[0][wv] = __builtin_popcountll(bf);
         s_n[1][wv] = __builtin_popcountll(be);
@@ -2063,18 +2067,17 @@ __global__ __launch_bounds__(256) void estep_tree_kernel(EstepArgs a, PrepConst 
     __syncthreads();
     const unsigned long long lt = (1ull << lane) - 1ull;
     if (f2 || enumer) {
-        const int l = f2 ? 0 : 1;
-        int base = s_b[l] + __builtin_popcountll((f2 ? bf : be) & lt);
+        // NT = 2 (pair mode): a symbol the factorised tables can represent (D within range; hard:
+        // f2d = 0, every unresolved symbol) goes to the pair list (counter 3), a narrow one to
+        // the enumeration list's slots (counter 2: no n_tx = 2 symbol is enumerated in pair mode,
+        // and the enumeration is not launched) for estep_soft2_kernel; otherwise the live
+        // unresolved symbols go to the enumeration list
+        const bool p0 = f2 && wide;
+        const int l = p0 ? 0 : 1;
+        int base = s_b[l] + __builtin_popcountll((p0 ? bf : be) & lt);
         for (int w = 0; w < wv; ++w) base += s_n[l][w];
-        // NT = 2 soft: a symbol the factorised pass can represent goes to its list (counter 3)
-        // (D within range -> the factorised tables; else the narrow-posterior path, flagged by
-        // the entry's sign bit; hard: f2d = 0, every unresolved symbol); the other live
-        // symbols go to the enumeration's list (counter 2)
-        if (f2)
-            a.list[2 * nsym + 2 * kEstepListCnt + base] =
-                wide ? (int32_t)gsym : (int32_t)((uint32_t)gsym | 0x80000000u);
-        else
-            cnt[kEstepListCnt + base] = (int32_t)gsym;
+        if (p0) a.list[2 * nsym + 2 * kEstepListCnt + base] = (int32_t)gsym;
+        else cnt[kEstepListCnt + base] = (int32_t)gsym;
     }
     if (c.count) {
         const unsigned long long one = __ballot(single);
@@ -2529,7 +2532,8 @@ hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStre
                 switch (pb.NT * 16 + pb.NR) {
 #define SBCE_SPH(nt, nr) case nt * 16 + nr: \
     hipLaunchKernelGGL((estep_tree_kernel<nt, nr>), pg, pblk, 0, s, as, pc); \
-    if (hard) hipLaunchKernelGGL((estep_bfs_kernel<nt, 2>), bg, bblk, 0, s, as, pc); \
+    if (nt == 2 && pc.pair) {} /* no enumeration: the pair passes take every listed symbol */ \
+    else if (hard) hipLaunchKernelGGL((estep_bfs_kernel<nt, 2>), bg, bblk, 0, s, as, pc); \
     else hipLaunchKernelGGL((estep_bfs_kernel<nt, 1>), bg, bblk, 0, s, as, pc); \
     e = hipGetLastError(); \
     break;

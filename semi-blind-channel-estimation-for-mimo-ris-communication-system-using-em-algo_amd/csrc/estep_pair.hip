@@ -387,9 +387,9 @@ __global__ __launch_bounds__(64 * kF2Waves) void estep_fact2_kernel(EstepArgs a,
     // symbols by a static stride (every symbol costs the same: no work grabbing), the next one's
     // index, channel and observation loaded while the current one is computed
     auto fetch = [&](int k, long& gs, cd (&hh)[2 * NR], cd (&yy)[NR]) {
-        gs = k < nwork ? (long)plist[k] : 0;         // (a negative entry: soft2, see below)
+        gs = k < nwork ? (long)plist[k] : 0;
         if (k < nwork) {
-            const long g0 = gs & 0x7fffffffL;
+            const long g0 = gs;
             const double* rec = a.prep + (size_t)g0 * c.stride;
 #pragma unroll
             for (int e = 0; e < 2 * NR; ++e) hh[e] = cmk(rec[4 + 2 * e], rec[5 + 2 * e]);
@@ -401,8 +401,7 @@ __global__ __launch_bounds__(64 * kF2Waves) void estep_fact2_kernel(EstepArgs a,
     cd hnext[2 * NR], ynext[NR];
     fetch(gi, gnext, hnext, ynext);
     for (; gi < nwork; gi += nwaves) {
-        const bool soft2 = gnext < 0;                // sign bit: a symbol whose range D is too wide
-        const long gsym = gnext & 0x7fffffffL;
+        const long gsym = gnext;
         cd hc[2 * NR], yc[NR];
 #pragma unroll
         for (int e = 0; e < 2 * NR; ++e) hc[e] = hnext[e];
@@ -418,7 +417,6 @@ __global__ __launch_bounds__(64 * kF2Waves) void estep_fact2_kernel(EstepArgs a,
             continue;
         }
         const double is2 = a.varn_t ? uniform_d(trial_noise(a.varn_t[b]).inv_s2) : c.inv_s2;
-        if (soft2) continue;                         // estep_soft2_kernel's
         cd z0 = czero(), z1 = czero(), g = czero();
         double g00 = 0.0, g11 = 0.0;
 #pragma unroll
@@ -517,8 +515,8 @@ __global__ __launch_bounds__(64 * kF2Waves) void estep_fact2_kernel(EstepArgs a,
 }
 
 
-// Narrow posteriors of n_tx = 2 (the tree pass's entries with the sign bit: range D above the
-// factorised tables' limit): lane = x_0, r = y - h_0 x_0; d(x_1) = g_11 |x_1 - z|^2 + (||r||^2 -
+// Narrow posteriors of n_tx = 2 (the tree pass's narrow list: range D above the factorised
+// tables' limit): lane = x_0, r = y - h_0 x_0; d(x_1) = g_11 |x_1 - z|^2 + (||r||^2 -
 // g_11 |z|^2), z = h_1^H r / g_11, so the lane's best x_1 is the per-axis nearest level pair (taken
 // when both per-axis rivals are farther by more than the distances' rounding, else every point is
 // scanned), d_min the wave minimum, and the x_1 within thr = 50 varn^2 of d_min (the sweep's e^-50
@@ -538,8 +536,9 @@ __global__ __launch_bounds__(64 * kF2Waves) void estep_soft2_kernel(EstepArgs a,
     const int lane = threadIdx.x & 63;
     const long nsym = (long)c.B * c.Td;
     int32_t* cnt = a.list + nsym;
-    const int32_t* plist = a.list + 2 * nsym + 2 * kEstepListCnt;
-    const int nwork = __builtin_amdgcn_readfirstlane(cnt[3]);
+    // the tree pass's narrow symbols: the enumeration list's slots (counter 2, estep_tree_kernel)
+    const int32_t* plist = cnt + kEstepListCnt;
+    const int nwork = __builtin_amdgcn_readfirstlane(cnt[2]);
     const int nwaves = gridDim.x * kF2Waves;
     int32_t* s_f = s_fail[wave];
     int nf = 0;
@@ -561,9 +560,7 @@ __global__ __launch_bounds__(64 * kF2Waves) void estep_soft2_kernel(EstepArgs a,
         lim[k] = k < K ? s_grid.lim[k] : INFINITY;
     }
     for (int gi = blockIdx.x * kF2Waves + wave; gi < nwork; gi += nwaves) {
-        const int32_t ent = plist[gi];
-        if (ent >= 0) continue;                      // the factorised tables' symbol
-        const long gsym = (long)(ent & 0x7fffffff);
+        const long gsym = plist[gi];
         const int b = (int)(gsym / c.Td);
         if (a.done && a.done[b]) continue;
         if (K == 0) {                                // not a square grid: the sweep weighs it
