@@ -17,7 +17,7 @@ DebugConfig g_debug;
 
 namespace {
 constexpr DebugConfig kDebugDefault = {false, false, false, false, false, 128, false, false, false,
-                                       true, false, false, 0, false};
+                                       true, false, false, 0, 0};
 constexpr int kSphereBudgetMax = 256;      // estep.hip kBfsPmax
 
 void read_debug_env(DebugConfig& c) {
@@ -38,7 +38,7 @@ void read_debug_env(DebugConfig& c) {
     if ((v = env("SBCE_ESTEP_PAIR"))) c.estep_nopair = v[0] == '0';
     if ((v = env("SBCE_CPLX3"))) c.cplx3 = v[0] != '0';
     if ((v = env("SBCE_MSTEP_SMALL"))) { c.mstep_nosmall = v[0] == '0'; c.small_valu = v[0] == 'v'; }
-    if ((v = env("SBCE_PM_IMPL"))) c.pm_wave = v[0] == 'w';
+    if ((v = env("SBCE_PM_IMPL"))) c.pm_impl = (v[0] == 'w' || v[0] == 't' || v[0] == 'q') ? v[0] : 0;
     if ((v = env("SBCE_SMALL_STOP"))) c.small_stop = (v[0] >= '1' && v[0] <= '3') ? v[0] - '0' : 0;
 }
 

@@ -700,10 +700,213 @@ __global__ __launch_bounds__(64) void estep_pm_thread_kernel(EstepArgs a, PmCons
     out[5] = S11;
 }
 
+// FOUR threads per symbol (a quad; 16 symbols per 64-thread block): thread t takes the candidates
+// l = t (mod 4) through the nearest-point and exponential passes -- in the weight sum's tree those
+// are one 16-leaf subtree each (l's low two bits are the butterfly's last two levels), so the quad
+// finishes the tree by two shuffles with the same operands -- and the moment sums, each still over
+// the candidates in order, are split by moment over the quad (m, S_0., S_1.).  4x the waves of one
+// thread per symbol: the passes' exp / nearest-point chains were latency-bound at ~2 waves/SIMD.
+constexpr int kPmQuadSym = 16;          // symbols per 64-thread block
+template <int MODE, int NR>
+__global__ __launch_bounds__(64) void estep_pm_quad_kernel(EstepArgs a, PmConst c) {
+    static_assert(MODE == 2 || MODE == 3, "PM / PM-soft");
+    constexpr int NT = 2, NO = NT * NR;
+    __shared__ cd s_cons[64];
+    __shared__ GridLds s_grid;
+    __shared__ uint8_t s_sb[64 * kPmQuadSym];      // [candidate][symbol]: b's index
+    __shared__ double s_w[64 * kPmQuadSym];        // [candidate][symbol]: exp(-(d - d_min) / s2)
+    if ((int)threadIdx.x < c.M) s_cons[threadIdx.x] = a.cons[threadIdx.x];
+    __syncthreads();
+    grid_build(s_cons, c.M, &s_grid);
+    const GridReg greg = grid_load(s_grid);
+    const long nsym = (long)c.B * c.Td;
+    const int qs = threadIdx.x >> 2, tq = threadIdx.x & 3;   // the quad's symbol, thread in quad
+    const long gsym = (long)blockIdx.x * kPmQuadSym + qs;
+    if (gsym >= nsym) return;                      // quad-uniform
+    const int b = (int)(gsym / c.Td);
+    if (a.done && a.done[b]) return;
+    double inv_s2 = c.inv_s2;
+    if (a.varn_t) inv_s2 = trial_noise(a.varn_t[b]).inv_s2;   // per-trial noise variance (ABI 6)
+    const int P = c.P, JA = c.JA;
+
+    // ---- 1. H_true, H_off, y ----
+    cd Ht[NO], Ho[NO];
+    {
+        const cd* th = a.theta + (size_t)b * P * NO;
+        const cd* ps = a.psid + (size_t)gsym * P;
+#pragma unroll
+        for (int o = 0; o < NO; ++o) { Ht[o] = czero(); Ho[o] = th[o]; }
+        for (int p = 0; p < P; ++p) {
+            const cd psi = ps[p];
+#pragma unroll
+            for (int o = 0; o < NO; ++o) {
+                Ht[o] = cfma(Ht[o], psi, th[p * NO + o]);
+                if (p + 1 < P) Ho[o] = cfma(Ho[o], psi, th[(p + 1) * NO + o]);
+            }
+        }
+    }
+    cd yv[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) yv[r] = a.yd[(size_t)gsym * NR + r];
+
+    // ---- 2. greedy order: drop the stream with the largest diag((H^H H)^-1) first ----
+    int kmax = 0;
+    {
+        cd G[NT][NT], I[NT][NT];
+#pragma unroll
+        for (int u = 0; u < NT; ++u)
+#pragma unroll
+            for (int v = 0; v < NT; ++v) {
+                cd acc = czero();
+#pragma unroll
+                for (int r = 0; r < NR; ++r) acc = cfmac(acc, Ho[v * NR + r], Ho[u * NR + r]);
+                G[u][v] = acc;
+                I[u][v] = (u == v) ? cmk(1.0, 0.0) : czero();
+            }
+#pragma unroll
+        for (int cc = 0; cc < NT; ++cc) {
+            const cd piv = G[cc][cc];
+            const double den = cabs2(piv);
+            const cd inv = cmk(piv.x / den, -piv.y / den);
+            cd rg[NT], ri[NT], fi[NT];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) { rg[j] = G[cc][j]; ri[j] = I[cc][j]; }
+#pragma unroll
+            for (int i = 0; i < NT; ++i) fi[i] = G[i][cc];
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    const cd rsg = cmul(rg[j], inv), rsi = cmul(ri[j], inv);
+                    G[i][j] = (i == cc) ? rsg : csub(G[i][j], cmul(fi[i], rsg));
+                    I[i][j] = (i == cc) ? rsi : csub(I[i][j], cmul(fi[i], rsi));
+                }
+        }
+        // np.argmax over the complex diagonal: lexicographic (real, imag), first maximum
+        const cd v0 = I[0][0], v1 = I[1][1];
+        if (v1.x > v0.x || (v1.x == v0.x && v1.y > v0.y)) kmax = 1;
+    }
+    const int oa = kmax, ob = 1 - kmax;              // A = {ord[0]}, B = {ord[1]}
+
+    // ---- 3. G_B = (B^H B)^{-1} B^H (1 x NR), G_B y, G_B A ----
+    cd Gy = czero(), GA = czero();
+    {
+        cd HA[NR], HB[NR];                           // columns A, B of H_off (no dynamic indexing)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            HA[r] = csel(oa != 0, Ho[NR + r], Ho[r]);
+            HB[r] = csel(ob != 0, Ho[NR + r], Ho[r]);
+        }
+        cd g = czero();
+#pragma unroll
+        for (int r = 0; r < NR; ++r) g = cfmac(g, HB[r], HB[r]);
+        const double den = cabs2(g);
+        const cd inv = cmk(g.x / den, -g.y / den);
+        const cd gi = cmul(cmk(1.0, 0.0), inv);      // gj_inverse on the 1 x 1 [g | 1]
+        cd GB[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) GB[r] = cfma(czero(), gi, cconj(HB[r]));
+#pragma unroll
+        for (int r = 0; r < NR; ++r) Gy = cfma(Gy, GB[r], yv[r]);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) GA = cfma(GA, GB[r], HA[r]);
+    }
+
+    // ---- 4./5. candidates: x = [a, b] in concatenated order, distances ----
+    // three passes over the candidates (no per-candidate register arrays): b's index kept in LDS,
+    // the distance recomputed (the same operations, so the same value) where it is needed
+    uint8_t* sb_col = s_sb + qs;                       // [64 candidates][16 symbols]
+    double* w_col = s_w + qs;
+    auto dist = [&](cd x0, cd x1) {
+        double dd = 0.0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            cd res = yv[r];
+            res = csub(res, cmul(Ht[0 * NR + r], x0));
+            res = csub(res, cmul(Ht[1 * NR + r], x1));
+            dd += cabs2(res);
+        }
+        return dd;
+    };
+    double dm = INFINITY;
+    for (int i = tq; i < JA; i += 4) {
+        const cd x0 = s_cons[i];
+        cd z = Gy;
+        z = csub(z, cmul(GA, x0));
+        double db;
+        const int sb = nearest_point(greg, s_grid, s_cons, c.M, z, db);
+        sb_col[i * kPmQuadSym] = (uint8_t)sb;
+        if (MODE == 3) dm = fmin(dm, dist(x0, s_cons[sb]));
+    }
+    if (MODE == 3) {                                   // the quad's minimum (exact)
+        dm = fmin(dm, shfl_xor_d(dm, 1));
+        dm = fmin(dm, shfl_xor_d(dm, 2));
+    }
+    // weights: 1 (PM) or softmax(-d / varn^2); the wave kernel's 64-lane xor-butterfly sum is the
+    // pairwise tree over the candidates in bit-reversed order (lanes l, l + 32 first), summed here
+    // by a binary counter over six levels
+    double zs = 1.0;
+    if (MODE == 3) {
+        // thread tq sums the 16 consecutive k = 16 r + kk (r = bitrev2(tq): k's bits 5, 4 are l's
+        // bits 0, 1) by the counter's first four levels; levels 5 and 6 pair r = (0, 1), (2, 3),
+        // then the two halves: the quad's xor-2 and xor-1 partners
+        const int r = ((tq & 1) << 1) | (tq >> 1);
+        double st[4];
+#pragma unroll
+        for (int lev = 0; lev < 4; ++lev) st[lev] = 0.0;
+        double br = 0.0;
+        for (int kk = 0; kk < 16; ++kk) {
+            const int k = 16 * r + kk;
+            const int l = (int)(__builtin_bitreverse32((uint32_t)k) >> 26);
+            double v = 0.0;
+            if (l < JA) {
+                v = exp(-(dist(s_cons[l], s_cons[sb_col[l * kPmQuadSym]]) - dm) * inv_s2);
+                w_col[l * kPmQuadSym] = v;
+            }
+            bool carry = true;
+#pragma unroll
+            for (int lev = 0; lev < 4; ++lev) {
+                if (carry) {
+                    if ((kk >> lev) & 1) v = st[lev] + v;
+                    else { st[lev] = v; carry = false; }
+                }
+            }
+            if (kk == 15) br = v;
+        }
+        const double h2 = br + shfl_xor_d(br, 2);        // B_0 + B_1 / B_2 + B_3 (commutative)
+        zs = h2 + shfl_xor_d(h2, 1);
+    }
+
+    wave_sync();                                       // the quad's b indices and weights
+    // ---- 6. moments, candidates in order; thread tq of the quad forms outputs 2 tq, 2 tq + 1:
+    //      (m_0, m_1), (S_00, S_01), (S_10, S_11) as x_a conj(x_b) with x_b = 1 for the means ----
+    const cd one = cmk(1.0, 0.0);
+    cd acc1 = czero(), acc2 = czero();
+    for (int i = 0; i < JA; ++i) {
+        const cd x0 = s_cons[i];
+        const cd x1 = s_cons[sb_col[i * kPmQuadSym]];
+        double w = 1.0;
+        if (MODE == 3) w = w_col[i * kPmQuadSym] / zs;
+        const cd a1 = tq == 2 ? x1 : x0, b1 = tq == 0 ? one : x0;
+        const cd a2 = tq == 1 ? x0 : x1, b2 = tq == 0 ? one : x1;
+        acc1 = caxpy(acc1, w, tq == 0 ? x0 : cmulc(a1, b1));
+        acc2 = caxpy(acc2, w, tq == 0 ? x1 : cmulc(a2, b2));
+    }
+    if (tq < 3) {
+        cd* out = a.mom + (size_t)gsym * (NT + NT * NT);
+        out[2 * tq] = acc1;
+        out[2 * tq + 1] = acc2;
+    }
+}
+
 template <int MODE>
-hipError_t launch_pm_thread_nr(int NR, dim3 g, hipStream_t s, const EstepArgs& a, const PmConst& c) {
+hipError_t launch_pm_thread_nr(int NR, dim3 g, hipStream_t s, const EstepArgs& a, const PmConst& c,
+                               bool quad) {
     switch (NR) {
-#define SBCE_PT(n) case n: hipLaunchKernelGGL((estep_pm_thread_kernel<MODE, n>), g, dim3(64), 0, s, a, c); break;
+#define SBCE_PT(n) case n: \
+    if (quad) hipLaunchKernelGGL((estep_pm_quad_kernel<MODE, n>), g, dim3(64), 0, s, a, c); \
+    else hipLaunchKernelGGL((estep_pm_thread_kernel<MODE, n>), g, dim3(64), 0, s, a, c); \
+    break;
         SBCE_PT(1) SBCE_PT(2) SBCE_PT(3) SBCE_PT(4) SBCE_PT(5) SBCE_PT(6) SBCE_PT(7) SBCE_PT(8)
 #undef SBCE_PT
         default: return hipErrorInvalidValue;
@@ -753,7 +956,7 @@ hipError_t launch_estep_pm(const Problem& pb, const EstepArgs& a, int mode, int 
     c.s2 = pb.varn * pb.varn;
     c.vx = pb.varx * pb.varx;
     const long nsym = (long)pb.B * pb.Td;
-    if ((mode == SBCE_ESTEP_ZF || mode == SBCE_ESTEP_MMSE) && pb.NT <= 2 && !g_debug.pm_wave) {
+    if ((mode == SBCE_ESTEP_ZF || mode == SBCE_ESTEP_MMSE) && pb.NT <= 2 && g_debug.pm_impl != 'w') {
         // thread per symbol (BASELINE cfg 5: 2 x 2); bitwise the wave kernel's results
         const long tb = (nsym + 63) / 64;
         if (tb == 0) return hipSuccess;
@@ -765,13 +968,18 @@ hipError_t launch_estep_pm(const Problem& pb, const EstepArgs& a, int mode, int 
                                      : launch_det_thread_nr<2, 5>(pb.NR, g, s, a, c);
     }
     if ((mode == SBCE_ESTEP_PM || mode == SBCE_ESTEP_PM_SOFT) && pb.NT == 2 && c.NA == 1 &&
-        !g_debug.pm_wave) {
-        // thread per symbol, one-stream list (BASELINE cfg 5: 2 x 2, r = 1, 64-QAM)
-        const long tb = (nsym + 63) / 64;
+        g_debug.pm_impl != 'w') {
+        // one-stream list (BASELINE cfg 5: 2 x 2, r = 1, 64-QAM): a quad per symbol while one
+        // thread per symbol would leave fewer than ~1.5 waves per SIMD (cfg5 T_d = 15: 57 vs 122
+        // us), else one thread per symbol (T_d = 120: 205 vs 224 us: the quad repeats the setup
+        // and the moment loop per thread); both bitwise the wave kernel's.  SBCE_PM_IMPL=t / q
+        // forces one.
+        const bool quad = g_debug.pm_impl == 'q' || (g_debug.pm_impl != 't' && nsym < 96 * 1024);
+        const long tb = quad ? (nsym + kPmQuadSym - 1) / kPmQuadSym : (nsym + 63) / 64;
         if (tb == 0) return hipSuccess;
         const dim3 g((unsigned)tb);
-        return mode == SBCE_ESTEP_PM ? launch_pm_thread_nr<2>(pb.NR, g, s, a, c)
-                                     : launch_pm_thread_nr<3>(pb.NR, g, s, a, c);
+        return mode == SBCE_ESTEP_PM ? launch_pm_thread_nr<2>(pb.NR, g, s, a, c, quad)
+                                     : launch_pm_thread_nr<3>(pb.NR, g, s, a, c, quad);
     }
     const size_t lds = (64 + (size_t)kPmWaves * PmLds::TOTAL) * sizeof(cd);
     const long blocks = (nsym + kPmWaves - 1) / kPmWaves;

@@ -239,9 +239,10 @@ struct DebugConfig {
     int small_stop;      // SBCE_SMALL_STOP=1|2|3  DIAGNOSTIC: the one-workgroup M-step stops after its
                          //                        build (1) / factorisation (2) / symbol staging
                          //                        without the build's arithmetic (3); results invalid
-    bool pm_wave;        // SBCE_PM_IMPL=wave      ZF/MMSE (n_tx <= 2) and PM (n_tx = 2, |A| = 1) E-steps
-                         //                        one wave per symbol too
-                         //                        (bitwise the thread kernel's results; not flagged)
+    char pm_impl;        // SBCE_PM_IMPL=wave      ZF/MMSE (n_tx <= 2) and PM (n_tx = 2, |A| = 1) E-steps
+                         //                        one wave per symbol too; =t / =q the PM one thread /
+                         //                        one quad per symbol at any size (all bitwise the
+                         //                        same results; not flagged)
 };
 extern DebugConfig g_debug;
 bool debug_nondefault();   // a result-affecting switch differs from its default

@@ -643,20 +643,23 @@ def test_detector_estep_vs_oracle(sbce, shape):
                                    (2, 8, 3, 12, 50, 64, 20), (2, 3, 2, 8, 17, 4, 40)])
 def test_pm_thread_kernel_bitwise_wave_kernel(sbce, shape):
     """PM / PM-soft at n_tx = 2 with a one-stream list (partition_r = 1 < log2 M, BASELINE cfg 5)
-    run one thread per symbol; the one-wave-per-symbol kernel (SBCE_PM_IMPL=wave) gives bitwise
-    the same m and S (greedy order, G_B, nearest points, butterfly weight sum, moment order)."""
+    run one thread or one quad of threads per symbol (by size; SBCE_PM_IMPL=t / q force one); the
+    one-wave-per-symbol kernel (SBCE_PM_IMPL=wave) gives bitwise the same m and S (greedy order,
+    G_B, nearest points, butterfly weight sum, moment order) as both."""
     n_tx, n_rx, N, T_p, T_d, M, snr = shape
     varn = float(sbce.signal_model.snr_to_varn(snr))
     b = sbce.signal_model.synthetic_batch(3, n_tx, n_rx, N, T_p, T_d, M, varn, seed=47)
     for kind in ("pm", "pm_soft"):
-        m, S = sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx, kind,
-                                partition_r=1)
         with sbce._lib.debug_env(SBCE_PM_IMPL="wave"):
             mw, Sw = sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx,
                                       kind, partition_r=1)
-        assert np.array_equal(m, mw, equal_nan=True), kind
-        assert np.array_equal(S, Sw, equal_nan=True), kind
-        assert np.isfinite(m).all(), kind
+        for arm in ("", "t", "q"):
+            with sbce._lib.debug_env(SBCE_PM_IMPL=arm):
+                m, S = sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], b["theta0"], varn, n_tx,
+                                        kind, partition_r=1)
+            assert np.array_equal(m, mw, equal_nan=True), (kind, arm)
+            assert np.array_equal(S, Sw, equal_nan=True), (kind, arm)
+            assert np.isfinite(m).all(), (kind, arm)
 
 
 @pytest.mark.parametrize("shape", [(2, 2, 15, 20, 120, 64, -5), (2, 2, 15, 20, 60, 64, 33),
