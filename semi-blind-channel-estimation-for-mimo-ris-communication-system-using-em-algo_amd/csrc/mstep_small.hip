@@ -348,8 +348,12 @@ __device__ __forceinline__ void mstep_small_body(const MstepArgs& a, int NT, int
             const double dia = col[c].x;
             const bool bad = !(dia > tol);
             const bool drop = bad && !chol;
-            const double piv = sqrt(bad ? tol : dia);
-            const double inv = drop ? 0.0 : 1.0 / piv;
+            // pivot and its inverse as the batched panel factor forms them (v_rsq_f64 seed, two
+            // Newton steps: ~5 dependent ops on the column chain instead of sqrt + division)
+            const double pv = bad ? tol : dia;
+            const double rs = fast_rsqrt64(pv);
+            const double piv = pv * rs;
+            const double inv = drop ? 0.0 : rs;
             anybad |= bad;
             if (tid == 0) dinv[c] = inv;
             if (tj == cl) {
