@@ -87,9 +87,15 @@ extern "C" {
 /* M-step solve modes (SURVEY.md §7 hard part 3) */
 #define SBCE_SOLVE_CHOL 0       /* Hermitian Cholesky of the reduced L x L system
                                    (== LU of the K x K reference system,
-                                   Proposed_method_NMSEvsTp.py:80, on HPD R) */
-#define SBCE_SOLVE_CHOL_DROP 1  /* non-HPD pivots (<= 1e-14 max diag R) dropped: a basic
-                                   solution on the kept coordinates, NOT minimum-norm */
+                                   Proposed_method_NMSEvsTp.py:80, on HPD R).  A pivot
+                                   <= 1e-14 max diag R (R not numerically HPD: rank-deficient
+                                   when T_p + n_tx T_d < L) sets SBCE_STATUS_NONHPD and its
+                                   direction is dropped: theta stays finite, solves the normal
+                                   equations, and its range-space part is lstsq's minimum-norm
+                                   solution (the reference's LU returns rounding noise there) */
+#define SBCE_SOLVE_CHOL_DROP 1  /* the same solve (kept for ABI 1-6 callers): non-HPD pivots
+                                   dropped, a basic solution on the kept coordinates, NOT
+                                   minimum-norm */
 #define SBCE_SOLVE_MINNORM 2    /* minimum-norm least squares, np.linalg.lstsq of PM.py:108
                                    (the intended fallback of all_detectorsvsTd.py:238-241):
                                    R's rank is cut at eps*K*lambda_max(R) (lstsq's default

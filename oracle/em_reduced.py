@@ -136,6 +136,52 @@ def mstep_solve(R, rhs):
     return np.conj(X).reshape(-1)
 
 
+def mstep_chol_policy(R, rhs, clamp=False, rel_tol=1e-14):
+    """The device's CHOL solve policy for a non-HPD R, restated unblocked (right-looking):
+    the np.linalg.solve of PMd/Proposed_method_NMSEvsTp.py:80 on an HPD R; a pivot
+    <= rel_tol * max diag R is flagged and its direction DROPPED (column zeroed, its y and x
+    components 0) -- libsbce since round 6, include/sbce.h SBCE_SOLVE_CHOL.
+    clamp=True restates the round-5 policy instead (the pivot raised to sqrt(tol), the column
+    kept), which overflows on a rank-deficient R: past the numerical rank the Schur complement
+    is rounding noise delta, not PSD, and each clamped column feeds delta^2 / tol back.
+    Returns (theta, bad) with bad the flagged pivots."""
+    A = np.array(R, dtype=complex)
+    L = A.shape[0]
+    tol = rel_tol * np.max(A.diagonal().real)
+    bad = np.zeros(L, dtype=bool)
+    with np.errstate(all="ignore"):
+        for c in range(L):
+            d = A[c, c].real
+            bad[c] = not d > tol
+            if bad[c] and not clamp:
+                A[c:, c] = 0.0
+                continue
+            piv = np.sqrt(tol if bad[c] else d)
+            A[c, c] = piv
+            col = A[c + 1:, c] / piv
+            A[c + 1:, c] = col
+            A[c + 1:, c + 1:] -= np.outer(col, col.conj())
+        Lf = np.tril(A)
+        y = np.array(rhs, dtype=complex)
+        for c in range(L):
+            y[c] = 0.0 if Lf[c, c] == 0 else (y[c] - Lf[c, :c] @ y[:c]) / Lf[c, c]
+        x = np.zeros_like(y)
+        for c in range(L - 1, -1, -1):
+            x[c] = 0.0 if Lf[c, c] == 0 else (y[c] - Lf[c + 1:, c].conj() @ x[c + 1:]) / Lf[c, c]
+    return np.conj(x).reshape(-1), bad
+
+
+def range_part(R, theta, n_rx):
+    """theta's component on R's numerical range (lstsq's cut eps * K * lambda_max on R's
+    eigenvalues, K = L n_rx): for any solution of a consistent R X = B^H it is the
+    minimum-norm solution, the size-independent check of a rank-deficient solve."""
+    w, V = np.linalg.eigh(R)
+    keep = w > np.finfo(float).eps * R.shape[0] * n_rx * w.max()
+    Vr = V[:, keep]
+    X = np.conj(np.asarray(theta).reshape(R.shape[0], n_rx))
+    return np.conj(Vr @ (Vr.conj().T @ X)).reshape(-1)
+
+
 def em_reduced(Y_d, Y_p, U_p, Psi, aps, varn, itera, theta0, mode="soft",
                return_trace=False, h=None):
     """Reduced-form EM over one trial.  Inputs in array form:

@@ -17,7 +17,7 @@ DebugConfig g_debug;
 
 namespace {
 constexpr DebugConfig kDebugDefault = {false, false, false, false, false, 128, false, false, false,
-                                       true, false, false, 0, 0};
+                                       true, false, false, false, false, 0, 0};
 constexpr int kSphereBudgetMax = 256;      // estep.hip kBfsPmax
 
 void read_debug_env(DebugConfig& c) {
@@ -37,7 +37,12 @@ void read_debug_env(DebugConfig& c) {
     if ((v = env("SBCE_CHOL_IMPL"))) c.chol_valu = v[0] == 'v';
     if ((v = env("SBCE_ESTEP_PAIR"))) c.estep_nopair = v[0] == '0';
     if ((v = env("SBCE_CPLX3"))) c.cplx3 = v[0] != '0';
-    if ((v = env("SBCE_MSTEP_SMALL"))) { c.mstep_nosmall = v[0] == '0'; c.small_valu = v[0] == 'v'; }
+    if ((v = env("SBCE_MSTEP_SMALL"))) {
+        c.mstep_nosmall = v[0] == '0';
+        c.small_valu = v[0] == 'v';
+        c.small_v1 = v[0] == '1';
+    }
+    if ((v = env("SBCE_SMALL2_LDS"))) c.small2_lds = v[0] == '1';
     if ((v = env("SBCE_PM_IMPL"))) c.pm_impl = (v[0] == 'w' || v[0] == 't' || v[0] == 'q') ? v[0] : 0;
     if ((v = env("SBCE_SMALL_STOP"))) c.small_stop = (v[0] >= '1' && v[0] <= '3') ? v[0] - '0' : 0;
 }
@@ -54,7 +59,7 @@ bool debug_nondefault() {
            c.backsub_general != d.backsub_general || c.chol_valu != d.chol_valu ||
            c.estep_nopair != d.estep_nopair || c.cplx3 != d.cplx3 ||
            c.mstep_nosmall != d.mstep_nosmall || c.small_stop != d.small_stop ||
-           c.small_valu != d.small_valu ||
+           c.small_valu != d.small_valu || c.small_v1 != d.small_v1 ||
            (chol_debug_skip_mask() & 31);
 }
 
@@ -276,6 +281,8 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     if (prefactor && (rc = hip_rc(launch_pilot_factor(pb, ma, s)))) return rc;
     // L <= 64: the whole M-step in one launch (BASELINE cfg 5: L = 32)
     const bool small = mstep_small_supported(pb, solve_mode) && !(gauss && pb.NR == 1);
+    // the LLF kernel reads theta before the stop decision of the same iteration: no fold with it
+    const bool fold_stop = small && early && !p->llf && mstep_small2_selected(pb);
     for (int it = 0; it < iters; ++it) {
         if (p->x_sup) {
             if ((rc = hip_rc(launch_sup_shift_y(pb, ea.yd, ea.psid, ea.theta, (const cd*)p->x_sup,
@@ -288,7 +295,14 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
             if ((rc = hip_rc(launch_estep(pb, ea, estep_mode, s)))) return rc;
         }
         if (small) {
-            if ((rc = hip_rc(launch_mstep_small(pb, ma, false, s)))) return rc;
+            MstepArgs ms = ma;
+            if (fold_stop) {                 // the oracle early stop rides in the M-step launch
+                ms.h_true = (const cd*)p->h_true;
+                ms.done_w = done;
+                ms.iters_done = p->iters_done;
+                ms.it = it;
+            }
+            if ((rc = hip_rc(launch_mstep_small(pb, ms, false, s)))) return rc;
         } else {
             if ((rc = hip_rc(launch_mstep_build(pb, ma, s, prefactor)))) return rc;
             // Gaussian prior, n_rx = 1: the reference's all-ones covariance term stays in A
@@ -301,7 +315,7 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
                                     (const cd*)p->x_d_true, p->llf, iters, it, ea.done, p->varn_t,
                                     s))))
             return rc;
-        if (early &&
+        if (early && !fold_stop &&
             (rc = hip_rc(launch_early_stop(pb, ma.theta, (const cd*)p->h_true, done, p->iters_done,
                                            it, s))))
             return rc;

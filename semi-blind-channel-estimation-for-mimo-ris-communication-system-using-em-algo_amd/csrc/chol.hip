@@ -22,8 +22,14 @@
 // row r) with wave-level syncs only; its inverse D^{-1} (lower) drives the TRSM
 // and both triangular block solves (conj(D^{-1}) is kept in R's unused strict
 // upper diagonal block for the back substitution).
-// Pivots <= 1e-14 * max(diag R) are flagged (status bit 0); solve_mode DROP
-// zeroes that direction, CHOL clamps the pivot to the tolerance.
+// Pivots <= 1e-14 * max(diag R) are flagged (status bit 0) and their direction is dropped
+// (column zeroed, y and x components 0) in every public solve mode.  A clamp (pivot raised to
+// sqrt(tol), the column kept) is unstable on a rank-deficient R: past the numerical rank the
+// Schur complement is rounding noise, not PSD, so a column of noise delta divided by sqrt(tol)
+// feeds back delta^2 / tol into the next pivots and overflows within ~10 columns (round 5's
+// all-NaN theta at L = 600; oracle.em_reduced.mstep_chol_policy(clamp=True) shows it on the CPU).
+// Dropped, the solution's range-space part is lstsq's minimum-norm solution (to ~1e-13).  Only
+// the min-norm solve's C = G^H G (HPD by construction) clamps (kSolveClampHpd).
 #include <stdlib.h>
 
 #include "sbce_internal.h"
@@ -52,7 +58,7 @@ __device__ __forceinline__ void factor_diag(cd* dr, int w, int lane, double tol,
             wave_sync();
             const double dia = colbuf[NB].x;
             const bool bad = !(dia > tol);
-            const bool drop = bad && solve_mode != SBCE_SOLVE_CHOL;
+            const bool drop = bad && solve_mode != kSolveClampHpd;
             const double piv = sqrt(bad ? tol : dia);
             const double inv = drop ? 0.0 : 1.0 / piv;
             if (lane == 0) { dinv[c] = inv; if (bad) *flag |= 1; }
@@ -398,7 +404,7 @@ __device__ __forceinline__ void factor_diag_lds(cd* A, int w, int lane, double t
         // min-norm solve (tol = 32 x lstsq's cut, minnorm.hip): a pivot between 4 cut and
         // 64 tol may be decided differently from the singular values lstsq thresholds
         near_any |= solve_mode == SBCE_SOLVE_MINNORM && dia > tol * (1.0 / 8) && dia < tol * 64;
-        const bool drop = bad && solve_mode != SBCE_SOLVE_CHOL;
+        const bool drop = bad && solve_mode != kSolveClampHpd;
         const double pv = bad ? tol : dia;
         const double rs = fast_rsqrt64(pv);
         const double piv = drop ? 0.0 : pv * rs;
@@ -1411,7 +1417,7 @@ hipError_t launch_chol_batched(const Problem& pb, const MstepArgs& a, hipStream_
     // the wide schedule: even panels j >= 2 update panels j and j+1 by [0, jb) in one launch
     // (panel_update2_kernel), odd panels are pre-updated by panel j-1 inside their factor launch:
     // half the left-looking HBM re-reads of one update launch per panel
-    const bool g3 = g_debug.cplx3 && a.solve_mode == SBCE_SOLVE_CHOL;
+    const bool g3 = g_debug.cplx3 && (a.solve_mode == SBCE_SOLVE_CHOL || a.solve_mode == kSolveClampHpd);
     for (int j = 0; j < npan; ++j) {
         const int jb = j * PW;
         const int rem = (pb.L - jb + NB - 1) / NB;

@@ -633,7 +633,7 @@ hipError_t launch_minnorm(const Problem& pb, const MstepArgs& a, hipStream_t s) 
     MstepArgs c = a;
     c.R = a.gram; c.rhs = a.grhs; c.theta = nullptr; c.tol = a.tol2;
     c.clamp_status = SBCE_STATUS_RANK;     // a clamped pivot of C: flagged, the refinement below runs
-    c.solve_mode = SBCE_SOLVE_CHOL;
+    c.solve_mode = kSolveClampHpd;        // C is HPD: its rare tiny pivot is clamped, not dropped
     const TileExt exC{a.act, a.act, 1};
     if ((e = launch_tile_factor(pb, c, exC, nullptr, s)) != hipSuccess) return e;
     if ((e = launch_tile_back(pb, c, a.act, s)) != hipSuccess) return e;

@@ -814,7 +814,7 @@ static hipError_t launch_herk(const Problem& pb, const MstepArgs& a, int kb_lo, 
     if (ntiles <= 0) return hipSuccess;
     const long nblk = 8L * ((pb.B + 7) / 8) * ntiles;
     if (nblk > 0x7fffffffL) return hipErrorInvalidValue;
-    if (g_debug.cplx3 && a.solve_mode == SBCE_SOLVE_CHOL)
+    if (g_debug.cplx3 && (a.solve_mode == SBCE_SOLVE_CHOL || a.solve_mode == kSolveClampHpd))
         hipLaunchKernelGGL(tile_herk_kernel<true>, dim3((unsigned)nblk), dim3(256), 0, s, a, pb.L, kb_lo,
                            nkb, tj_lo, tj_hi, (int)ntiles, ex);
     else
@@ -833,7 +833,7 @@ hipError_t launch_tile_factor_step(const Problem& pb, const MstepArgs& a, int k,
     const size_t inv_lds = (size_t)TB * TB * sizeof(cd) + (size_t)TB * 8 * sizeof(cd);
     hipLaunchKernelGGL(tile_inverse_kernel, dim3(pb.B), dim3(64), inv_lds, s, a, pb.L, k0, w, pb.NR, ex);
     const int below = nb - k - 1;
-    if (below > 0 && g_debug.cplx3 && a.solve_mode == SBCE_SOLVE_CHOL)
+    if (below > 0 && g_debug.cplx3 && (a.solve_mode == SBCE_SOLVE_CHOL || a.solve_mode == kSolveClampHpd))
         hipLaunchKernelGGL((tile_gemm_kernel<false, true>), dim3(below, pb.B), dim3(256), 0, s, a, pb.L, k,
                            pb.NR, ex);
     else if (below > 0)

@@ -236,6 +236,10 @@ struct DebugConfig {
     bool mstep_nosmall;  // SBCE_MSTEP_SMALL=0     L <= 64: the batched build + panel Cholesky instead of
                          //                        the one-workgroup M-step (mstep_small.hip)
     bool small_valu;     // SBCE_MSTEP_SMALL=v     the 256-thread VALU-build kernel also at P <= 16
+    bool small2_lds;     // SBCE_SMALL2_LDS=1      mstep_small2_kernel stages the symbols in LDS chunks
+                         //                        instead of streaming them per wave (A/B; not flagged)
+    bool small_v1;       // SBCE_MSTEP_SMALL=1     n_tx <= 2: the round-5 MFMA-build kernel instead of
+                         //                        mstep_small2_kernel (A/B; not flagged)
     int small_stop;      // SBCE_SMALL_STOP=1|2|3  DIAGNOSTIC: the one-workgroup M-step stops after its
                          //                        build (1) / factorisation (2) / symbol staging
                          //                        without the build's arithmetic (3); results invalid
@@ -336,6 +340,12 @@ constexpr int kEstepListCnt = 16;      // int32 counters after the sweep's list
 // the factorised-weight pass (estep_pair.hip) takes a symbol whose range D is at most this
 constexpr double kPairDmax = 640.0;
 
+// Internal solve mode of the min-norm solve's second factorisation (C = G^H G, minnorm.hip):
+// a pivot at or below its threshold is CLAMPED there (C is HPD by construction, so the clamp
+// never meets a non-PSD Schur complement).  R's own factorisations never clamp: in every
+// public mode a pivot at or below 1e-14 max diag R is dropped (see SBCE_SOLVE_CHOL, sbce.h).
+constexpr int kSolveClampHpd = 16;
+
 struct MstepArgs {
     const cd* yd;
     const cd* yp;      // [B][Tp][NR]
@@ -371,6 +381,11 @@ struct MstepArgs {
     // (HPD by construction: a clamp there means the kept subspace is too ill-conditioned for
     // the normal equations to hold lstsq's accuracy)
     int clamp_status = SBCE_STATUS_NONHPD;
+    // the oracle early stop folded into the M-step launch (mstep_small2_kernel; null: not folded)
+    const cd* h_true = nullptr;   // [B][K]
+    int32_t* done_w = nullptr;    // [B] set when |‖theta‖ - ‖h‖| < 1 after iteration it > 0
+    int32_t* iters_done = nullptr;
+    int it = 0;
 };
 
 // Per-trial extents of one tiled-factorisation launch sequence (mstep_large.hip): column
@@ -396,6 +411,7 @@ bool chol_supported(const Problem& pb);
 // L <= 64 (n_tx not 4, 8), CHOL / CHOL_DROP: build + solve of one trial in one workgroup
 // (mstep_small.hip); write_sys also stores R and B^H in a.R / a.rhs (sbce_mstep's outputs)
 bool mstep_small_supported(const Problem& pb, int solve_mode);
+bool mstep_small2_selected(const Problem& pb);   // the launch folds the early stop (a.h_true)
 hipError_t launch_mstep_small(const Problem& pb, const MstepArgs& a, bool write_sys, hipStream_t s);
 int chol_debug_skip_mask();
 constexpr int kLargeL = 512;   // L above this: tiled build + blocked right-looking Cholesky

@@ -31,12 +31,14 @@ as a fresh (K,1) complex128 array, the posterior exponent uses varn**2
 variance varn.  The reference's per-iteration ``print(norm(theta))`` is
 available with ``verbose=True``.  Near-singular normal equations do not raise
 (``np.linalg.solve`` only raises on an exactly zero LU pivot, which float
-rounding essentially never produces): the device Cholesky clamps the pivot and
-flags the trial (``last_status``).  ``solve='lstsq'`` is np.linalg.lstsq of PM.py:108
+rounding essentially never produces): the device Cholesky drops a pivot at or below
+1e-14 max diag R and flags the trial (``last_status``): theta stays finite and its
+range-space part is lstsq's minimum-norm solution (where the reference's LU returns
+rounding noise).  ``solve='lstsq'`` is np.linalg.lstsq of PM.py:108
 (the minimum-norm solution with lstsq's default singular-value cut, include/sbce.h
 SBCE_SOLVE_MINNORM): the reference's policy for rank-deficient normal equations and
-the intended fallback of all_detectorsvsTd.py:238-241.  ``solve='drop'`` drops non-HPD
-pivots (a basic, not minimum-norm, solution; kept for A/B comparisons).
+the intended fallback of all_detectorsvsTd.py:238-241.  ``solve='drop'`` is the same
+solve as 'chol' (kept for older callers).
 """
 import ctypes
 
@@ -504,10 +506,13 @@ def estep_batch(y_d, psi_d, cons, theta, varn, n_tx, mode="soft", partition_r=0,
     return mom[..., :n_tx], mom[..., n_tx:].reshape(B, T_d, n_tx, n_tx)
 
 
-def mstep_batch(y_d, y_p, psi_d, u_p, cons, m, S, varn, solve="chol", return_tol=False):
+def mstep_batch(y_d, y_p, psi_d, u_p, cons, m, S, varn, solve="chol", return_tol=False,
+                ws_fill=None):
     """One device M-step (sbce_mstep) from given moments: returns theta (B,K),
     R (B,L,L), rhs (B,L,n_rx), status (B,) [, tol (B,): the min-norm pivot threshold
-    32 eps K lambda_max(R) (sbce_debug_minnorm_tol), return_tol=True with solve='lstsq']."""
+    32 eps K lambda_max(R) (sbce_debug_minnorm_tol), return_tol=True with solve='lstsq'].
+    ws_fill: a byte value the workspace is filled with first (tests: results must not
+    depend on what a workspace held)."""
     torch = _torch()
     lib = _lib.load()
     B, T_d, n_rx = np.shape(y_d)
@@ -515,6 +520,8 @@ def mstep_batch(y_d, y_p, psi_d, u_p, cons, m, S, varn, solve="chol", return_tol
     n_tx = np.shape(m)[2]
     theta = np.zeros((B, L * n_rx), dtype=complex)
     dims, ptrs, keep = _stage_setup(torch, y_d, y_p, psi_d, u_p, cons, theta, varn)
+    if ws_fill is not None:
+        keep[6].fill_(int(ws_fill))
     mom = np.concatenate([np.asarray(m).reshape(B, T_d, n_tx),
                           np.asarray(S).reshape(B, T_d, n_tx * n_tx)], axis=2)
     Mo = _dev(torch, mom, np.complex128)

@@ -58,14 +58,19 @@ def pilot_symbols(n_tx, M, T_p, rs=None):
     return [np.reshape(cons[rs.choice(range(0, M), n_tx, "True")], (n_tx, 1)) for _ in range(T_p)]
 
 
-def irs_matrix(T_p, T_d, N, beta_min=0.0, beta_max=2 * np.pi, amp=1.0, pilot="dft_n", rs=None):
+def irs_matrix(T_p, T_d, N, beta_min=0.0, beta_max=2 * np.pi, amp=1.0, pilot="dft_n", rs=None,
+               data="random"):
     """(PsiTilde_tp, PsiTilde_td) of PMd/Proposed_method_NMSEvsTp.py:86-97.
 
     pilot='dft_n'  : (N+1) x T_p, rows n < N = exp(-2j pi t n / N), row N = 0 (PMd scripts)
     pilot='dft_tp' : N x T_p, exp(-2j pi t n / T_p) (root scripts :73-77; the caller
                      inserts the ones row, :129)
     pilot='dft_n_full': (N+1) x T_p, all rows filled (PMd/Log_likelihood.py:106-108)
-    PsiTilde_td is N x T_d uniform phases in [beta_min, beta_max).
+    data='random'  : PsiTilde_td is N x T_d uniform phases in [beta_min, beta_max)
+    data='dft_td'  : the root T_d script's deterministic data phases (Proposed_method_NMSEvsTd.py
+                     :92-94): (N+1) x T_d exp(-2j pi t n / T_d), whose row 0 is the direct path's
+                     ones -- returned as rows 1..N (N x T_d, no RNG draw) so that insert_direct
+                     gives the reference's matrix, as for the random phases.
     """
     rs = _rs(rs)
     # element-wise scalar evaluation, exactly as the reference loops (bitwise replay)
@@ -83,6 +88,10 @@ def irs_matrix(T_p, T_d, N, beta_min=0.0, beta_max=2 * np.pi, amp=1.0, pilot="df
     for n in range(rows):
         for t in range(T_p):
             Ptp[n, t] = np.exp((-1j * 2 * np.pi * (t) * (n)) / (den))
+    if data == "dft_td":
+        return Ptp, dft_phases(N + 1, T_d, T_d)[1:]
+    if data != "random":
+        raise ValueError(data)
     cols = []
     for _ in range(T_d):
         beta = (beta_max - beta_min) * rs.uniform(0, 1, (N, 1)) + beta_min

@@ -102,11 +102,19 @@ def nmse_vs_tp(T_p=(4, 12, 20, 28, 36, 40), T_d=50, N=32, n_rx=4, n_tx=4, itera=
 
 
 def nmse_vs_td(T_d=(20, 30, 40, 50, 60, 70, 80, 90, 100), T_p=16, N=32, n_rx=2, n_tx=2, itera=3,
-               monte_iter=1, M=4, varn=0.1, seed=0, replay=True, mode="soft", varh=1.0):
+               monte_iter=1, M=4, varn=0.1, seed=0, replay=True, mode="soft", varh=1.0,
+               variant="pmd"):
     """Mean NMSE per data length (PMd/Proposed_method_NMSEvsTd.py:140-157; C-order h, :15).
 
     Reference draw order per trial: channelMatrix, pilotSymbols(T_p), then for each T_d:
-    symbols(T_d), irsMatrix, receivedSignals."""
+    symbols(T_d), irsMatrix, receivedSignals.
+    variant='root': the root-level Proposed_method_NMSEvsTd.py -- the same draw order, N x T_p
+    DFT pilot phases over T_p plus a ones row (:81-86, :95), deterministic (N+1) x T_d DFT data
+    phases over T_d (:92-94, no RNG draw: signal_model.irs_matrix(data='dft_td')) and the EM
+    started from theta = 0 (:46, em_zero_init)."""
+    if variant not in ("pmd", "root"):
+        raise ValueError(variant)
+    root = variant == "root"
     dist, world, rank = _dist()
     mine = set(shard(monte_iter, world, rank).tolist())
     points = [[] for _ in T_d]
@@ -120,10 +128,16 @@ def nmse_vs_td(T_d=(20, 30, 40, 50, 60, 70, 80, 90, 100), T_p=16, N=32, n_rx=2, 
         X_p = sm.pilot_symbols(n_tx, M, T_p, rs=rs)
         for k, td in enumerate(T_d):
             X_d, _ = sm.symbols(n_tx, M, td, rs=rs)
-            Ptp, Ptd = sm.irs_matrix(T_p, td, N, rs=rs)
+            if root:
+                Ptp, Ptd = sm.irs_matrix(T_p, td, N, pilot="dft_tp", data="dft_td", rs=rs)
+                Ptp = sm.insert_direct(Ptp)
+            else:
+                Ptp, Ptd = sm.irs_matrix(T_p, td, N, rs=rs)
             Ptd = sm.insert_direct(Ptd)
             Y_p, Y_d, U_p, _, h0 = sm.received_signals(T_p, td, Ptp, Ptd, n_rx, n_tx, X_d, X_p, h,
-                                                       varn, rs=rs)
+                                                       varn, rs=rs, with_initial=not root)
+            if root:
+                h0 = np.zeros(len(h), dtype=complex)
             if i in mine:
                 points[k].append(dict(Y_d=Y_d, Y_p=Y_p, Psi_d=Ptd, U_p=U_p, h0=h0, h=h))
     acc = Accumulators(len(T_d))

@@ -320,6 +320,36 @@ def case_root():
                             theta=np.asarray(th).reshape(-1), nmse=nmse(th, h))
 
 
+def case_root_td():
+    """Root-level Proposed_method_NMSEvsTd.py: zero init (:44-47), C-order h (:25), N x T_p DFT
+    over T_p plus a ones row (:81-86, :95) and DETERMINISTIC (N+1) x T_d DFT data phases over T_d
+    (:92-94); per trial channelMatrix, pilotSymbols, then per T_d point symbols, irsMatrix,
+    receivedSignals (:137-143).  Two T_d points of one trial."""
+    N, n_tx, n_rx, T_p, M, varn, itera = 4, 1, 3, 6, 4, 0.1, 3
+    T_ds = (8, 12)
+    ns = load_defs(os.path.join(REF, "Proposed_method_NMSEvsTd.py"), N=N, n_tx=n_tx,
+                   beta_min=0.0, beta_max=2 * np.pi)
+    np.random.seed(5)
+    h = quiet(ns["channelMatrix"], n_tx, n_rx, N, 1)
+    X_p = ns["pilotSymbols"](n_tx, M, T_p)
+    out = dict(h=h, X_p=X_p, h0=np.zeros(len(h), dtype=complex))
+    for k, T_d in enumerate(T_ds):
+        X_d, aps = ns["symbols"](n_tx, M, T_d)
+        Ptp, Ptd = ns["irsMatrix"](T_p, T_d, N, 0, 1)
+        Y_p, Y_d, Z_p, Z_d = ns["receivedSignals"](T_p, T_d, Ptp, Ptd, n_rx, n_tx, X_d, X_p,
+                                                   h, varn, M)
+        th = quiet(ns["em"], Y_d, Y_p, T_d, T_p, Z_p, Ptd, aps, M, varn, itera)
+        out.update({f"X_d{k}": np.stack([x.reshape(-1) for x in X_d]), f"Ptd{k}": Ptd,
+                    f"Y_d{k}": np.stack([y.reshape(-1) for y in Y_d]),
+                    f"Y_p{k}": np.stack([y.reshape(-1) for y in Y_p]),
+                    f"Z_p{k}": np.stack(Z_p), f"theta{k}": np.asarray(th).reshape(-1),
+                    f"nmse{k}": nmse(th, h)})
+        out["Ptp"], out["aps"] = Ptp, aps
+    out["X_p"] = np.stack([x.reshape(-1) for x in X_p])
+    return "root_td", dict(out, N=N, n_tx=n_tx, n_rx=n_rx, T_p=T_p, T_ds=np.array(T_ds), M=M,
+                           varn=varn, itera=itera, seed=5)
+
+
 def case_pm(name, N, n_tx, n_rx, T_d, T_p, M, varn, itera, seed, r_uniform, r_soft):
     """PM.em_pm (uniform list, lstsq) and PM_beta.em_pm (posterior list) on north-star data."""
     ns = load_defs(os.path.join(PMD, "Proposed_method_NMSEvsTp.py"),
@@ -543,6 +573,7 @@ CASES = {
     "kat2_snr": (case_kat2, ()),
     "kat2_driver": (case_kat2_driver, ()),
     "root_tp": (case_root, ()),
+    "root_td": (case_root_td, ()),
     "nt4_m4": (case_shape, ("nt4_m4", 3, 4, 4, 16, 8, 4, 0.1, 2, 5)),
     "nt3_m4": (case_shape, ("nt3_m4", 3, 3, 2, 10, 8, 4, 0.2, 2, 9)),
     "nt1_m16": (case_shape, ("nt1_m16", 5, 1, 3, 20, 6, 16, 0.3, 3, 4)),

@@ -168,15 +168,15 @@ def test_cfg1_shape_full_em_vs_oracle(sbce):
                         *estep_moments(th0, b["y_d"][0], b["psi_d"][0].T, aps, varn)[:2])
     cond = np.linalg.cond(R0)
     assert rel(r["theta"][0], th0) < max(1e-10, 1e-14 * cond)
-    assert abs(nmse(r["theta"][0], b["h"][0]) / nmse(th0, b["h"][0]) - 1) < 1e-3
+    assert abs(nmse(r["theta"][0], b["h"][0]) / nmse(th0, b["h"][0]) - 1) < max(1e-9, 1e-13 * cond)
 
 
 def test_cfg1_nmse_trajectory_20_iterations_vs_oracle(sbce):
     """The headline workload's NMSE, pinned: BASELINE cfg 1 (4x4, N_RIS = 64, T_p = 16,
     T_d = 256, 16-QAM, 20 dB) on the first 8 trials of bench.py's synthetic batch, all 20 EM
     iterations, against the oracle's trajectories (tests/golden/cfg1_traj.npz, made by
-    tests/golden/make_cfg1_traj.py).  North-star bar: NMSE within 1e-3 relative at every
-    iteration; measured agreement is reported per iteration."""
+    tests/golden/make_cfg1_traj.py).  Asserted at what it measures (~1e-12): NMSE within 1e-9
+    relative at every iteration and theta within 1e-10 after 20 (the north-star bar is 1e-3)."""
     g = golden("cfg1_traj")
     n = g["nmse"].shape[0]
     varn = float(sbce.signal_model.snr_to_varn(float(g["snr"])))
@@ -190,8 +190,8 @@ def test_cfg1_nmse_trajectory_20_iterations_vs_oracle(sbce):
         nm = np.array([nmse(r["theta"][i], b["h"][i]) for i in range(n)])
         err = np.abs(nm / g["nmse"][:, it] - 1).max()
         worst.append(err)
-        assert err < 1e-3, (it, err)
-    assert rel(r["theta"], g["theta"]) < 1e-6, rel(r["theta"], g["theta"])
+        assert err < 1e-9, (it, err)
+    assert rel(r["theta"], g["theta"]) < 1e-10, rel(r["theta"], g["theta"])
     print("cfg1 trajectory: max relative NMSE deviation per iteration", np.array(worst))
 
 
@@ -326,9 +326,29 @@ def test_snr_sweep_entry_point_reproduces_reference_curve(sbce):
     assert np.allclose(curves["hard"], k["nmse_ml"], rtol=1e-9, atol=0)
 
 
+def test_root_td_variant_em_zero_init_and_sweep_vs_reference(sbce):
+    """Root-level Proposed_method_NMSEvsTd.py (tests/golden/root_td.npz: the reference's own em,
+    zero init, deterministic DFT data phases :92-94): the drop-in em_zero_init per T_d point, and
+    sweeps.nmse_vs_td(variant='root') replaying the script's draw order, reproduce its theta and
+    NMSE at 1e-10 / 1e-9."""
+    d = golden("root_td")
+    for k in range(len(d["T_ds"])):
+        Y_d = [y[:, None] for y in d[f"Y_d{k}"]]
+        Y_p = [y[:, None] for y in d[f"Y_p{k}"]]
+        th = sbce.em_zero_init(Y_d, Y_p, int(d["T_ds"][k]), int(d["T_p"]), list(d[f"Z_p{k}"]),
+                               d[f"Ptd{k}"], d["aps"], int(d["M"]), float(d["varn"]), int(d["itera"]))
+        assert rel(th, d[f"theta{k}"]) < THETA_TOL
+    x, nm = sbce.sweeps.nmse_vs_td(tuple(int(t) for t in d["T_ds"]), int(d["T_p"]), int(d["N"]),
+                                   int(d["n_rx"]), int(d["n_tx"]), int(d["itera"]), 1, int(d["M"]),
+                                   float(d["varn"]), int(d["seed"]), variant="root")
+    assert np.allclose(nm, [float(d["nmse0"]), float(d["nmse1"])], rtol=1e-9, atol=0)
+
+
 @pytest.mark.parametrize("script,args,rows", [
     ("Proposed_method_NMSEvsTp.py", ["--monte-iter", "2", "--T-p", "8", "40", "--N", "8"], 2),
     ("Proposed_method_NMSEvsTd.py", ["--monte-iter", "2", "--T-d", "20", "40", "--N", "8"], 2),
+    ("Proposed_method_NMSEvsTd.py", ["--variant", "root", "--T-d", "20", "40", "--N", "8",
+                                     "--itera", "4"], 2),
     ("nmse_vs_snr.py", ["--monte-iter", "2", "--SNR", "0", "20"], 2),
     ("log_max_SER.py", ["--monte-iter", "2", "--SNR", "0", "20", "--N", "8"], 2),
     ("ParallelProtocol_Tp.py", ["--monte-iter", "2", "--T-p", "8", "60", "--N", "8",
@@ -482,9 +502,10 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape):
 def test_small_mstep_matches_batched_path(sbce, shape, solve):
     """L <= 64 (n_tx not 4, 8): R and B^H of the one-workgroup kernel's VALU build (P > 16;
     SBCE_MSTEP_SMALL=v forces it at P <= 16 too) are bitwise the batched build's (same per-element
-    operation order); its MFMA build (P <= 16, the default there) agrees to 1e-13; the solves agree
-    with the batched panel Cholesky (SBCE_MSTEP_SMALL=0) and numpy.linalg.solve; the same trials
-    are flagged."""
+    operation order); its MFMA builds (P <= 16: the round-6 mstep_small2_kernel for n_tx <= 2,
+    n_rx <= 4 -- block-per-wave three-MFMA build, one-wave solve -- and the round-5 kernel,
+    SBCE_MSTEP_SMALL=1) agree to 1e-13; the solves agree with the batched panel Cholesky
+    (SBCE_MSTEP_SMALL=0) and numpy.linalg.solve; the same trials are flagged."""
     n_tx, n_rx, N, T_p, T_d, M = shape
     b = sbce.signal_model.synthetic_batch(3, n_tx, n_rx, N, T_p, T_d, M, 0.1, seed=41)
     x = b["x_d"]
@@ -492,10 +513,11 @@ def test_small_mstep_matches_batched_path(sbce, shape, solve):
     args = (b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], x, S, 0.1)
     with sbce._lib.debug_env(SBCE_MSTEP_SMALL="0"):
         th0, R0, rhs0, st0 = sbce.mstep_batch(*args, solve=solve)
-    for arm, env in (("default", {}), ("valu", {"SBCE_MSTEP_SMALL": "v"})):
+    for arm, env in (("default", {}), ("v1", {"SBCE_MSTEP_SMALL": "1"}),
+                     ("valu", {"SBCE_MSTEP_SMALL": "v"})):
         with sbce._lib.debug_env(**env):
             th, R, rhs, st = sbce.mstep_batch(*args, solve=solve)
-        wave = arm == "default" and N + 1 <= 16 and n_tx <= 3
+        wave = arm != "valu" and N + 1 <= 16 and n_tx <= 3
         if wave:
             assert rel(R, R0) < 1e-13 and rel(rhs, rhs0) < 1e-13, arm
         else:
@@ -531,6 +553,47 @@ def test_small_mstep_full_em_matches_batched_path(sbce):
             it0 = eng0.iters_done.cpu().numpy()
         assert np.array_equal(it, it0), mode
         assert rel(th, th0) < 1e-9, mode
+
+
+@pytest.mark.parametrize("shape", [
+    # (n_tx, n_rx, N, T_p, T_d, M)   rank R <= T_p + T_d < L: unregularised hard moments
+    (4, 4, 149, 16, 200, 16),        # L = 600: the tiled L > 512 factorisation (round-5 all-NaN case)
+    (4, 4, 64, 16, 100, 16),         # L = 260: the batched-panel Cholesky (cfg1 geometry)
+    (2, 2, 15, 4, 5, 4),             # L = 32: the one-workgroup M-step
+])
+def test_chol_on_rank_deficient_R_is_finite_flagged_and_minnorm_on_range(sbce, shape):
+    """CHOL (np.linalg.solve, Proposed_method_NMSEvsTp.py:80) on a rank-deficient R, S_t = x x^H
+    unregularised: every trial flagged NONHPD; theta finite and BITWISE the same in a 0x00 and a
+    0xFF (NaN-pattern) workspace; it solves the normal equations (residual <= 1e-10) and its
+    range-space part equals numpy.linalg.lstsq's minimum-norm solution at 1e-10 -- the same
+    properties as the CPU restatement of the policy (oracle.mstep_chol_policy,
+    test_oracle.py::test_chol_policy_on_rank_deficient_R).  Round 5 returned an all-NaN theta at
+    L = 600: its clamped pivots fed the Schur complement's rounding noise back squared."""
+    import torch
+    from oracle.em_reduced import mstep_chol_policy, mstep_lstsq, range_part
+    n_tx, n_rx, N, T_p, T_d, M = shape
+    varn = float(sbce.signal_model.snr_to_varn(20.0))
+    b = sbce.signal_model.synthetic_batch(2, n_tx, n_rx, N, T_p, T_d, M, varn, seed=11)
+    x = b["x_d"]
+    S = x[..., :, None] * np.conj(x[..., None, :])
+    args = (b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], x, S, varn)
+    outs = [sbce.mstep_batch(*args, solve="chol", ws_fill=f) for f in (0x00, 0xFF)]
+    th, R, rhs, st = outs[0]
+    assert np.isfinite(th).all()
+    assert np.array_equal(th.view(np.uint64), outs[1][0].view(np.uint64))
+    assert np.array_equal(st, outs[1][3])
+    assert (st & sbce._lib.SBCE_STATUS_NONHPD).all()
+    for i in range(2):
+        R0, rhs0 = mstep_build(b["u_p"][i], b["y_p"][i], b["psi_d"][i].T, b["y_d"][i], x[i], S[i])
+        lo = np.tril_indices(R0.shape[0])
+        assert rel(R[i][lo], R0[lo]) < 1e-12
+        th_ls, rank = mstep_lstsq(R0, rhs0)
+        assert rank <= T_p + T_d < R0.shape[0]
+        X = np.conj(th[i]).reshape(R0.shape[0], n_rx)
+        assert np.abs(R0 @ X - rhs0).max() / np.abs(rhs0).max() < 1e-10
+        assert rel(range_part(R0, th[i], n_rx), th_ls) < 1e-10
+        th_cpu, _ = mstep_chol_policy(R0, rhs0)
+        assert rel(range_part(R0, th_cpu, n_rx), th_ls) < 1e-10
 
 
 # ---------------------------------------------------------------- large-L M-step (L > 512)
@@ -836,7 +899,7 @@ def test_workspace_contents_never_leak_into_results(sbce, case):
     elif case == "pm_lstsq":
         shape, kw = (4, 3, 3, 40, 12, 40, 16), dict(mode="pm_soft", partition_r=1, solve="lstsq")
     elif case == "large_chol":
-        shape = (2, 4, 4, 149, 16, 700, 16)              # L = 600 < T_p + T_d: tiled, HPD
+        shape = (2, 4, 4, 149, 16, 200, 16)              # L = 600 > T_p + T_d: tiled, NON-HPD R
     elif case == "cfg1_chol_streams":
         kw = dict(streams=2)
     b = sbce.signal_model.synthetic_batch(*shape, varn, seed=11)

@@ -623,3 +623,56 @@ def test_snr_sweep_five_detectors_one_collective(sbce, monkeypatch):
         ref = k["curve"][dets.index(key)]
         assert np.allclose(curves[mode], ref, rtol=1e-9, atol=0), mode
         assert not flagged[mode].any()
+
+
+@pytest.mark.parametrize("shape", [(4, 4, 64, 16, 100), (4, 4, 149, 16, 200), (2, 2, 15, 4, 5)])
+def test_chol_policy_on_rank_deficient_R(sbce, shape):
+    """np.linalg.solve (Proposed_method_NMSEvsTp.py:80) on a rank-deficient R (hard moments,
+    rank R <= T_p + T_d < L) has no reproducible answer: the reference's
+    LU returns rounding noise.  The device's CHOL policy (oracle.mstep_chol_policy): pivots
+    <= 1e-14 max diag R dropped -- finite theta that solves the normal equations and whose
+    range-space part is lstsq's minimum-norm solution.  The round-5 clamp policy overflows
+    (the cause of the all-NaN theta at L = 600)."""
+    from oracle.em_reduced import mstep_chol_policy, mstep_lstsq, range_part
+    n_tx, n_rx, N, T_p, T_d = shape
+    varn = float(sbce.signal_model.snr_to_varn(20.0))
+    b = sbce.signal_model.synthetic_batch(1, n_tx, n_rx, N, T_p, T_d, 16 if n_tx == 4 else 4, varn,
+                                          seed=11)
+    x = b["x_d"][0]
+    S = x[:, :, None] * np.conj(x[:, None, :])
+    R, rhs = mstep_build(b["u_p"][0], b["y_p"][0], b["psi_d"][0].T, b["y_d"][0], x, S)
+    th_ls, rank = mstep_lstsq(R, rhs)
+    assert rank <= T_p + T_d < R.shape[0]
+    th_c, bad_c = mstep_chol_policy(R, rhs, clamp=True)
+    if R.shape[0] > 64:
+        assert not np.isfinite(th_c).all()               # the old clamp overflows
+    th, bad = mstep_chol_policy(R, rhs)
+    assert np.isfinite(th).all() and bad.any()           # (a noise pivot may sit above tol)
+    X = np.conj(th).reshape(R.shape[0], n_rx)
+    assert np.abs(R @ X - rhs).max() / np.abs(rhs).max() < 1e-10
+    assert rel(range_part(R, th, n_rx), th_ls) < 1e-10
+
+
+def test_root_td_variant_replay_and_oracle(sbce):
+    """Root-level Proposed_method_NMSEvsTd.py (tests/golden/root_td.npz, the reference's own run):
+    C-order h, pilots then per T_d point symbols / deterministic DFT data phases over T_d
+    (:92-94, irs_matrix(data='dft_td'), no RNG draw) / noise; the zero-initialised EM (:44-77)
+    restated by the oracle reproduces the reference theta at both T_d points."""
+    sm = sbce.signal_model
+    d = golden("root_td")
+    N, n_tx, n_rx, T_p, M = (int(d[k]) for k in ("N", "n_tx", "n_rx", "T_p", "M"))
+    np.random.seed(int(d["seed"]))
+    h = sm.channel_matrix(n_tx, n_rx, N, 1.0, order="C")
+    X_p = sm.pilot_symbols(n_tx, M, T_p)
+    assert np.array_equal(h, d["h"])
+    for k, T_d in enumerate(d["T_ds"]):
+        X_d, aps = sm.symbols(n_tx, M, int(T_d))
+        Ptp, Ptd = sm.irs_matrix(T_p, int(T_d), N, pilot="dft_tp", data="dft_td")
+        Ptp, Ptd = sm.insert_direct(Ptp), sm.insert_direct(Ptd)
+        assert np.array_equal(Ptd, d[f"Ptd{k}"]) and np.array_equal(Ptp, d["Ptp"])
+        Y_p, Y_d, U_p, _, _ = sm.received_signals(T_p, int(T_d), Ptp, Ptd, n_rx, n_tx, X_d, X_p, h,
+                                                  float(d["varn"]), with_initial=False)
+        assert rel(Y_d, d[f"Y_d{k}"]) < 1e-14 and rel(Y_p, d[f"Y_p{k}"]) < 1e-14
+        th = em_reduced(Y_d, Y_p, U_p, Ptd, aps, float(d["varn"]), int(d["itera"]),
+                        np.zeros(len(h), dtype=complex))
+        assert rel(th, d[f"theta{k}"]) < 1e-12

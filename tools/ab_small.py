@@ -1,6 +1,7 @@
 """A/B of the L <= 64 M-step on BASELINE cfg 5's largest grid point (T_d = 120, the 20 SNR points
 batched: 1280 trials): sbce_mstep time of the one-workgroup kernel (full, build only, build +
-factorisation: SBCE_SMALL_STOP) vs the batched path (SBCE_MSTEP_SMALL=0), HIP events.
+factorisation: SBCE_SMALL_STOP, the round-5 kernel's VALU build) vs the round-5 kernel
+(SBCE_MSTEP_SMALL=1) and the batched path (SBCE_MSTEP_SMALL=0), HIP events.
 
   python tools/ab_small.py [T_d] [reps]
 """
@@ -26,9 +27,9 @@ def main():
     batch = {k: np.concatenate([p[k] for p in pts]) for k in ("y_d", "y_p", "psi_d", "u_p", "theta0", "h")}
     batch["cons"] = pts[0]["cons"]
     vt = np.repeat(varn, 64)
-    for arm, env in (("small", {}), ("small_build", {"SBCE_SMALL_STOP": "1"}),
-                     ("small_factor", {"SBCE_SMALL_STOP": "2"}),
-                     ("small_stage", {"SBCE_SMALL_STOP": "3"}), ("batched", {"SBCE_MSTEP_SMALL": "0"})):
+    for arm, env in (("small", {}), ("small_lds", {"SBCE_SMALL2_LDS": "1"}), ("small_v1", {"SBCE_MSTEP_SMALL": "1"}),
+                     ("small_build", {"SBCE_SMALL_STOP": "1"}), ("small_factor", {"SBCE_SMALL_STOP": "2"}),
+                     ("batched", {"SBCE_MSTEP_SMALL": "0"})):
         with pkg._lib.debug_env(**env):
             eng = pkg.EMEngine(batch, vt, mode="soft")
             eng.estep()
