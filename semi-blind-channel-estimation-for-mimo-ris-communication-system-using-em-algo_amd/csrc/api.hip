@@ -17,7 +17,7 @@ DebugConfig g_debug;
 
 namespace {
 constexpr DebugConfig kDebugDefault = {false, false, false, false, false, 128, false, false, false,
-                                       true, false, false, false, false, 0, 0};
+                                       true, false, false, false, 0, 0};
 constexpr int kSphereBudgetMax = 256;      // estep.hip kBfsPmax
 
 void read_debug_env(DebugConfig& c) {
@@ -42,9 +42,8 @@ void read_debug_env(DebugConfig& c) {
         c.small_valu = v[0] == 'v';
         c.small_v1 = v[0] == '1';
     }
-    if ((v = env("SBCE_SMALL2_LDS"))) c.small2_lds = v[0] == '1';
     if ((v = env("SBCE_PM_IMPL"))) c.pm_impl = (v[0] == 'w' || v[0] == 't' || v[0] == 'q') ? v[0] : 0;
-    if ((v = env("SBCE_SMALL_STOP"))) c.small_stop = (v[0] >= '1' && v[0] <= '3') ? v[0] - '0' : 0;
+    if ((v = env("SBCE_SMALL_STOP"))) c.small_stop = (v[0] >= '1' && v[0] <= '4') ? v[0] - '0' : 0;
 }
 
 __attribute__((constructor)) void load_debug_env() { read_debug_env(g_debug); }
@@ -412,6 +411,12 @@ int sbce_debug_chol_timing(int mode, double* out6) {
 
 // Diagnostic, not part of include/sbce.h: per-phase cycle sums (32) of the MFMA Cholesky
 // (SBCE_CHOL_SKIP bit 64); reset != 0 clears them.
+// Diagnostic, not part of include/sbce.h: s_memtime stamps (48) of trial 0's solve wave in the
+// n_tx <= 2 small M-step (SBCE_SMALL_STOP=4).
+int sbce_debug_small_clock(unsigned long long* out48) {
+    return out48 ? hip_rc(small_debug_clock(out48)) : SBCE_EINVAL;
+}
+
 int sbce_debug_chol_clock(unsigned long long* out32, int reset) {
     if (reset) return hip_rc(chol_debug_clock_reset());
     return out32 ? hip_rc(chol_debug_clock(out32)) : SBCE_EINVAL;

@@ -18,6 +18,8 @@
 // Pivot rule and status bits are the batched path's (chol.hip factor_diag): a pivot that is not
 // above tol is flagged (clamp_status); SBCE_SOLVE_CHOL clamps it to tol, CHOL_DROP drops the
 // direction (l_cc = 0, its unknowns 0).
+#include <type_traits>
+
 #include "sbce_internal.h"
 
 namespace sbce {
@@ -445,21 +447,28 @@ mstep_small5_kernel(MstepArgs a, int NT, int P, int Tp, int Td, int L, int write
 // The kernel above spends its time in two places (cfg 5, 1280 trials, five workgroups per CU):
 // wave 0 carries two of the five MFMA items (the (0,0) block and a B^H row tile, whose 16 x 16
 // tile uses 2 of its 16 columns), so SIMD 0 runs 8 of the 20 MFMAs of every k-step; and the
-// factorisation / back substitution take one 256-thread barrier per column (64 barriers).  Here:
-//   build   the symbols pass through LDS in 16-symbol chunks (double-buffered: chunk k+1's loads
-//           are in flight in every thread's registers while chunk k is consumed; one barrier per
-//           chunk); role w < NBLK builds block w (the (0,0), (1,0), (1,1) blocks of R) over ALL
-//           symbols, complex products by three real MFMAs (Gauss: P1 = sum xr yr, P2 = sum xi yi,
-//           P3 = sum (xr + xi)(yr + yi); re = P1 - P2, im = P3 - P1 - P2); role NBLK builds B^H
-//           on the VALU (lane = (p, symbol), reduced over the symbols at the end); roles rotate
-//           over the waves with the block index;
-//   solve   ONE wave: right-looking Cholesky with the forward substitution fused, lane (r, h)
-//           holding row r's columns j = 2e + h in registers; per column the pivot by v_readlane,
-//           the scaled column published through a double-buffered LDS vector (wave-level sync
-//           only), y_c by v_readlane; back substitution with L's rows read from LDS.
-// The oracle early stop (|‖theta‖ - ‖h‖| < 1, early_stop_kernel) is folded into the epilogue when
-// a.h_true is set.  Pivot rule and status as factor_diag (a pivot not above 1e-14 max diag R is
-// flagged and dropped).
+// factorisation / back substitution take one 256-thread barrier per column (64 barriers).  Here
+// two launches:
+//   build   (mstep_small2_build_kernel, 4 waves per trial, five trials per CU) wave w < NBLK
+//           builds block w of R (the (0,0), (1,0), (1,1) blocks) over ALL symbols, wave NBLK
+//           B^H = sum_t (psi_t (x) m_t) y_t^H as one more 16 x (NT NR) MFMA product (the pilots in
+//           NT passes, their u_t not being a product); complex products by three real MFMAs
+//           (Gauss: P1 = sum xr yr, P2 = sum xi yi, P3 = sum (xr + xi)(yr + yi); re = P1 - P2,
+//           im = P3 - P1 - P2); each wave streams its operands from global memory with the raw
+//           values of the next k-steps in flight (a staging of the symbols in LDS by 16-symbol
+//           chunks, one barrier per chunk, measured slower: 113.6 vs 98.8 us at T_d = 120);
+//           R (full) and B^H to the workspace, no barrier;
+//   solve   (mstep_small2_solve_kernel, ONE wave per trial, no occupancy cap: the row registers,
+//           the column values and the right-hand sides stay in VGPRs -- at the build's 96-VGPR
+//           cap they went to scratch, one memory round trip per column) right-looking Cholesky
+//           with the forward substitution fused, lane (r, h) holding row r's columns 2e + h, a
+//           rolled loop over column pairs whose current column is register slot 0, the pivot by
+//           v_readlane, the scaled column published through a double-buffered LDS vector and
+//           read back in one batch (a branch per slot put every read's latency on the chain), y_c
+//           by v_readlane; back substitution with L's rows from LDS; theta = conj(x).
+// The oracle early stop (|‖theta‖ - ‖h‖| < 1, early_stop_kernel) is folded into the solve's
+// epilogue when a.h_true is set.  Pivot rule and status as factor_diag (a pivot not above 1e-14
+// max diag R is flagged and dropped).
 // right-hand side h + 2k of a lane's half h: the entry of v without a lane-dependent index
 template <int NR>
 __device__ __forceinline__ cd rhs_pick(const cd (&v)[NR], int h, int k) {
@@ -468,338 +477,282 @@ __device__ __forceinline__ cd rhs_pick(const cd (&v)[NR], int h, int k) {
     return csel(h != 0, v1, v0);
 }
 
-// Symbol chunks of the build (16 symbols, staged in LDS, double-buffered): a data chunk holds
-// psi [16][P <= 16] at 0, the moments [16][MS <= 6] at 256 and y_d [16][NR <= 4] at 352; a pilot
-// chunk u_p [16][L <= 32] at 0 and y_p [16][NR] at 512.  R (32 x 33) aliases the two buffers
-// once the last chunk is consumed.
-constexpr int kS2Chunk = 16, kS2Buf = 576, kS2Ldr = 33;
+// DIAGNOSTIC (SBCE_SMALL_STOP=4, results unchanged): s_memtime stamps of trial 0's solve wave --
+// [0] start, [1] loads done, [2] tol, [3 + k] column pair k factored, [40] factor done, [41] back
+// substitution done (tools/small_clock.py)
+__device__ unsigned long long g_small_clk[48];
 
-template <int NT, int NR, bool GLB>
+template <int NT, int NR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void
-mstep_small2_kernel(MstepArgs a, int P, int Tp, int Td, int L, int write_sys, int stop) {
+mstep_small2_build_kernel(MstepArgs a, int P, int Tp, int Td, int L) {
     const int b = blockIdx.x;
     if (a.done && a.done[b]) return;
     constexpr int NBLK = NT * (NT + 1) / 2;
     constexpr int MS = NT + NT * NT;
-    constexpr int LDR = kS2Ldr;
-    constexpr int CH = kS2Chunk;
-    __shared__ __attribute__((aligned(16))) cd stage[2 * kS2Buf];   // symbol chunks, then R
-    __shared__ cd sB[32 * NR];
-    __shared__ cd colb[2][32];
-    __shared__ double dinv[32];
-    cd* sR = stage;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int T = Tp + Td;
     const cd* up = a.up + (size_t)b * Tp * L;
     const cd* yp = a.yp + (size_t)b * Tp * NR;
     const cd* ps = a.psid + (size_t)b * Td * P;
     const cd* mom = a.mom + (size_t)b * Td * MS;
     const cd* yd = a.yd + (size_t)b * Td * NR;
-    const int ncp = (Tp + CH - 1) / CH, nch = ncp + (Td + CH - 1) / CH;
-
-    // roles rotate with the block index: five workgroups share a CU, and a fixed role -> wave map
-    // would put every workgroup's serial solve (role 0) on the same SIMD
-    const int role = (wave + b) & 3;
+    cd* R = a.R + (size_t)b * L * L;
+    cd* rh = a.rhs + (size_t)b * L * NR;
+    const int role = (wave + b) & 3;                 // rotates the roles over the SIMDs
     const int li = lane & 15, lk = lane >> 4;
     const bool lon = li < P;
-    // chunk k's values: thread tid loads entries tid, tid + 256, tid + 512 of its segments
-    cd ld[3];
-    auto fetch = [&](int k) {
-#pragma unroll
-        for (int h = 0; h < 3; ++h) {
-            const int e = tid + 256 * h;
-            ld[h] = czero();
-            if (k >= nch) continue;
-            if (k < ncp) {
-                const int t0 = k * CH, n = (Tp - t0) < CH ? (Tp - t0) : CH;
-                if (e < n * L) ld[h] = up[(size_t)t0 * L + e];
-                else if (e < n * L + n * NR) ld[h] = yp[(size_t)t0 * NR + e - n * L];
-            } else {
-                const int t0 = (k - ncp) * CH, n = (Td - t0) < CH ? (Td - t0) : CH;
-                if (e < n * P) ld[h] = ps[(size_t)t0 * P + e];
-                else if (e < n * (P + MS)) ld[h] = mom[(size_t)t0 * MS + e - n * P];
-                else if (e < n * (P + MS + NR)) ld[h] = yd[(size_t)t0 * NR + e - n * (P + MS)];
-            }
-        }
+    // this wave's product: block (bi, bj) of R (role < NBLK) or B^H (role NBLK, bh)
+    const bool bh = role == NBLK;
+    const int bi = role >= 1 ? 1 : 0, bj = role == 2 ? 1 : 0;
+    const int ca = li / NR, cr = li - ca * NR;      // B^H: column (a, r) of the product
+    const bool con = li < NT * NR;
+    const int VP = bh ? NT * Tp : Tp;                // virtual symbols: pilot slots, then data
+    const int V = VP + Td;
+    d4v p1 = {0.0, 0.0, 0.0, 0.0}, p2 = p1, p3 = p1;
+    auto mfma3 = [&](cd x, cd y) {
+        p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, y.x, p1, 0, 0, 0);
+        p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(x.y, y.y, p2, 0, 0, 0);
+        p3 = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x + x.y, y.x + y.y, p3, 0, 0, 0);
     };
-    auto store = [&](int k) {                        // the fetched values into buffer k & 1
-        cd* buf = stage + (k & 1) * kS2Buf;
+    {
+        // Each role streams its operands: the pilots, then the data symbols, each with the raw
+        // values of the next KD k-steps in flight in registers; loads never branch (indices
+        // clamped, invalid lanes / symbols zeroed by select), addresses advance by increments
+        const int lc = lon ? li : 0;
+        if (role < NBLK) {
+            // block (bi, bj) of R: A = u_t[p NT + bi] / psi_t[p] S_t[bi][bj],
+            //                      B = conj(u_t[q NT + bj]) / conj(psi_t[q])
+            constexpr int KD = 3;
+            cd ra[KD], rc[KD];
+            {   // pilots
+                const cd* pa = up + lc * NT + bi;
+                const cd* pb = up + lc * NT + bj;
+                auto raw = [&](int t, cd& x, cd& y) {
+                    const int tt = t < Tp ? t : (Tp > 0 ? Tp - 1 : 0);
+                    const bool ok = lon && t < Tp;
+                    const cd u1 = Tp > 0 ? pa[(size_t)tt * L] : czero();
+                    const cd u2 = Tp > 0 ? pb[(size_t)tt * L] : czero();
+                    x = csel(ok, u1, czero());
+                    y = csel(ok, u2, czero());
+                };
 #pragma unroll
-        for (int h = 0; h < 3; ++h) {
-            const int e = tid + 256 * h;
-            if (k >= nch) continue;
-            if (k < ncp) {
-                const int t0 = k * CH, n = (Tp - t0) < CH ? (Tp - t0) : CH;
-                if (e < n * L) buf[e] = ld[h];
-                else if (e < n * L + n * NR) buf[512 + e - n * L] = ld[h];
-            } else {
-                const int t0 = (k - ncp) * CH, n = (Td - t0) < CH ? (Td - t0) : CH;
-                if (e < n * P) buf[e] = ld[h];
-                else if (e < n * (P + MS)) buf[256 + e - n * P] = ld[h];
-                else if (e < n * (P + MS + NR)) buf[352 + e - n * (P + MS)] = ld[h];
-            }
-        }
-    };
-    // role < NBLK: block (bi, bj) of R, C[p][q] = sum_t x_t[p] y_t[q], lane (li, lk) = (row / column
-    // li, symbol 4s + lk of the chunk's k-step s); role NBLK: B^H[(p, a)][r] = sum_t w_t[p][a]
-    // conj(y_t[r]) on the VALU, lane (li, lk) = (p, symbol), reduced over lk at the end
-    // chunk loop: chunk k+1's loads in flight while chunk k is consumed, one barrier per chunk.
-    // Each role runs its own copy of the loop (the same barrier count; role is wave-uniform), so
-    // the accumulators of one role are not live in the other's registers.
-    auto chunks = [&](auto&& consume) {
-        fetch(0);
-        store(0);
-        __syncthreads();
-        for (int k = 0; k < nch; ++k) {
-            fetch(k + 1);
-            const bool pil = k < ncp;
-            const int t0 = pil ? k * CH : (k - ncp) * CH;
-            const int n = pil ? ((Tp - t0) < CH ? (Tp - t0) : CH) : ((Td - t0) < CH ? (Td - t0) : CH);
-            consume(stage + (k & 1) * kS2Buf, pil, n);
-            store(k + 1);                            // buffer (k+1)&1 was last read in chunk k-1
-            __syncthreads();
-        }
-    };
-    const int T = Tp + Td;
-    if (GLB && role < NBLK) {
-        // GLB: no staging -- each role streams its operands from global memory, the raw values of
-        // the next KD k-steps in flight in registers (x, y formed at use), no barrier
-        const int bi = role >= 1 ? 1 : 0, bj = role == 2 ? 1 : 0;
-        auto raw = [&](int t, cd& ra, cd& rc) {
-            ra = czero();
-            rc = czero();
-            if (lon && t < Tp) {
-                ra = up[(size_t)t * L + li * NT + bi];
-                rc = up[(size_t)t * L + li * NT + bj];
-            } else if (lon && t < T) {
-                ra = ps[(size_t)(t - Tp) * P + li];
-                rc = mom[(size_t)(t - Tp) * MS + NT + bi * NT + bj];
-            }
-        };
-        constexpr int KD = 3;
-        d4v p1 = {0.0, 0.0, 0.0, 0.0}, p2 = p1, p3 = p1;
-        cd ra[KD], rc[KD];
+                for (int d = 0; d < KD; ++d) raw(4 * d + lk, ra[d], rc[d]);
+                for (int t0 = 0; t0 < Tp; t0 += 4 * KD) {
 #pragma unroll
-        for (int d = 0; d < KD; ++d) raw(4 * d + lk, ra[d], rc[d]);
-        for (int t0 = 0; t0 < T; t0 += 4 * KD) {
-#pragma unroll
-            for (int d = 0; d < KD; ++d) {
-                const int t = t0 + 4 * d + lk;
-                const cd x = t < Tp ? ra[d] : cmul(ra[d], rc[d]);
-                const cd y = cconj(t < Tp ? rc[d] : ra[d]);
-                raw(t + 4 * KD, ra[d], rc[d]);
-                p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, y.x, p1, 0, 0, 0);
-                p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(x.y, y.y, p2, 0, 0, 0);
-                p3 = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x + x.y, y.x + y.y, p3, 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {                // lane holds C[lk + 4v][li]
-            const int p = lk + 4 * v, q = li;
-            if (p < P && q < P) {
-                const cd c = cmk(p1[v] - p2[v], p3[v] - p1[v] - p2[v]);
-                sR[(p * NT + bi) * LDR + q * NT + bj] = c;
-                if (bi != bj) sR[(q * NT + bj) * LDR + p * NT + bi] = cconj(c);
-            }
-        }
-    } else if (GLB) {
-        if (role == NBLK) {
-            // B^H as one more MFMA product, C[p][(a, r)] = sum_v A_v[p] B_v[(a, r)] (columns a NR + r <
-            // NT NR <= 16): data symbols A = psi_t[p], B = m_t[a] conj(y_t[r]); the pilots in NT
-            // passes ap (their u_t[p NT + a] is not a product), A = u_t[p NT + ap], B = conj(y_p,t[r])
-            // in the columns of a = ap.  Virtual symbol v: NT Tp pilot slots, then the data.
-            const int ca = li / NR, cr = li - ca * NR;
-            const bool con = li < NT * NR;
-            const int VP = NT * Tp, V = VP + Td;
-            auto raw = [&](int v, cd& ra, cd& rm, cd& ry) {
-                ra = czero();
-                rm = czero();
-                ry = czero();
-                if (v < VP) {
-                    const int ap = v / Tp, t = v - ap * Tp;
-                    if (lon) ra = up[(size_t)t * L + li * NT + ap];
-                    if (con && ca == ap) {
-                        rm = cmk(1.0, 0.0);
-                        ry = yp[(size_t)t * NR + cr];
-                    }
-                } else if (v < V) {
-                    const int t = v - VP;
-                    if (lon) ra = ps[(size_t)t * P + li];
-                    if (con) {
-                        rm = mom[(size_t)t * MS + ca];
-                        ry = yd[(size_t)t * NR + cr];
+                    for (int d = 0; d < KD; ++d) {
+                        const cd x = ra[d], y = cconj(rc[d]);
+                        raw(t0 + 4 * (KD + d) + lk, ra[d], rc[d]);
+                        mfma3(x, y);
                     }
                 }
-            };
+            }
+            {   // data
+                const cd* pp = ps + lc;
+                const cd* pm = mom + NT + bi * NT + bj;
+                auto raw = [&](int t, cd& x, cd& y) {
+                    const int tt = t < Td ? t : Td - 1;
+                    const bool ok = lon && t < Td;
+                    x = csel(ok, pp[(size_t)tt * P], czero());
+                    y = pm[(size_t)tt * MS];
+                };
+#pragma unroll
+                for (int d = 0; d < KD; ++d) raw(4 * d + lk, ra[d], rc[d]);
+                for (int t0 = 0; t0 < Td; t0 += 4 * KD) {
+#pragma unroll
+                    for (int d = 0; d < KD; ++d) {
+                        const cd x = cmul(ra[d], rc[d]), y = cconj(ra[d]);
+                        raw(t0 + 4 * (KD + d) + lk, ra[d], rc[d]);
+                        mfma3(x, y);
+                    }
+                }
+            }
+        } else if (bh) {
+            // B^H[(p, a)][r] (column a NR + r of a 16 x (NT NR) product): A = psi_t[p] / u_t[p NT +
+            // ap] (one pilot pass per stream ap), B = m_t[a] conj(y_t[r]) / conj(y_p,t[r]) in the
+            // columns of a = ap
             constexpr int KD = 2;
-            d4v p1 = {0.0, 0.0, 0.0, 0.0}, p2 = p1, p3 = p1;
+            const int cc = con ? ca : 0, rc2 = con ? cr : 0;
             cd ra[KD], rm[KD], ry[KD];
+            for (int ap = 0; ap < NT; ++ap) {        // pilots
+                const cd* pa = up + lc * NT + ap;
+                const cd* py = yp + rc2;
+                const bool col_on = con && ca == ap;
+                auto raw = [&](int t, cd& x, cd& m, cd& y) {
+                    const int tt = t < Tp ? t : (Tp > 0 ? Tp - 1 : 0);
+                    const bool ok = t < Tp;
+                    const cd u = Tp > 0 ? pa[(size_t)tt * L] : czero();
+                    const cd yv = Tp > 0 ? py[(size_t)tt * NR] : czero();
+                    x = csel(ok && lon, u, czero());
+                    m = cmk(ok && col_on ? 1.0 : 0.0, 0.0);
+                    y = yv;
+                };
 #pragma unroll
-            for (int d = 0; d < KD; ++d) raw(4 * d + lk, ra[d], rm[d], ry[d]);
-            for (int v0 = 0; v0 < V; v0 += 4 * KD) {
+                for (int d = 0; d < KD; ++d) raw(4 * d + lk, ra[d], rm[d], ry[d]);
+                for (int t0 = 0; t0 < Tp; t0 += 4 * KD) {
 #pragma unroll
-                for (int d = 0; d < KD; ++d) {
-                    const cd x = ra[d];
-                    const cd y = cmulc(rm[d], ry[d]);
-                    raw(v0 + 4 * (KD + d) + lk, ra[d], rm[d], ry[d]);
-                    p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, y.x, p1, 0, 0, 0);
-                    p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(x.y, y.y, p2, 0, 0, 0);
-                    p3 = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x + x.y, y.x + y.y, p3, 0, 0, 0);
-                }
-            }
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {            // lane holds C[lk + 4v][li]
-                const int p = lk + 4 * v;
-                if (p < P && con) sB[(p * NT + ca) * NR + cr] = cmk(p1[v] - p2[v], p3[v] - p1[v] - p2[v]);
-            }
-        }
-    } else if (role < NBLK) {
-        // block (bi, bj) of R, C[p][q] = sum_t x_t[p] y_t[q], lane (li, lk) = (row / column li,
-        // symbol 4s + lk of the chunk's k-step s)
-        const int bi = role >= 1 ? 1 : 0, bj = role == 2 ? 1 : 0;
-        d4v p1 = {0.0, 0.0, 0.0, 0.0}, p2 = p1, p3 = p1;
-        chunks([&](const cd* buf, bool pil, int n) {
-#pragma unroll
-            for (int s4 = 0; s4 < CH / 4; ++s4) {
-                const int tau = 4 * s4 + lk;
-                cd x = czero(), y = czero();
-                if (lon && tau < n) {
-                    if (pil) {
-                        x = buf[tau * L + li * NT + bi];
-                        y = cconj(buf[tau * L + li * NT + bj]);
-                    } else {
-                        const cd psi = buf[tau * P + li];
-                        x = cmul(psi, buf[256 + tau * MS + NT + bi * NT + bj]);
-                        y = cconj(psi);
+                    for (int d = 0; d < KD; ++d) {
+                        const cd x = ra[d], y = cmulc(rm[d], ry[d]);
+                        raw(t0 + 4 * (KD + d) + lk, ra[d], rm[d], ry[d]);
+                        mfma3(x, y);
                     }
                 }
-                p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, y.x, p1, 0, 0, 0);
-                p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(x.y, y.y, p2, 0, 0, 0);
-                p3 = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x + x.y, y.x + y.y, p3, 0, 0, 0);
             }
-        });
-        // every chunk consumed (barrier above): R, aliasing the chunk buffers
+            {   // data
+                const cd* pp = ps + lc;
+                const cd* pm = mom + cc;
+                const cd* py = yd + rc2;
+                auto raw = [&](int t, cd& x, cd& m, cd& y) {
+                    const int tt = t < Td ? t : Td - 1;
+                    const bool ok = t < Td;
+                    x = csel(ok && lon, pp[(size_t)tt * P], czero());
+                    m = csel(ok && con, pm[(size_t)tt * MS], czero());
+                    y = py[(size_t)tt * NR];
+                };
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {                // lane holds C[lk + 4v][li]
-            const int p = lk + 4 * v, q = li;
-            if (p < P && q < P) {
-                const cd c = cmk(p1[v] - p2[v], p3[v] - p1[v] - p2[v]);
-                sR[(p * NT + bi) * LDR + q * NT + bj] = c;
-                if (bi != bj) sR[(q * NT + bj) * LDR + p * NT + bi] = cconj(c);
-            }
-        }
-    } else {
-        // role NBLK: B^H[(p, a)][r] = sum_t w_t[p][a] conj(y_t[r]) on the VALU, lane (li, lk) =
-        // (p, symbol), reduced over lk at the end (w = u_t[p NT + a] or psi_t[p] m_t[a]); other
-        // roles only help stage the chunks
-        const bool bh = role == NBLK;
-        cd acc[NT][NR];
+                for (int d = 0; d < KD; ++d) raw(4 * d + lk, ra[d], rm[d], ry[d]);
+                for (int t0 = 0; t0 < Td; t0 += 4 * KD) {
 #pragma unroll
-        for (int q = 0; q < NT; ++q)
-#pragma unroll
-            for (int r2 = 0; r2 < NR; ++r2) acc[q][r2] = czero();
-        chunks([&](const cd* buf, bool pil, int n) {
-#pragma unroll
-            for (int s4 = 0; s4 < CH / 4; ++s4) {
-                const int tau = 4 * s4 + lk;
-                if (!(bh && lon && tau < n)) continue;
-#pragma unroll
-                for (int q = 0; q < NT; ++q) {
-                    const cd w = pil ? buf[tau * L + li * NT + q]
-                                     : cmul(buf[tau * P + li], buf[256 + tau * MS + q]);
-#pragma unroll
-                    for (int r2 = 0; r2 < NR; ++r2)
-                        acc[q][r2] = cfmac(acc[q][r2], w, buf[(pil ? 512 : 352) + tau * NR + r2]);
+                    for (int d = 0; d < KD; ++d) {
+                        const cd x = ra[d], y = cmulc(rm[d], ry[d]);
+                        raw(t0 + 4 * (KD + d) + lk, ra[d], rm[d], ry[d]);
+                        mfma3(x, y);
+                    }
                 }
             }
-        });
-#pragma unroll
-        for (int q = 0; q < NT; ++q)
-#pragma unroll
-            for (int r2 = 0; r2 < NR; ++r2) {
-                cd v = acc[q][r2];
-                v.x += __shfl_xor(v.x, 16); v.y += __shfl_xor(v.y, 16);
-                v.x += __shfl_xor(v.x, 32); v.y += __shfl_xor(v.y, 32);
-                if (bh && lk == 0 && lon) sB[(li * NT + q) * NR + r2] = v;
-            }
+        }
     }
-    __syncthreads();
-    if (role != 0 || stop == 1) return;              // the solve is one wave's (stop: DIAGNOSTIC)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {                    // lane holds C[lk + 4v][li]
+        const int p = lk + 4 * v, q = li;
+        const cd c = cmk(p1[v] - p2[v], p3[v] - p1[v] - p2[v]);
+        if (role < NBLK && p < P && q < P) {
+            R[(size_t)(p * NT + bi) * L + q * NT + bj] = c;
+            if (bi != bj) R[(size_t)(q * NT + bj) * L + p * NT + bi] = cconj(c);
+        } else if (bh && p < P && con) {
+            rh[(p * NT + ca) * NR + cr] = c;
+        }
+    }
+}
 
-    if (write_sys) {                                 // sbce_mstep's r_out / rhs_out
-        cd* R = a.R + (size_t)b * L * L;
-        for (int e = lane; e < L * L; e += 64) R[e] = sR[(e / L) * LDR + e % L];
-        cd* rh = a.rhs + (size_t)b * L * NR;
-        for (int e = lane; e < L * NR; e += 64) rh[e] = sB[e];
-    }
-    // ---- right-looking Cholesky + forward substitution, lane (r, h): row r, columns 2e + h ----
+template <int NR>
+__global__ __launch_bounds__(64) void mstep_small2_solve_kernel(MstepArgs a, int L, int stop) {
+    const int b = blockIdx.x;
+    if (a.done && a.done[b]) return;
+    const unsigned long long clk0 = __builtin_amdgcn_s_memtime();
+    constexpr int LDR = 33;
+    __shared__ cd sL[32 * LDR];                      // L's rows for the back substitution
+    __shared__ cd colb[2][64];                       // column c (rows 0..31; 32..63 padding)
+    __shared__ double dinv[32];
+    const int lane = threadIdx.x;
+    const bool clk = stop == 4 && b == 0 && lane == 0;
+    const cd* Rg = a.R + (size_t)b * L * L;
+    const cd* rh = a.rhs + (size_t)b * L * NR;
+    // ---- lane (r, h): row r, columns 2e + h -----------------------------------------------------
     const int r = lane & 31, h = lane >> 5;
     const bool rin = r < L;
     cd A[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
         const int j = 2 * e + h;
-        A[e] = (rin && j <= r) ? sR[r * LDR + j] : czero();
+        A[e] = (rin && j <= r) ? Rg[(size_t)r * L + j] : czero();
     }
     cd Y[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const int rr = h + 2 * k;
-        Y[k] = (rin && rr < NR) ? sB[r * NR + rr] : czero();
+        Y[k] = (rin && rr < NR) ? rh[r * NR + rr] : czero();
     }
-    const double tol = 1e-14 * wave_max_dpp((rin && (r & 1) == h) ? sR[r * LDR + r].x : 0.0);
+    double dg = 0.0;                                 // the diagonal, on lane (r, r & 1)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dg = (rin && 2 * e + h == r) ? A[e].x : dg;
+    if (clk) {
+        g_small_clk[0] = clk0;
+        g_small_clk[1] = __builtin_amdgcn_s_memtime();
+    }
+    const double tol = 1e-14 * wave_max_dpp(dg);
     bool anybad = false;
+    if (clk) g_small_clk[2] = __builtin_amdgcn_s_memtime();
+    colb[0][lane] = czero();                         // the padding rows stay finite
+    colb[1][lane] = czero();
+    // The trailing update touches every slot of every lane (no per-slot predicate): the slots
+    // past a row's diagonal and the rows at or above the current column only ever hold products
+    // of bounded factor entries, and nothing reads them -- pivots come from the diagonal slot,
+    // the published column from rows below it, L's stored rows from slots on or below the
+    // diagonal.  Only slot 0 is excluded where it holds a finished column.  ~4 FMAs per slot
+    // instead of ~14 instructions.
+#pragma unroll 1
+    for (int k = 0; 2 * k < L; ++k) {
 #pragma unroll
-    for (int c = 0; c < 32; ++c) {
-        if (c >= L) continue;                        // wave-uniform
-        const int hc = c & 1, ec = c >> 1;
-        const double d = lane_d(A[ec].x, c + 32 * hc);
-        const bool bad = !(d > tol);
-        anybad |= bad;
-        const double pv = bad ? tol : d;
-        const double rs = fast_rsqrt64(pv);
-        const double inv = bad ? 0.0 : rs;           // dropped direction (sbce.h SBCE_SOLVE_CHOL)
-        cd* col = colb[c & 1];
-        if (h == hc) {
-            if (r == c) A[ec] = cmk(bad ? 0.0 : pv * rs, 0.0);
-            else if (r > c) A[ec] = cscale(A[ec], inv);
-            if (r > c) col[r] = A[ec];
-        }
-        if (lane == 0) dinv[c] = inv;
-        if (r == c) {
-            Y[0] = cscale(Y[0], inv);
-            Y[1] = cscale(Y[1], inv);
-        }
-        cd yc[NR];
-#pragma unroll
-        for (int rr = 0; rr < NR; ++rr)
-            yc[rr] = cmk(lane_d(Y[rr >> 1].x, c + 32 * (rr & 1)), lane_d(Y[rr >> 1].y, c + 32 * (rr & 1)));
-        wave_sync();
-        if (rin && r > c) {
-            const cd lr = col[r];
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int j = 2 * e + h;
-                if (j > c && j <= r) A[e] = csub(A[e], cmulc(lr, col[j]));
+        for (int hc = 0; hc < 2; ++hc) {
+            const int c = 2 * k + hc;
+            if (c >= L) break;                       // wave-uniform
+            const double d = lane_d(A[0].x, c + 32 * hc);
+            const bool bad = !(d > tol);
+            anybad |= bad;
+            const double pv = bad ? tol : d;
+            const double rs = fast_rsqrt64(pv);
+            const double inv = bad ? 0.0 : rs;       // dropped direction (sbce.h SBCE_SOLVE_CHOL)
+            cd* col = colb[hc];
+            if (h == hc && r >= c) {
+                const cd v = r == c ? cmk(bad ? 0.0 : pv * rs, 0.0) : cscale(A[0], inv);
+                A[0] = v;
+                if (r > c) col[r] = v;
             }
+            if (lane == 0) dinv[c] = inv;
+            if (r == c) {
+                Y[0] = cscale(Y[0], inv);
+                Y[1] = cscale(Y[1], inv);
+            }
+            cd yc[NR];
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int rr = h + 2 * k;
-                if (rr < NR) Y[k] = csub(Y[k], cmul(lr, rhs_pick(yc, h, k)));
+            for (int rr = 0; rr < NR; ++rr)
+                yc[rr] = cmk(lane_d(Y[rr >> 1].x, c + 32 * (rr & 1)), lane_d(Y[rr >> 1].y, c + 32 * (rr & 1)));
+            wave_sync();
+            const cd lr = col[r];                    // rows <= c: stale, only garbage slots use it
+            const cd* cb = col + 2 * k + h;          // slot e <-> column 2 (k + e) + h
+            // slots past 15 - k hold columns >= 32, past every row: the update runs over the first
+            // 16 / 12 / 8 / 4 slots (a wave-uniform choice of four static slot ranges)
+            auto upd = [&](auto ns) {
+                constexpr int N = decltype(ns)::value;
+                cd cv[N];
+#pragma unroll
+                for (int e = 0; e < N; ++e) cv[e] = cb[2 * e];
+#pragma unroll
+                for (int e = 0; e < N; ++e) {
+                    // slot 0 is column 2k + h: the current column (h == hc) or, at hc = 1, the
+                    // finished column 2k of half 0 -- only at hc = 0 does half 1's slot 0 trail
+                    if (e == 0 && !(hc == 0 && h == 1)) continue;
+                    // A -= lr conj(cv): four FMAs
+                    A[e].x = fma(-lr.x, cv[e].x, A[e].x);
+                    A[e].x = fma(-lr.y, cv[e].y, A[e].x);
+                    A[e].y = fma(-lr.y, cv[e].x, A[e].y);
+                    A[e].y = fma(lr.x, cv[e].y, A[e].y);
+                }
+            };
+            const int emax = 15 - k;
+            if (emax >= 12) upd(std::integral_constant<int, 16>());
+            else if (emax >= 8) upd(std::integral_constant<int, 12>());
+            else if (emax >= 4) upd(std::integral_constant<int, 8>());
+            else upd(std::integral_constant<int, 4>());
+            if (rin && r > c) {
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int rr = h + 2 * q;
+                    if (rr < NR) Y[q] = csub(Y[q], cmul(lr, rhs_pick(yc, h, q)));
+                }
             }
         }
+        if (clk) g_small_clk[3 + k] = __builtin_amdgcn_s_memtime();
+        if (rin && 2 * k + h <= r) sL[r * LDR + 2 * k + h] = A[0];
+#pragma unroll
+        for (int e = 0; e < 15; ++e) A[e] = A[e + 1];
     }
-    if (stop == 2) return;                           // DIAGNOSTIC phase timing (results invalid)
+    if (clk) g_small_clk[40] = __builtin_amdgcn_s_memtime();
     // ---- back substitution L^H x = y: x_c = y_c / l_cc, then y_r -= conj(L[c][r]) x_c, r < c ----
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-        const int j = 2 * e + h;
-        if (rin && j <= r) sR[r * LDR + j] = A[e];
-    }
     wave_sync();
-#pragma unroll
-    for (int c = 31; c >= 0; --c) {
-        if (c >= L) continue;                        // wave-uniform
+#pragma unroll 1
+    for (int c = L - 1; c >= 0; --c) {
         const double iv = dinv[c];
         if (r == c) {
             Y[0] = cscale(Y[0], iv);
@@ -809,15 +762,14 @@ mstep_small2_kernel(MstepArgs a, int P, int Tp, int Td, int L, int write_sys, in
 #pragma unroll
         for (int rr = 0; rr < NR; ++rr)
             xc[rr] = cmk(lane_d(Y[rr >> 1].x, c + 32 * (rr & 1)), lane_d(Y[rr >> 1].y, c + 32 * (rr & 1)));
-        if (r < c) {
-            const cd lcr = sR[c * LDR + r];
+        const cd lcr = sL[c * LDR + (r & 31)];
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int rr = h + 2 * k;
-                if (rr < NR) Y[k] = csub(Y[k], cmulc(rhs_pick(xc, h, k), lcr));
-            }
+        for (int q = 0; q < 2; ++q) {
+            const int rr = h + 2 * q;
+            if (rr < NR) Y[q] = csel(r < c, csub(Y[q], cmulc(rhs_pick(xc, h, q), lcr)), Y[q]);
         }
     }
+    if (clk) g_small_clk[41] = __builtin_amdgcn_s_memtime();
     cd* th = a.theta + (size_t)b * L * NR;
     double nt = 0.0;
 #pragma unroll
@@ -867,6 +819,11 @@ bool mstep_small2_selected(const Problem& pb) {
            g_debug.small_stop != 3 && !g_debug.small_v1;
 }
 
+hipError_t small_debug_clock(unsigned long long* out48) {
+    return hipMemcpyFromSymbol(out48, HIP_SYMBOL(g_small_clk), sizeof(g_small_clk), 0,
+                               hipMemcpyDeviceToHost);
+}
+
 bool mstep_small_supported(const Problem& pb, int solve_mode) {
     return !g_debug.mstep_nosmall && !g_debug.chol_valu && chol_debug_skip_mask() == 0 &&
            (solve_mode == SBCE_SOLVE_CHOL || solve_mode == SBCE_SOLVE_CHOL_DROP) &&
@@ -877,18 +834,28 @@ bool mstep_small_supported(const Problem& pb, int solve_mode) {
 hipError_t launch_mstep_small(const Problem& pb, const MstepArgs& a, bool write_sys, hipStream_t s) {
     const int w = write_sys ? 1 : 0;
     if (mstep_small2_selected(pb)) {
+        // build (R and B^H to the workspace), then the one-wave solve; the early stop (a.h_true)
+        // rides in the solve launch
+        MstepArgs ab = a;
         switch (pb.NT * 8 + pb.NR) {
 #define SBCE_MS2(nt, nr) case nt * 8 + nr: \
-    if (g_debug.small2_lds) \
-        hipLaunchKernelGGL((mstep_small2_kernel<nt, nr, false>), dim3(pb.B), dim3(256), 0, s, a, pb.P, pb.Tp, pb.Td, pb.L, w, g_debug.small_stop); \
-    else \
-        hipLaunchKernelGGL((mstep_small2_kernel<nt, nr, true>), dim3(pb.B), dim3(256), 0, s, a, pb.P, pb.Tp, pb.Td, pb.L, w, g_debug.small_stop); \
-    return hipGetLastError();
+    hipLaunchKernelGGL((mstep_small2_build_kernel<nt, nr>), dim3(pb.B), dim3(256), 0, s, ab, pb.P, pb.Tp, pb.Td, pb.L); \
+    break;
             SBCE_MS2(1, 1) SBCE_MS2(1, 2) SBCE_MS2(1, 3) SBCE_MS2(1, 4)
             SBCE_MS2(2, 1) SBCE_MS2(2, 2) SBCE_MS2(2, 3) SBCE_MS2(2, 4)
 #undef SBCE_MS2
+            default: return hipErrorInvalidValue;
         }
-        return hipErrorInvalidValue;
+        if (g_debug.small_stop == 1) return hipGetLastError();      // DIAGNOSTIC: build only
+        switch (pb.NR) {
+#define SBCE_MS2S(nr) case nr: \
+    hipLaunchKernelGGL((mstep_small2_solve_kernel<nr>), dim3(pb.B), dim3(64), 0, s, a, pb.L, g_debug.small_stop); \
+    break;
+            SBCE_MS2S(1) SBCE_MS2S(2) SBCE_MS2S(3) SBCE_MS2S(4)
+#undef SBCE_MS2S
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
     }
     const int KB = (pb.L + 15) / 16;
     // P <= 16 (BASELINE cfg 5): the MFMA build, R and B^H through LDS; else the VALU build

@@ -236,8 +236,6 @@ struct DebugConfig {
     bool mstep_nosmall;  // SBCE_MSTEP_SMALL=0     L <= 64: the batched build + panel Cholesky instead of
                          //                        the one-workgroup M-step (mstep_small.hip)
     bool small_valu;     // SBCE_MSTEP_SMALL=v     the 256-thread VALU-build kernel also at P <= 16
-    bool small2_lds;     // SBCE_SMALL2_LDS=1      mstep_small2_kernel stages the symbols in LDS chunks
-                         //                        instead of streaming them per wave (A/B; not flagged)
     bool small_v1;       // SBCE_MSTEP_SMALL=1     n_tx <= 2: the round-5 MFMA-build kernel instead of
                          //                        mstep_small2_kernel (A/B; not flagged)
     int small_stop;      // SBCE_SMALL_STOP=1|2|3  DIAGNOSTIC: the one-workgroup M-step stops after its
@@ -412,6 +410,7 @@ bool chol_supported(const Problem& pb);
 // (mstep_small.hip); write_sys also stores R and B^H in a.R / a.rhs (sbce_mstep's outputs)
 bool mstep_small_supported(const Problem& pb, int solve_mode);
 bool mstep_small2_selected(const Problem& pb);   // the launch folds the early stop (a.h_true)
+hipError_t small_debug_clock(unsigned long long* out48);   // SBCE_SMALL_STOP=4 stamps
 hipError_t launch_mstep_small(const Problem& pb, const MstepArgs& a, bool write_sys, hipStream_t s);
 int chol_debug_skip_mask();
 constexpr int kLargeL = 512;   // L above this: tiled build + blocked right-looking Cholesky

@@ -27,7 +27,7 @@ def main():
     batch = {k: np.concatenate([p[k] for p in pts]) for k in ("y_d", "y_p", "psi_d", "u_p", "theta0", "h")}
     batch["cons"] = pts[0]["cons"]
     vt = np.repeat(varn, 64)
-    for arm, env in (("small", {}), ("small_lds", {"SBCE_SMALL2_LDS": "1"}), ("small_v1", {"SBCE_MSTEP_SMALL": "1"}),
+    for arm, env in (("small", {}), ("small_v1", {"SBCE_MSTEP_SMALL": "1"}),
                      ("small_build", {"SBCE_SMALL_STOP": "1"}), ("small_factor", {"SBCE_SMALL_STOP": "2"}),
                      ("batched", {"SBCE_MSTEP_SMALL": "0"})):
         with pkg._lib.debug_env(**env):
