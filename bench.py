@@ -207,6 +207,16 @@ def load_pmc_traffic(path):
         return None
 
 
+def estep_issued(args, config, trials):
+    """Issued FP64 flops of one E-step (tools/sq_issued.sh: SQ instruction counters of the same
+    launches, 64 lanes x VALU FP64 ops + 512 x MFMA_MOPS_F64), or None when the summary is absent
+    or was taken on another configuration / batch."""
+    sq = load_pmc_traffic(args.sq or os.path.join(ROOT, "profiles", f"sq_{config}_latest.json"))
+    if not sq or sq.get("config") != config or sq.get("trials") != trials:
+        return None
+    return sq.get("issued_fp64_flops_per_estep")
+
+
 def kernel_traffic(pmc, kernel):
     """HBM bytes of ONE launch of `kernel` from a PMC summary, or None."""
     k = (pmc or {}).get("kernels", {}).get(kernel)
@@ -416,6 +426,9 @@ def parse_args(argv=None):
                          "barriers, max-over-ranks timing and the accumulator all-reduce only")
     ap.add_argument("--pmc", default=None,
                     help="PMC summary (default: profiles/pmc_<config>_latest.json)")
+    ap.add_argument("--sq", default=None,
+                    help="issued-work SQ summary of the E-step (tools/sq_issued.sh; default: "
+                         "profiles/sq_<config>_latest.json)")
     return ap.parse_args(argv)
 
 
@@ -584,7 +597,9 @@ def grid_roofline(args, g, engines, k_last, torch):
     pmc = load_pmc_traffic(args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}_latest.json"))
     pmc_ok = bool(pmc and pmc.get("config") == args.config and pmc.get("trials") == B)
     ms = phases.get("estep_soft")
-    flops = estep_flops_per_trial_iter(n_tx, n_rx, T_d, M) * B
+    enum_flops = estep_flops_per_trial_iter(n_tx, n_rx, T_d, M) * B
+    issued = estep_issued(args, args.config, B)
+    flops = issued if issued else enum_flops
     algo = estep_bytes_per_trial_iter(n_tx, n_rx, P, T_d) * B
     traffic = phase_traffic(pmc, ESTEP_KERNELS, ESTEP_KERNELS) if pmc_ok else None
     ach = flops / (ms * 1e-3) / 1e12 if ms else None
@@ -593,8 +608,13 @@ def grid_roofline(args, g, engines, k_last, torch):
             "point": {"T_d": T_d, "trials": B, "theta": "h (converged regime)"},
             "ms": ms, "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": ach / FP64_PEAK_TFLOPS if ach else None, "flops_per_launch": flops,
-            "flops_note": "data-independent enumeration work T_d M^n_tx (4 n_rx + 2) per trial; "
-                          "the pruned search issues less",
+            "flops_note": ("FP64 work the launch's kernels ISSUE (SQ counters, "
+                           "profiles/sq_cfg5_latest.json: 64 lanes x VALU FP64 ops + 512 x "
+                           "MFMA_MOPS_F64)" if issued else
+                           "data-independent enumeration work T_d M^n_tx (4 n_rx + 2) per trial; "
+                           "the pruned search issues less"),
+            "enumeration_flops_per_launch": enum_flops,
+            "enumeration_equivalent_tflops": enum_flops / (ms * 1e-3) / 1e12 if ms else None,
             "traffic": traffic, "algorithmic_bytes": algo,
             "traffic_ratio": traffic / algo if traffic else None,
             "hbm_frac_algorithmic": algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS if ms else None}
@@ -966,8 +986,17 @@ def main(argv=None):
         executed = mfma_issued * 2048 if mfma_issued is not None else flops
         # the E-step is a search (tree pass, enumeration, sweep of the listed remainder): its
         # time is set by per-symbol latency, not a pipe's peak; reported for reference
-        estep_roof = {"bound": "latency", "pipe": "FP64 VALU tree search + FP64 MFMA sweep",
+        issued = estep_issued(args, args.config, B)
+        e_ach = issued / (estep_ms * 1e-3) / 1e12 if issued else None
+        estep_roof = {"bound": "fp64 issue" if issued else "latency",
+                      "pipe": "FP64 VALU tree search + FP64 MFMA sweep",
                       "phase": "E-step", "kernels": ESTEP_KERNELS, "ms": estep_ms,
+                      "issued_fp64_flops_per_launch": issued,
+                      "achieved": e_ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                      "frac": e_ach / FP64_PEAK_TFLOPS if e_ach else None,
+                      "issued_note": ("FP64 work the E-step's kernels issue (SQ counters, "
+                                      "profiles/sq_<config>_latest.json: 64 lanes x VALU FP64 ops + "
+                                      "512 x MFMA_MOPS_F64 per launch) / its live time"),
                       "sphere_pass": sphere,
                       "traffic": traffic_of(ESTEP_KERNELS, ESTEP_KERNELS),
                       "sweep_mfma_flops_per_launch": executed,

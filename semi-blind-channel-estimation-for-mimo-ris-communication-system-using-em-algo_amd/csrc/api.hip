@@ -255,9 +255,16 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     const Carve c = carve(pb, solve_mode);
     char* ws = (char*)p->workspace;
     int32_t* done = (int32_t*)(ws + c.done);
-    if (hipMemsetAsync(done, 0, (size_t)pb.B * sizeof(int32_t), s) != hipSuccess) return SBCE_EHIP;
-    if ((rc = status_init(p->status, pb.B, s))) return rc;
     const bool early = p->h_true != nullptr;
+    // L <= 64: the whole M-step in one launch (BASELINE cfg 5: L = 32)
+    const bool small = mstep_small_supported(pb, solve_mode) && !(gauss && pb.NR == 1);
+    // n_tx <= 2 small path: its solve launch zeroes the E-step's list counters for the next
+    // iteration, em_init_kernel for the first -- no counter memset per E-step
+    const bool small2 = small && mstep_small2_selected(pb);
+    int32_t* list_cnt = c.has_prep ? (int32_t*)(ws + c.list) + (size_t)pb.B * pb.Td : nullptr;
+    if ((rc = hip_rc(launch_em_init(pb.B, done, p->status, debug_nondefault() ? SBCE_STATUS_DEBUG : 0,
+                                    small2 ? list_cnt : nullptr, s))))
+        return rc;
 
     EstepArgs ea;
     ea.yd = (const cd*)p->y_d; ea.psid = (const cd*)p->psi_d; ea.theta = (const cd*)p->theta;
@@ -267,6 +274,7 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     ea.prep = c.has_prep ? (double*)(ws + c.prep) : nullptr;
     ea.list = c.has_prep ? (int32_t*)(ws + c.list) : nullptr;
     ea.tree = c.has_prep ? (double*)(ws + c.tree) : nullptr;
+    ea.lists_zeroed = small2 && list_cnt != nullptr;
     MstepArgs ma;
     ma.yd = ea.yd; ma.yp = (const cd*)p->y_p; ma.psid = ea.psid; ma.up = (const cd*)p->u_p;
     ma.mom = ea.mom; ma.R = (cd*)(ws + c.R); ma.rhs = (cd*)(ws + c.rhs); ma.theta = (cd*)p->theta;
@@ -278,10 +286,8 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
     // the Kronecker factors of the pilot regressors do not change across iterations
     const bool prefactor = rbuild_herm_supported(pb);
     if (prefactor && (rc = hip_rc(launch_pilot_factor(pb, ma, s)))) return rc;
-    // L <= 64: the whole M-step in one launch (BASELINE cfg 5: L = 32)
-    const bool small = mstep_small_supported(pb, solve_mode) && !(gauss && pb.NR == 1);
     // the LLF kernel reads theta before the stop decision of the same iteration: no fold with it
-    const bool fold_stop = small && early && !p->llf && mstep_small2_selected(pb);
+    const bool fold_stop = small2 && early && !p->llf;
     for (int it = 0; it < iters; ++it) {
         if (p->x_sup) {
             if ((rc = hip_rc(launch_sup_shift_y(pb, ea.yd, ea.psid, ea.theta, (const cd*)p->x_sup,
@@ -295,6 +301,7 @@ int sbce_em(const sbce_dims* d, const sbce_ptrs* p, int iters, int estep_mode, i
         }
         if (small) {
             MstepArgs ms = ma;
+            if (ea.lists_zeroed) ms.zero_cnt = list_cnt;
             if (fold_stop) {                 // the oracle early stop rides in the M-step launch
                 ms.h_true = (const cd*)p->h_true;
                 ms.done_w = done;

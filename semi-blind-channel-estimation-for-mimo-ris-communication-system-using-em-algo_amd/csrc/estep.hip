@@ -2524,8 +2524,10 @@ hipError_t launch_estep(const Problem& pb, const EstepArgs& a, int mode, hipStre
             hipError_t e = hipErrorInvalidValue;
             if (sphere) {
                 // sphere pass (tree records, enumeration), then the tile bounds of the listed
-                const hipError_t me = hipMemsetAsync(a.list + nsym, 0, 5 * sizeof(int32_t), s);
-                if (me != hipSuccess) return me;
+                if (!a.lists_zeroed) {
+                    const hipError_t me = hipMemsetAsync(a.list + nsym, 0, 5 * sizeof(int32_t), s);
+                    if (me != hipSuccess) return me;
+                }
                 const long nbfs = (nsym + kBfsSpw * kBfsWaves - 1) / (kBfsSpw * kBfsWaves);
                 const dim3 bg((unsigned)nbfs), bblk(64 * kBfsWaves);
                 const bool hard = mode == SBCE_ESTEP_HARD;

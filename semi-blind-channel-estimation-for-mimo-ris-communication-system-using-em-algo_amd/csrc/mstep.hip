@@ -621,6 +621,24 @@ hipError_t launch_llf(const Problem& pb, const cd* theta, const cd* yp, const cd
     return hipGetLastError();
 }
 
+namespace {
+__global__ __launch_bounds__(256) void em_init_kernel(int B, int32_t* done, int32_t* status, int sv,
+                                                      int32_t* cnt) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < B) {
+        done[i] = 0;
+        if (status) status[i] = sv;
+    }
+    if (cnt && i < 5) cnt[i] = 0;
+}
+}  // namespace
+
+hipError_t launch_em_init(int B, int32_t* done, int32_t* status, int sv, int32_t* cnt, hipStream_t s) {
+    hipLaunchKernelGGL(em_init_kernel, dim3((B + 255) / 256 > 0 ? (B + 255) / 256 : 1), dim3(256), 0,
+                       s, B, done, status, sv, cnt);
+    return hipGetLastError();
+}
+
 hipError_t launch_early_stop(const Problem& pb, const cd* theta, const cd* h, int32_t* done,
                              int32_t* iters_done, int it, hipStream_t s) {
     hipLaunchKernelGGL(early_stop_kernel, dim3(pb.B), dim3(256), 0, s, theta, h, done, iters_done,

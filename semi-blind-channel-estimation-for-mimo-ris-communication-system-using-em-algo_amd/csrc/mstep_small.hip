@@ -638,6 +638,8 @@ mstep_small2_build_kernel(MstepArgs a, int P, int Tp, int Td, int L) {
 template <int NR>
 __global__ __launch_bounds__(64) void mstep_small2_solve_kernel(MstepArgs a, int L, int stop) {
     const int b = blockIdx.x;
+    // the next E-step's list counters (its first kernel runs after this launch: stream order)
+    if (a.zero_cnt && b == 0 && threadIdx.x < 5) a.zero_cnt[threadIdx.x] = 0;
     if (a.done && a.done[b]) return;
     const unsigned long long clk0 = __builtin_amdgcn_s_memtime();
     constexpr int LDR = 33;

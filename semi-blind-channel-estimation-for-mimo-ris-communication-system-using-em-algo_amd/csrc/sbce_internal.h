@@ -275,6 +275,8 @@ struct EstepArgs {
                        // null: no sphere
     double* tree;      // [B*Td][32] the sphere pass's per-symbol search-tree records
     const double* varn_t = nullptr;   // [B] per-trial noise variances (sbce_ptrs.varn_t), or null
+    bool lists_zeroed = false;        // the 5 list counters after list[B*Td] are already 0 (zeroed
+                                      // by em_init_kernel / the previous M-step's solve launch)
 };
 
 // The posterior constants of one noise variance v, in the operation order of the host's scalar
@@ -384,6 +386,7 @@ struct MstepArgs {
     int32_t* done_w = nullptr;    // [B] set when |‖theta‖ - ‖h‖| < 1 after iteration it > 0
     int32_t* iters_done = nullptr;
     int it = 0;
+    int32_t* zero_cnt = nullptr;  // the small solve launch zeroes these 5 E-step list counters
 };
 
 // Per-trial extents of one tiled-factorisation launch sequence (mstep_large.hip): column
@@ -465,6 +468,9 @@ hipError_t launch_nmse(const Problem& pb, const cd* theta, const cd* h, double* 
 hipError_t launch_llf(const Problem& pb, const cd* theta, const cd* yp, const cd* up,
                       const cd* yd, const cd* psid, const cd* xd, double* llf, int iters,
                       int it, const int32_t* done, const double* varn_t, hipStream_t s);
+// sbce_em's start in one launch: done[b] = 0, status[b] = status_value, and (cnt) 5 counters = 0
+hipError_t launch_em_init(int B, int32_t* done, int32_t* status, int status_value, int32_t* cnt,
+                          hipStream_t s);
 hipError_t launch_early_stop(const Problem& pb, const cd* theta, const cd* h,
                              int32_t* done, int32_t* iters_done, int it, hipStream_t s);
 
