@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: SBCE_CHOL_GROUP was removed after this A/B, see profiles/r06/chol; git history)
 # A/B of the trial-grouped Cholesky at cfg1 (bench.py default line, 3 stream sub-batches of ~333
 # trials): SBCE_CHOL_GROUP unset / 167 / 111 / 84, each in its own process
 R=${GRAFT_REPO_ROOT:-$(pwd)}
