@@ -413,6 +413,9 @@ def parse_args(argv=None):
     ap.add_argument("--roofline-only", action="store_true",
                     help="cfg5: only the roofline launches (the largest T_d point's E-steps and "
                          "M-step), no grid steps -- for the PMC passes of tools/profile_cfg5.sh")
+    ap.add_argument("--graphs", type=int, default=1,
+                    help="cfg5: each sbce_em call replayed as one captured HIP graph (1, default) "
+                         "or launched eagerly (0)")
     ap.add_argument("--streams", type=int, default=None,
                     help="sub-batches on concurrent HIP streams per GPU (default: 3 at cfg1, else 1)")
     ap.add_argument("--rccl-init", choices=["lazy", "eager"], default="lazy",
@@ -662,6 +665,15 @@ def grid_main(args, ranks, pkg):
     torch.cuda.synchronize()
     streams = [torch.cuda.Stream() for _ in range(3)]
     cur = torch.cuda.current_stream()
+    graphs = None
+    if args.graphs and not args.roofline_only:
+        # every sbce_em call as one captured HIP graph (EMEngine.capture): the grid's 40 calls
+        # launch ~4 kernels per iteration each, and eagerly the host enqueue sets the pace
+        for _, _, _, eng in engines:
+            eng.run(iters)                       # first launches load the code objects
+        torch.cuda.synchronize()
+        graphs = [eng.capture(iters) for _, _, _, eng in engines]
+        torch.cuda.synchronize()
 
     def step():
         ev = torch.cuda.Event()
@@ -669,7 +681,12 @@ def grid_main(args, ranks, pkg):
         for st in streams:
             st.wait_event(ev)
         for i, (_, _, _, eng) in enumerate(engines):
-            eng.run(iters, stream=streams[i % len(streams)])
+            st = streams[i % len(streams)]
+            if graphs is None:
+                eng.run(iters, stream=st)
+            else:
+                with torch.cuda.stream(st):
+                    graphs[i].replay()
         for st in streams:
             cur.wait_stream(st)
 
@@ -720,7 +737,8 @@ def grid_main(args, ranks, pkg):
                    "trials_per_point_per_gpu": B, "em_iters": iters, "detectors": list(dets),
                    "partition_r": g["partition_r"], "solve": "chol", "early_stop": "oracle (h)",
                    "grid_batch": args.grid_batch, "sbce_em_calls_per_step": len(engines),
-                   "streams_per_gpu": len(streams), "parallelism": f"trials-sharded x{world}"},
+                   "streams_per_gpu": len(streams), "hip_graphs": graphs is not None,
+                   "parallelism": f"trials-sharded x{world}"},
         "value_note": ("value counts the trial-iterations the EMs executed (each EM stops at the "
                        "reference's oracle criterion, all_detectorsvsTd.py:87-89 etc.); "
                        f"nominal {nominal * world:.0f} per step (all {iters} iterations), executed "
@@ -821,7 +839,7 @@ def main(argv=None):
     # bounds skip provably negligible tiles): one counted launch outside the timed loops
     mfma_issued = None
     sphere = None
-    lib = pkg._lib.load()
+    lib = pkg._lib.load_ab()          # the counters live in the A/B build (eng.lib inside debug_env)
     if mode in ("soft", "hard") and hasattr(lib, "sbce_debug_estep_mfma"):
         import ctypes
         cnt = ctypes.c_ulonglong(0)

@@ -10,6 +10,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsbce.so")
+# the A/B build (csrc/sbce_internal.h SBCE_AB): the same C-ABI plus the SBCE_* switches; loaded
+# only by debug_env() (tests' cross-checks, tools), never by the product path
+AB_LIB_PATH = os.path.join(_HERE, "libsbce_ab.so")
 
 SBCE_ABI_VERSION = 6
 SBCE_ESTEP_SOFT = 0
@@ -59,6 +62,8 @@ class Ptrs(ctypes.Structure):
 
 
 _lib = None
+_ab = None
+_ab_active = 0
 
 
 def load(path=None):
@@ -71,6 +76,8 @@ def load(path=None):
     and the process would run two HIP runtimes (the second to initialise finds no device:
     hipErrorNoDevice on every launch)."""
     global _lib
+    if path is None and _ab_active:
+        return load_ab()
     if _lib is not None and path is None:
         return _lib
     p = path or LIB_PATH
@@ -112,25 +119,45 @@ def load(path=None):
     return lib
 
 
+def load_ab():
+    """The A/B build libsbce_ab.so (same C-ABI; the SBCE_* switches live only there)."""
+    global _ab
+    if _ab is None:
+        _ab = load(AB_LIB_PATH)
+    return _ab
+
+
+def use_ab():
+    """Route every later load() to the A/B build for the rest of the process (development
+    tools only: A/B arms, counters, clocks)."""
+    global _ab_active
+    _ab_active += 1
+    return load_ab()
+
+
 def reload_debug_env():
-    """Re-read the SBCE_* A/B switches (include/sbce.h SBCE_STATUS_DEBUG) into the loaded
-    library; they are otherwise read once, when libsbce.so is loaded.  Returns True when a
+    """Re-read the SBCE_* A/B switches (include/sbce.h SBCE_STATUS_DEBUG) into the A/B library;
+    they are otherwise read once, when libsbce_ab.so is loaded.  Returns True when a
     result-affecting switch is active."""
-    lib = load()
+    lib = load_ab()
     lib.sbce_debug_reload_env.restype = ctypes.c_int
-    return bool(lib.sbce_debug_reload_env())
+    return lib.sbce_debug_reload_env() == 1
 
 
 @contextlib.contextmanager
 def debug_env(**env):
-    """Run a block with SBCE_* debug switches set (diagnostics and A/B tests only):
-    ``with debug_env(SBCE_ESTEP_IMPL="valu"): ...``; restores the environment after."""
+    """Run a block on the A/B library with SBCE_* debug switches set (diagnostics and A/B tests
+    only): ``with debug_env(SBCE_ESTEP_IMPL="valu"): ...``.  Inside the block load() -- and so
+    every package call and engine made there -- returns libsbce_ab.so; the environment is
+    restored after.  The product library libsbce.so has no switches."""
+    global _ab_active
     old = {k: os.environ.get(k) for k in env}
+    _ab_active += 1
     try:
         for k, v in env.items():
             os.environ[k] = str(v)
         reload_debug_env()
-        yield
+        yield load_ab()
     finally:
         for k, v in old.items():
             if v is None:
@@ -138,6 +165,7 @@ def debug_env(**env):
             else:
                 os.environ[k] = v
         reload_debug_env()
+        _ab_active -= 1
 
 
 def check(rc, what):

@@ -13,11 +13,10 @@ using namespace sbce;
 
 namespace sbce {
 
+#if SBCE_AB
 DebugConfig g_debug;
 
 namespace {
-constexpr DebugConfig kDebugDefault = {false, false, false, false, false, 128, false, false, false,
-                                       true, false, false, false, 0, 0};
 constexpr int kSphereBudgetMax = 256;      // estep.hip kBfsPmax
 
 void read_debug_env(DebugConfig& c) {
@@ -61,6 +60,9 @@ bool debug_nondefault() {
            c.small_valu != d.small_valu || c.small_v1 != d.small_v1 ||
            (chol_debug_skip_mask() & 31);
 }
+#else
+bool debug_nondefault() { return false; }   // the product build has no switch
+#endif
 
 }  // namespace sbce
 
@@ -435,9 +437,14 @@ int sbce_debug_chol_clock(unsigned long long* out32, int reset) {
 // stream); while bits 0-4 are set every trial of every path is flagged SBCE_STATUS_DEBUG.
 // 0 restores normal operation.
 int sbce_debug_chol_skip(int mask) {
+#if SBCE_AB
     if (mask < 0) return SBCE_EINVAL;
     chol_debug_skip(mask);
     return SBCE_OK;
+#else
+    (void)mask;
+    return SBCE_EUNSUPPORTED;                        // libsbce_ab.so only
+#endif
 }
 
 // Diagnostic, not part of include/sbce.h: one piece of the M-step for kernel timing (bench.py's
@@ -502,9 +509,14 @@ int sbce_debug_minnorm_rank(const sbce_dims* d, const sbce_ptrs* p, int32_t* out
 // Diagnostic, not part of include/sbce.h: re-read the SBCE_* debug switches from the
 // environment (they are otherwise read once, when the library is loaded).  Returns 1 when a
 // result-affecting switch is now non-default (every trial is then flagged SBCE_STATUS_DEBUG).
+// The product build has no switches and reads nothing: it returns -1.
 int sbce_debug_reload_env(void) {
+#if SBCE_AB
     read_debug_env(g_debug);
     return debug_nondefault() ? 1 : 0;
+#else
+    return -1;
+#endif
 }
 
 // Diagnostic, not part of include/sbce.h: FP64 MFMAs issued by the exact E-step sweep since

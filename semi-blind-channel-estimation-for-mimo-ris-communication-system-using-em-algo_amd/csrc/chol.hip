@@ -529,8 +529,13 @@ __device__ unsigned long long g_chol_clk[32];
 
 // DIAGNOSTIC phase-skip mask of the Cholesky kernels (timing only, results invalid).  Set
 // only through sbce_debug_chol_skip(); every trial factored while it is nonzero carries
-// SBCE_STATUS_DEBUG, so a result computed with skipped phases can never pass as valid.
+// SBCE_STATUS_DEBUG, so a result computed with skipped phases can never pass as valid.  A/B
+// build only (sbce_internal.h SBCE_AB): the product library's mask is the constant 0.
+#if SBCE_AB
 int g_chol_skip = 0;
+#else
+constexpr int g_chol_skip = 0;
+#endif
 
 // Geometry of one chol_mfma_kernel launch: the factored L x L matrix starts at row/col
 // `off` of trial b's matrix (a.R + b*stride), leading dimension ld.  SOLVE = false
@@ -1527,7 +1532,11 @@ hipError_t chol_debug_clock(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chol_clk), sizeof(g_chol_clk), 0,
                                hipMemcpyDeviceToHost);
 }
+#if SBCE_AB
 void chol_debug_skip(int mask) { g_chol_skip = mask; }
+#else
+void chol_debug_skip(int) {}
+#endif
 int chol_debug_skip_mask() { return g_chol_skip; }
 hipError_t chol_debug_clock_reset() {
     static const unsigned long long z[32] = {0};

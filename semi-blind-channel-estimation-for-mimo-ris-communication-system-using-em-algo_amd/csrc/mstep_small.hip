@@ -16,8 +16,8 @@
 //      double-buffered LDS vector, every other update on the owner's registers;
 //   3. back substitution L^H x = y the same way (row c of L and x_c exchanged); theta = conj(x).
 // Pivot rule and status bits are the batched path's (chol.hip factor_diag): a pivot that is not
-// above tol is flagged (clamp_status); SBCE_SOLVE_CHOL clamps it to tol, CHOL_DROP drops the
-// direction (l_cc = 0, its unknowns 0).
+// above tol is flagged (clamp_status) and its direction dropped (l_cc = 0, its unknowns 0) under
+// SBCE_SOLVE_CHOL and CHOL_DROP alike (include/sbce.h).
 #include <type_traits>
 
 #include "sbce_internal.h"
@@ -753,9 +753,16 @@ __global__ __launch_bounds__(64) void mstep_small2_solve_kernel(MstepArgs a, int
     if (clk) g_small_clk[40] = __builtin_amdgcn_s_memtime();
     // ---- back substitution L^H x = y: x_c = y_c / l_cc, then y_r -= conj(L[c][r]) x_c, r < c ----
     wave_sync();
+    // the next column's 1 / l_cc and L row are read one column ahead (off the x_c chain)
+    double iv_n = dinv[L - 1];
+    cd lcr_n = sL[(L - 1) * LDR + (r & 31)];
 #pragma unroll 1
     for (int c = L - 1; c >= 0; --c) {
-        const double iv = dinv[c];
+        const double iv = iv_n;
+        const cd lcr = lcr_n;
+        const int cp = c > 0 ? c - 1 : 0;
+        iv_n = dinv[cp];
+        lcr_n = sL[cp * LDR + (r & 31)];
         if (r == c) {
             Y[0] = cscale(Y[0], iv);
             Y[1] = cscale(Y[1], iv);
@@ -764,7 +771,6 @@ __global__ __launch_bounds__(64) void mstep_small2_solve_kernel(MstepArgs a, int
 #pragma unroll
         for (int rr = 0; rr < NR; ++rr)
             xc[rr] = cmk(lane_d(Y[rr >> 1].x, c + 32 * (rr & 1)), lane_d(Y[rr >> 1].y, c + 32 * (rr & 1)));
-        const cd lcr = sL[c * LDR + (r & 31)];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int rr = h + 2 * q;

@@ -216,12 +216,18 @@ __device__ __forceinline__ double fast_rsqrt64(double x) {
 
 
 // ------------------------------------------------------------------ debug configuration
-// A/B switches of the development runs (SBCE_* environment variables), read ONCE when the
-// library is loaded (api.hip) and again only through sbce_debug_reload_env(): production
-// launches never consult the environment.  Any result-affecting non-default value makes
-// sbce_em / sbce_mstep / sbce_estep mark every trial SBCE_STATUS_DEBUG.
+// A/B switches of the development runs (SBCE_* environment variables).  They exist only in the
+// A/B build, libsbce_ab.so (compiled with SBCE_AB=1, the tests' and tools' cross-check library):
+// there they are read ONCE when the library is loaded (api.hip) and again only through
+// sbce_debug_reload_env(), and any result-affecting non-default value makes sbce_em /
+// sbce_mstep / sbce_estep mark every trial SBCE_STATUS_DEBUG.  The product library libsbce.so
+// (SBCE_AB=0) has no switch: g_debug is the compile-time default below, every selection on it
+// folds away, and nothing reads the environment.
 // Only the independent cross-check paths the tests compare against stay selectable; the
 // measured-and-rejected schedules of earlier rounds live in git history.
+#ifndef SBCE_AB
+#define SBCE_AB 0
+#endif
 struct DebugConfig {
     bool estep_valu;     // SBCE_ESTEP_IMPL=valu   VALU E-step instead of the MFMA sweep
     bool estep_noprune;  // SBCE_ESTEP_PRUNE=0     no column-tile bounds
@@ -246,7 +252,13 @@ struct DebugConfig {
                          //                        one quad per symbol at any size (all bitwise the
                          //                        same results; not flagged)
 };
+inline constexpr DebugConfig kDebugDefault = {false, false, false, false, false, 128, false, false,
+                                              false, true, false, false, false, 0, 0};
+#if SBCE_AB
 extern DebugConfig g_debug;
+#else
+inline constexpr DebugConfig g_debug = kDebugDefault;
+#endif
 bool debug_nondefault();   // a result-affecting switch differs from its default
 
 // ------------------------------------------------------------------ launch API

@@ -587,7 +587,6 @@ class EMEngine:
         the iterations each trial of the last run() performed."""
         torch = _torch()
         self.torch = torch
-        self.lib = _lib.load()
 
         def dev(x):
             if x is None:
@@ -686,6 +685,23 @@ class EMEngine:
             cur.wait_stream(st)
         return self.theta
 
+    def capture(self, itera, stream=None):
+        """run(itera) captured as ONE HIP graph (stream capture through torch.cuda.CUDAGraph; the
+        library's launches on the capturing stream are recorded like torch's own).  sbce_em's
+        launch sequence is fixed by the shapes -- the early stop and the sphere pass's work lists
+        are device-side -- so ``graph.replay()`` (on the current stream) reruns the whole EM on
+        this engine's buffers: one host launch instead of ~4 per iteration, for the sweep grids'
+        many small calls, which are host-launch-bound otherwise.  Call run() once before (the
+        first launch of each kernel loads its code object)."""
+        torch = self.torch
+        g = torch.cuda.CUDAGraph()
+        side = stream if stream is not None else torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.graph(g, stream=side):
+            self.run(itera)
+        torch.cuda.current_stream().wait_stream(side)
+        return g
+
     def estep(self):
         """One E-step launch over the batch from the current theta (for kernel timing)."""
         rc = self.lib.sbce_estep(self.dims, self.ptrs, self.mode, self.mom.data_ptr(),
@@ -698,6 +714,12 @@ class EMEngine:
                                  None, self.torch.cuda.current_stream().cuda_stream)
         _lib.check(rc, "sbce_mstep")
         self._minnorm_ws = self.solve == _lib.SBCE_SOLVE_MINNORM
+
+    @property
+    def lib(self):
+        """libsbce.so -- or libsbce_ab.so inside _lib.debug_env() (A/B and counter runs on the
+        same device state: one C-ABI, the workspace carve is the same code)."""
+        return _lib.load()
 
     def mstep_phase(self, phase):
         """One piece of the M-step from the last moments (kernel timing, sbce_debug_mstep_phase):

@@ -4,6 +4,7 @@ validation works without touching a GPU."""
 import ctypes
 import os
 import re
+import shutil
 import subprocess
 
 import pytest
@@ -28,6 +29,27 @@ def test_library_exports_every_declared_symbol(sbce):
         assert hasattr(lib, name), name
     assert lib.sbce_abi_version() == sbce._lib.SBCE_ABI_VERSION
     assert lib.sbce_strerror(-1)
+
+
+def test_product_library_has_no_switches_and_ab_build_has_same_abi(sbce):
+    """The product library reads no environment (no getenv import, sbce_debug_reload_env -1,
+    the skip mask refused); the A/B build (csrc/sbce_internal.h SBCE_AB) exports the same
+    C-ABI and reads its SBCE_* switches."""
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    def undef(path):
+        out = subprocess.run([nm, "-D", "--undefined-only", path], capture_output=True,
+                             text=True, check=True).stdout
+        return {ln.split()[-1].split("@")[0] for ln in out.splitlines() if ln.strip()}
+    assert "getenv" not in undef(sbce._lib.LIB_PATH)
+    assert "getenv" in undef(sbce._lib.AB_LIB_PATH)
+    prod, ab = sbce._lib.load(), sbce._lib.load_ab()
+    assert prod is not ab
+    for name in _declared():
+        assert hasattr(ab, name), name
+    assert ab.sbce_abi_version() == sbce._lib.SBCE_ABI_VERSION
+    assert prod.sbce_debug_reload_env() == -1
+    assert prod.sbce_debug_chol_skip(8) == -2
+    assert ab.sbce_debug_reload_env() == 0         # no switch set here: defaults
 
 
 def test_struct_layout_matches_c(sbce, tmp_path):

@@ -272,7 +272,7 @@ def test_sphere_estep_cfg1_geometry(sbce, snr):
     import ctypes
     varn = float(sbce.signal_model.snr_to_varn(snr))
     b = sbce.signal_model.synthetic_batch(4, 4, 4, 64, 16, 64, 16, varn, seed=5 + snr)
-    lib = sbce._lib.load()
+    lib = sbce._lib.load_ab()                     # the counters live in the A/B build
     scale = np.abs(b["cons"]).max() ** 2
     for th in (b["theta0"], b["h"] + 0.05 * b["theta0"] / np.abs(b["theta0"]).max()):
         res = {}
@@ -938,47 +938,55 @@ def test_engine_matches_em_batch_superimposed_and_gauss(sbce):
     assert np.array_equal(eng.run(2).cpu().numpy(), ref["theta"])
 
 
-def test_debug_switches_are_read_once_and_flag_status(sbce):
-    """Production launches never consult the environment: an SBCE_* switch set after the
-    library loaded changes nothing until sbce_debug_reload_env(), and while a
-    result-affecting switch is active every trial carries SBCE_STATUS_DEBUG."""
+def test_debug_switches_exist_only_in_the_ab_build_and_flag_status(sbce):
+    """The product library libsbce.so has no SBCE_* switch: an SBCE_* variable changes
+    nothing, and its sbce_debug_reload_env reads nothing (-1).  The A/B build libsbce_ab.so
+    (_lib.debug_env) reads them, and while a result-affecting switch is active every trial
+    carries SBCE_STATUS_DEBUG."""
     import os
     b = sbce.signal_model.synthetic_batch(2, 2, 2, 6, 8, 20, 16, 0.2, seed=3)
     args = (b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], 0.2, 2, b["theta0"])
     r0 = sbce.em_batch(*args)
     assert not (r0["status"] & sbce._lib.SBCE_STATUS_DEBUG).any()
+    prod = sbce._lib.load()
+    assert prod is not sbce._lib.load_ab()
     os.environ["SBCE_CHOL_IMPL"] = "valu"
     try:
-        r1 = sbce.em_batch(*args)                 # not reloaded: default kernels, no flag
+        assert prod.sbce_debug_reload_env() == -1
+        r1 = sbce.em_batch(*args)                 # product: the variable is never read
         assert np.array_equal(r1["theta"], r0["theta"]) and not r1["status"].any()
     finally:
         del os.environ["SBCE_CHOL_IMPL"]
-    with sbce._lib.debug_env(SBCE_CHOL_IMPL="valu"):
+    with sbce._lib.debug_env(SBCE_CHOL_IMPL="valu") as ab:
+        assert sbce._lib.load() is ab
         r2 = sbce.em_batch(*args)
     assert (r2["status"] & sbce._lib.SBCE_STATUS_DEBUG).all()
     assert rel(r2["theta"], r0["theta"]) < 1e-9
+    with sbce._lib.debug_env():                   # the A/B build at its defaults: the product's bits
+        r4 = sbce.em_batch(*args)
+    assert np.array_equal(r4["theta"], r0["theta"]) and not r4["status"].any()
     r3 = sbce.em_batch(*args)
     assert np.array_equal(r3["theta"], r0["theta"]) and not r3["status"].any()
 
 
 def test_debug_skip_mask_flags_every_trial(sbce):
-    """A diagnostic Cholesky phase-skip mask (results invalid) can only be set through
-    sbce_debug_chol_skip and marks every trial SBCE_STATUS_DEBUG; 0 restores valid runs."""
+    """A diagnostic Cholesky phase-skip mask (results invalid) exists only in the A/B build,
+    is set only through sbce_debug_chol_skip and marks every trial SBCE_STATUS_DEBUG; 0
+    restores valid runs.  The product library refuses it (SBCE_EUNSUPPORTED)."""
     varn = 0.1
     b = sbce.signal_model.synthetic_batch(4, 4, 4, 8, 16, 40, 4, varn, seed=1)
-    lib = sbce._lib.load()
-    good = sbce.em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, 2,
-                         b["theta0"])
+    args = (b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, 2, b["theta0"])
+    assert sbce._lib.load().sbce_debug_chol_skip(8) == -2
+    good = sbce.em_batch(*args)
     assert not (good["status"] & sbce._lib.SBCE_STATUS_DEBUG).any()
-    try:
-        assert lib.sbce_debug_chol_skip(8) == 0
-        bad = sbce.em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, 2,
-                            b["theta0"])
-    finally:
-        lib.sbce_debug_chol_skip(0)
+    with sbce._lib.debug_env() as lib:
+        try:
+            assert lib.sbce_debug_chol_skip(8) == 0
+            bad = sbce.em_batch(*args)
+        finally:
+            lib.sbce_debug_chol_skip(0)
+        again = sbce.em_batch(*args)
     assert (bad["status"] & sbce._lib.SBCE_STATUS_DEBUG).all()
-    again = sbce.em_batch(b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], varn, 2,
-                          b["theta0"])
     assert np.array_equal(again["theta"], good["theta"]) and not again["status"].any()
 
 

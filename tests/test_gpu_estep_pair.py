@@ -22,7 +22,7 @@ def _torch_first():
 
 
 def _run(sbce, b, th, varn, pair):
-    lib = sbce._lib.load()
+    lib = sbce._lib.load_ab()           # the counters live in the A/B build
     with sbce._lib.debug_env(SBCE_ESTEP_PAIR=pair, SBCE_ESTEP_COUNT="1"):
         lib.sbce_debug_estep_sphere(None, 1)
         lib.sbce_debug_estep_pair(None, 1)
@@ -86,7 +86,7 @@ def test_pair_estep_full_em_low_snr_vs_oracle(sbce):
 
 
 def _run_nt(sbce, b, th, varn, pair, n_tx):
-    lib = sbce._lib.load()
+    lib = sbce._lib.load_ab()           # the counters live in the A/B build
     with sbce._lib.debug_env(SBCE_ESTEP_PAIR=pair, SBCE_ESTEP_COUNT="1"):
         lib.sbce_debug_estep_pair(None, 1)
         m, S = sbce.estep_batch(b["y_d"], b["psi_d"], b["cons"], th, varn, n_tx)
@@ -134,7 +134,7 @@ def test_hard2_estep_nt2_matches_enumeration_and_oracle(sbce, n_rx, M, snr):
     b = sbce.signal_model.synthetic_batch(3, 2, n_rx, 15, 20, 60, M, varn, seed=80 + snr + n_rx,
                                           pinv="scipy")
     aps = sbce.qam.all_possible_symbols(b["cons"], 2)
-    lib = sbce._lib.load()
+    lib = sbce._lib.load_ab()           # the counters live in the A/B build
     for th in (b["theta0"], b["h"] + 0.05 * b["theta0"] / np.abs(b["theta0"]).max()):
         out = {}
         for pair in ("1", "0"):

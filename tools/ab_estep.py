@@ -12,6 +12,7 @@ import torch  # noqa: E402
 import __graft_entry__ as ge  # noqa: E402
 
 pkg = ge.package()
+pkg._lib.use_ab()       # the A/B build: SBCE_* switches, counters, clocks
 snr = float(os.environ.get("SNR", "20"))
 varn = float(pkg.signal_model.snr_to_varn(snr))
 batch = pkg.signal_model.synthetic_batch(1000, 4, 4, 64, 16, 256, 16, varn, seed=0)

@@ -21,6 +21,7 @@ def main():
     import torch
     import __graft_entry__ as ge
     pkg = ge.package()
+    pkg._lib.use_ab()       # the A/B build: SBCE_* switches, counters, clocks
     varn = float(pkg.signal_model.snr_to_varn(20.0))
     b = pkg.signal_model.synthetic_batch(a.trials, 8, 8, 256, 32, 1024, 16, varn, seed=0)
     eng = pkg.EMEngine(b, varn, mode="pm_soft", partition_r=1, solve="lstsq")

@@ -20,6 +20,7 @@ def main():
     import torch
     import __graft_entry__ as ge
     pkg = ge.package()
+    pkg._lib.use_ab()       # the A/B build: SBCE_* switches, counters, clocks
     varn = float(pkg.signal_model.snr_to_varn(20.0))
     b = pkg.signal_model.synthetic_batch(1000, 4, 4, 64, 16, 256, 16, varn, seed=0)
     res = {}

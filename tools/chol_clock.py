@@ -10,6 +10,7 @@ import torch  # noqa: E402
 import __graft_entry__ as ge  # noqa: E402
 
 pkg = ge.package()
+pkg._lib.use_ab()       # the A/B build: SBCE_* switches, counters, clocks
 LIB = pkg._lib.load()
 B = int(os.environ.get("B", "1000"))
 varn = float(pkg.signal_model.snr_to_varn(20.0))

@@ -3,6 +3,7 @@ sys.path.insert(0, os.getcwd())
 import numpy as np
 import __graft_entry__ as ge
 sbce = ge.package()
+sbce._lib.use_ab()       # the A/B build: SBCE_* switches, counters, clocks
 order = sys.argv[1]
 b = sbce.signal_model.synthetic_batch(2, 2, 2, 8, 12, 40, 4, 0.05, seed=4)
 x = b["x_d"]; S = x[..., :, None] * np.conj(x[..., None, :]) + 0.1 * np.eye(2)

@@ -8,6 +8,7 @@ sys.path.insert(0, ".")
 import __graft_entry__ as ge  # noqa: E402
 
 pkg = ge.package()
+pkg._lib.use_ab()       # the A/B build: SBCE_* switches, counters, clocks
 d = np.load("tools/data/cfg5_nan_trial.npz")
 vn = float(d["varn"])
 for name, env in (("default", {}), ("sweep_only", dict(SBCE_ESTEP_SPHERE="0")),

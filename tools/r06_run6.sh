@@ -1,0 +1,7 @@
+#!/bin/bash
+# small M-step solve look-ahead: targeted GPU tests, then the A/B timing and the solve clocks
+O=gpurun_out/r06_la; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_em.py -m gpu -x -q --timeout 120 --timeout-method thread -k "small or rank_deficient or cfg5 or root_td" > $O/tests.log 2>&1 || exit $?
+timeout -k 10 180 python tools/ab_small.py 120 > $O/ab120.log 2>&1 &&
+timeout -k 10 180 python tools/ab_small.py 15 > $O/ab15.log 2>&1 &&
+timeout -k 10 120 python tools/small_clock.py 120 > $O/clock.log 2>&1

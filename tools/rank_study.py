@@ -33,6 +33,7 @@ def main():
     import __graft_entry__ as ge
     from oracle.em_reduced import mstep_lstsq, nmse
     pkg = ge.package()
+    pkg._lib.use_ab()       # the A/B build: SBCE_* switches, counters, clocks
     n_tx, n_rx, N, T_p, T_d, M = 8, 8, 256, 32, 1024, 16
     varn = float(pkg.signal_model.snr_to_varn(20.0))
     b = pkg.signal_model.synthetic_batch(a.trials, n_tx, n_rx, N, T_p, T_d, M, varn, seed=a.seed)

@@ -11,6 +11,7 @@ import torch  # noqa: E402
 import __graft_entry__ as ge  # noqa: E402
 
 pkg = ge.package()
+pkg._lib.use_ab()       # the A/B build: SBCE_* switches, counters, clocks
 B = int(os.environ.get("B", "1000"))
 varn = float(pkg.signal_model.snr_to_varn(float(os.environ.get("SNR", "20"))))
 batch = pkg.signal_model.synthetic_batch(B, 4, 4, 64, 16, 256, 16, varn, seed=0)

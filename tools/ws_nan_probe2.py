@@ -9,6 +9,7 @@ sys.path.insert(0, ".")
 import __graft_entry__ as ge  # noqa: E402
 
 pkg = ge.package()
+pkg._lib.use_ab()       # the A/B build: SBCE_* switches, counters, clocks
 L_ = pkg._lib
 n_tx, n_rx, N, T_p, T_d, M = 4, 4, 149, 16, 200, 16
 solve = sys.argv[1] if len(sys.argv) > 1 else "chol"
