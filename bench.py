@@ -416,6 +416,9 @@ def parse_args(argv=None):
     ap.add_argument("--graphs", type=int, default=1,
                     help="cfg5: each sbce_em call replayed as one captured HIP graph (1, default) "
                          "or launched eagerly (0)")
+    ap.add_argument("--schedule", choices=("lpt", "rr"), default="lpt",
+                    help="cfg5: calls onto streams longest-first to the least loaded (lpt, by each "
+                         "call's measured time) or round robin in grid order (rr)")
     ap.add_argument("--streams", type=int, default=None,
                     help="sub-batches on concurrent HIP streams per GPU (default: 3 at cfg1, else 1)")
     ap.add_argument("--rccl-init", choices=["lazy", "eager"], default="lazy",
@@ -626,7 +629,7 @@ def grid_roofline(args, g, engines, k_last, torch):
 
 def grid_main(args, ranks, pkg):
     """--config cfg5: one step = the whole SNR x T_d grid, five detector EMs per point, `trials`
-    Monte-Carlo trials per point on every rank.  Calls are spread over 3 HIP streams.  value =
+    Monte-Carlo trials per point on every rank.  Calls are spread over 3 HIP streams (--streams), each a captured HIP graph (--graphs), longest first onto the least loaded stream (--schedule lpt).  value =
     trial-iterations EXECUTED (the oracle early stop ends a trial's EM; iters_done) / time."""
     import torch
     g = dict(GRID[args.config])
@@ -663,7 +666,7 @@ def grid_main(args, ranks, pkg):
                 engines.append((di, k, js, eng))
         del pts
     torch.cuda.synchronize()
-    streams = [torch.cuda.Stream() for _ in range(3)]
+    streams = [torch.cuda.Stream() for _ in range(args.streams or 3)]
     cur = torch.cuda.current_stream()
     graphs = None
     if args.graphs and not args.roofline_only:
@@ -674,19 +677,45 @@ def grid_main(args, ranks, pkg):
         torch.cuda.synchronize()
         graphs = [eng.capture(iters) for _, _, _, eng in engines]
         torch.cuda.synchronize()
+    # which stream runs which call: round robin in grid order, or longest-first onto the least
+    # loaded stream (LPT) by each call's time measured alone (one untimed replay each)
+    order = [[i for i in range(len(engines)) if i % len(streams) == s] for s in range(len(streams))]
+    call_ms = None
+    if args.schedule == "lpt":
+        call_ms = []
+        for i, (_, _, _, eng) in enumerate(engines):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cur)
+            if graphs is None:
+                eng.run(iters)
+            else:
+                graphs[i].replay()
+            e1.record(cur)
+            torch.cuda.synchronize()
+            call_ms.append(e0.elapsed_time(e1))
+        load = [0.0] * len(streams)
+        order = [[] for _ in streams]
+        for i in sorted(range(len(engines)), key=lambda i: -call_ms[i]):
+            s_min = min(range(len(streams)), key=lambda s: load[s])
+            order[s_min].append(i)
+            load[s_min] += call_ms[i]
 
     def step():
         ev = torch.cuda.Event()
         ev.record(cur)
         for st in streams:
             st.wait_event(ev)
-        for i, (_, _, _, eng) in enumerate(engines):
-            st = streams[i % len(streams)]
-            if graphs is None:
-                eng.run(iters, stream=st)
-            else:
-                with torch.cuda.stream(st):
-                    graphs[i].replay()
+        # calls are issued interleaved over the streams (the host enqueue never starves one)
+        for r in range(max(len(o) for o in order)):
+            for st, o in zip(streams, order):
+                if r >= len(o):
+                    continue
+                i = o[r]
+                if graphs is None:
+                    engines[i][3].run(iters, stream=st)
+                else:
+                    with torch.cuda.stream(st):
+                        graphs[i].replay()
         for st in streams:
             cur.wait_stream(st)
 
@@ -738,6 +767,8 @@ def grid_main(args, ranks, pkg):
                    "partition_r": g["partition_r"], "solve": "chol", "early_stop": "oracle (h)",
                    "grid_batch": args.grid_batch, "sbce_em_calls_per_step": len(engines),
                    "streams_per_gpu": len(streams), "hip_graphs": graphs is not None,
+                   "schedule": args.schedule,
+                   "call_ms_sum": None if call_ms is None else float(sum(call_ms)),
                    "parallelism": f"trials-sharded x{world}"},
         "value_note": ("value counts the trial-iterations the EMs executed (each EM stops at the "
                        "reference's oracle criterion, all_detectorsvsTd.py:87-89 etc.); "

@@ -42,6 +42,7 @@ void read_debug_env(DebugConfig& c) {
         c.small_v1 = v[0] == '1';
     }
     if ((v = env("SBCE_PM_IMPL"))) c.pm_impl = (v[0] == 'w' || v[0] == 't' || v[0] == 'q') ? v[0] : 0;
+    if ((v = env("SBCE_SMALL_SOLVE"))) c.small_col = v[0] == 'c';
     if ((v = env("SBCE_SMALL_STOP"))) c.small_stop = (v[0] >= '1' && v[0] <= '4') ? v[0] - '0' : 0;
 }
 
@@ -57,7 +58,7 @@ bool debug_nondefault() {
            c.backsub_general != d.backsub_general || c.chol_valu != d.chol_valu ||
            c.estep_nopair != d.estep_nopair || c.cplx3 != d.cplx3 ||
            c.mstep_nosmall != d.mstep_nosmall || c.small_stop != d.small_stop ||
-           c.small_valu != d.small_valu || c.small_v1 != d.small_v1 ||
+           c.small_valu != d.small_valu || c.small_v1 != d.small_v1 || c.small_col != d.small_col ||
            (chol_debug_skip_mask() & 31);
 }
 #else

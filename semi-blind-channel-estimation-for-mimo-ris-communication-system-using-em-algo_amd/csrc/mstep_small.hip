@@ -458,7 +458,10 @@ mstep_small5_kernel(MstepArgs a, int NT, int P, int Tp, int Td, int L, int write
 //           values of the next k-steps in flight (a staging of the symbols in LDS by 16-symbol
 //           chunks, one barrier per chunk, measured slower: 113.6 vs 98.8 us at T_d = 120);
 //           R (full) and B^H to the workspace, no barrier;
-//   solve   (mstep_small2_solve_kernel, ONE wave per trial, no occupancy cap: the row registers,
+//   solve   (mstep_small3_solve_kernel below by default -- 4-column panels, MFMA trailing
+//           updates; this column-by-column mstep_small2_solve_kernel with SBCE_SMALL_SOLVE=col in
+//           the A/B build)
+//           (mstep_small2_solve_kernel, ONE wave per trial, no occupancy cap: the row registers,
 //           the column values and the right-hand sides stay in VGPRs -- at the build's 96-VGPR
 //           cap they went to scratch, one memory round trip per column) right-looking Cholesky
 //           with the forward substitution fused, lane (r, h) holding row r's columns 2e + h, a
@@ -802,6 +805,216 @@ __global__ __launch_bounds__(64) void mstep_small2_solve_kernel(MstepArgs a, int
     if (lane == 0 && a.status && anybad) a.status[b] |= a.clamp_status;
 }
 
+// Blocked variant of the solve (round 6, the default): the column kernel above issues ~250
+// instructions per column (64 FMAs of trailing update + the slot bookkeeping) and is issue-bound
+// at ~1250 cycles a column.  Here the trailing matrix lives in MFMA accumulator layout -- the
+// lower 16 x 16 tiles (0,0), (1,0), (1,1) of R, lane (li, lk) holding C[lk + 4v][li] -- and the
+// factorisation goes by panels of 4 columns:
+//   1. the panel's 4 columns leave the accumulators through LDS (P[row][j]) and land one row
+//      per lane (rows on lanes 0..31, mirrored on 32..63, which carry the other right-hand
+//      sides: lane (r, h) holds y's components h, h + 2 of row r);
+//   2. 4 columns factored there: pivot by v_readlane, l_{rc} = a_{rc} / sqrt(d), the panel's
+//      later columns updated with l_{c+j,c} by v_readlane, y forward-substituted (y_c by
+//      v_readlane); L's rows to LDS (sL) for the back substitution;
+//   3. the trailing tiles updated by the panel: C -= L_p L_p^H as four real
+//      v_mfma_f64_16x16x4f64 per tile (k = the panel's 4 columns), operands from LDS.
+// Entries above the trailing part (finished rows / columns) take garbage updates that nothing
+// reads, as in the column kernel.  Pivot rule, dropped directions, status, the early stop, the
+// back substitution and theta are the column kernel's.
+template <int NR>
+__global__ __launch_bounds__(64) void mstep_small3_solve_kernel(MstepArgs a, int L, int stop) {
+    const int b = blockIdx.x;
+    if (a.zero_cnt && b == 0 && threadIdx.x < 5) a.zero_cnt[threadIdx.x] = 0;
+    if (a.done && a.done[b]) return;
+    const unsigned long long clk0 = __builtin_amdgcn_s_memtime();
+    constexpr int LDR = 33;
+    __shared__ cd sL[32 * LDR];                      // L's rows for the back substitution
+    __shared__ cd P[32 * 4];                         // the panel, row-major
+    __shared__ double dinv[32];
+    const int lane = threadIdx.x;
+    const bool clk = stop == 4 && b == 0 && lane == 0;
+    const cd* Rg = a.R + (size_t)b * L * L;
+    const cd* rh = a.rhs + (size_t)b * L * NR;
+    const int li = lane & 15, lk = lane >> 4;
+    // ---- trailing matrix: tiles (0,0), (1,0), (1,1) as [re, im] accumulators --------------------
+    d4v cre[3], cim[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        const int ti = t == 0 ? 0 : 1, tj = t == 2 ? 1 : 0;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int rr = 16 * ti + lk + 4 * v, cc = 16 * tj + li;
+            const cd x = (rr < L && cc < L) ? Rg[(size_t)rr * L + cc] : czero();
+            cre[t][v] = x.x;
+            cim[t][v] = x.y;
+        }
+    }
+    // ---- lane (r, h): row r of the panel, y components h, h + 2 ----------------------------------
+    const int r = lane & 31, h = lane >> 5;
+    const bool rin = r < L;
+    cd Y[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int rr = h + 2 * k;
+        Y[k] = (rin && rr < NR) ? rh[r * NR + rr] : czero();
+    }
+    // tol = 1e-14 max diag R: the diagonal sits in tiles 0 and 2 at lane li = lk + 4v
+    double dg = 0.0;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const bool on = li == lk + 4 * v;
+        dg = fmax(dg, on && lk + 4 * v < L ? cre[0][v] : 0.0);
+        dg = fmax(dg, on && 16 + lk + 4 * v < L ? cre[2][v] : 0.0);
+    }
+    if (clk) {
+        g_small_clk[0] = clk0;
+        g_small_clk[1] = __builtin_amdgcn_s_memtime();
+    }
+    const double tol = 1e-14 * wave_max_dpp(dg);
+    bool anybad = false;
+    if (clk) g_small_clk[2] = __builtin_amdgcn_s_memtime();
+#pragma unroll 1
+    for (int p = 0; 4 * p < L; ++p) {
+        const int c0 = 4 * p;
+        const bool lo = c0 < 16;                     // wave-uniform: the panel's tile column
+        const int lc0 = c0 & 15;
+        // 1. the panel's columns out of the accumulators: lanes li in [lc0, lc0 + 4)
+        if (li >= lc0 && li < lc0 + 4) {
+            const int j = li - lc0;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int rr = lk + 4 * v;
+                if (lo) {
+                    P[rr * 4 + j] = cmk(cre[0][v], cim[0][v]);
+                    P[(16 + rr) * 4 + j] = cmk(cre[1][v], cim[1][v]);
+                } else {
+                    P[(16 + rr) * 4 + j] = cmk(cre[2][v], cim[2][v]);
+                }
+            }
+        }
+        wave_sync();
+        cd pv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pv[j] = P[r * 4 + j];
+        // 2. factor the panel's columns (rows >= c meaningful), forward substitution
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = c0 + j;
+            if (c < L) {                             // wave-uniform
+            const double d = lane_d(pv[j].x, c);
+            const bool bad = !(d > tol);
+            anybad |= bad;
+            const double pvt = bad ? tol : d;
+            const double rs = fast_rsqrt64(pvt);
+            const double inv = bad ? 0.0 : rs;       // dropped direction (sbce.h SBCE_SOLVE_CHOL)
+            pv[j] = r == c ? cmk(bad ? 0.0 : pvt * rs, 0.0) : cscale(pv[j], inv);
+            if (lane == 0) dinv[c] = inv;
+            if (r == c) {
+                Y[0] = cscale(Y[0], inv);
+                Y[1] = cscale(Y[1], inv);
+            }
+            cd yc[NR];
+#pragma unroll
+            for (int rr = 0; rr < NR; ++rr)
+                yc[rr] = cmk(lane_d(Y[rr >> 1].x, c + 32 * (rr & 1)), lane_d(Y[rr >> 1].y, c + 32 * (rr & 1)));
+            if (rin && r > c) {
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int rr = h + 2 * q;
+                    if (rr < NR) Y[q] = csub(Y[q], cmul(pv[j], rhs_pick(yc, h, q)));
+                }
+            }
+            // the panel's later columns: a_{r,c'} -= l_{r,c} conj(l_{c',c})
+#pragma unroll
+            for (int j2 = j + 1; j2 < 4; ++j2) {
+                const cd cv = cmk(lane_d(pv[j].x, c0 + j2), lane_d(pv[j].y, c0 + j2));
+                pv[j2].x = fma(-pv[j].x, cv.x, pv[j2].x);
+                pv[j2].x = fma(-pv[j].y, cv.y, pv[j2].x);
+                pv[j2].y = fma(-pv[j].y, cv.x, pv[j2].y);
+                pv[j2].y = fma(pv[j].x, cv.y, pv[j2].y);
+            }
+            }
+        }
+        if (clk) g_small_clk[3 + p] = __builtin_amdgcn_s_memtime();
+        // L's rows for the back substitution; the panel (rows >= c0, zero above) for the MFMAs
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = c0 + j;
+            if (h == 0 && rin && c < L && r >= c) sL[r * LDR + c] = pv[j];
+        }
+        if (4 * (p + 1) >= L) break;                 // wave-uniform: no trailing part left
+        wave_sync();
+        if (h == 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) P[r * 4 + j] = r >= c0 + j ? pv[j] : czero();
+        }
+        wave_sync();
+        // 3. trailing tiles -= L_p L_p^H: lane (li, lk) feeds L_p[16 t + li][lk] to both operands
+        const cd x0 = P[li * 4 + lk], x1 = P[(16 + li) * 4 + lk];
+        auto upd = [&](int t, cd xa, cd xb) {
+            cre[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-xa.x, xb.x, cre[t], 0, 0, 0);
+            cre[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-xa.y, xb.y, cre[t], 0, 0, 0);
+            cim[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-xa.y, xb.x, cim[t], 0, 0, 0);
+            cim[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa.x, xb.y, cim[t], 0, 0, 0);
+        };
+        if (lo) {
+            upd(0, x0, x0);
+            upd(1, x1, x0);
+        }
+        upd(2, x1, x1);
+        wave_sync();                                 // P is rewritten by the next panel
+    }
+    if (clk) g_small_clk[40] = __builtin_amdgcn_s_memtime();
+    // ---- back substitution L^H x = y (the column kernel's) -----------------------------------------
+    wave_sync();
+    double iv_n = dinv[L - 1];
+    cd lcr_n = sL[(L - 1) * LDR + (r & 31)];
+#pragma unroll 1
+    for (int c = L - 1; c >= 0; --c) {
+        const double iv = iv_n;
+        const cd lcr = lcr_n;
+        const int cp = c > 0 ? c - 1 : 0;
+        iv_n = dinv[cp];
+        lcr_n = sL[cp * LDR + (r & 31)];
+        if (r == c) {
+            Y[0] = cscale(Y[0], iv);
+            Y[1] = cscale(Y[1], iv);
+        }
+        cd xc[NR];
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr)
+            xc[rr] = cmk(lane_d(Y[rr >> 1].x, c + 32 * (rr & 1)), lane_d(Y[rr >> 1].y, c + 32 * (rr & 1)));
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int rr = h + 2 * q;
+            if (rr < NR) Y[q] = csel(r < c, csub(Y[q], cmulc(rhs_pick(xc, h, q), lcr)), Y[q]);
+        }
+    }
+    if (clk) g_small_clk[41] = __builtin_amdgcn_s_memtime();
+    cd* th = a.theta + (size_t)b * L * NR;
+    double nt = 0.0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int rr = h + 2 * k;
+        if (rin && rr < NR) {
+            th[r * NR + rr] = cconj(Y[k]);
+            nt += cabs2(Y[k]);
+        }
+    }
+    if (a.h_true) {                                  // the oracle early stop (early_stop_kernel)
+        const int K = L * NR;
+        double nh = 0.0;
+        for (int e = lane; e < K; e += 64) nh += cabs2(a.h_true[(size_t)b * K + e]);
+        nt = wave_sum_dpp(nt);
+        nh = wave_sum_dpp(nh);
+        if (lane == 0) {
+            if (a.iters_done) a.iters_done[b] = a.it + 1;
+            if (a.it != 0 && fabs(sqrt(nt) - sqrt(nh)) < 1.0) a.done_w[b] = 1;
+        }
+    }
+    if (lane == 0 && a.status && anybad) a.status[b] |= a.clamp_status;
+}
+
 template <int KB, int MNT>
 hipError_t launch_nr(const Problem& pb, const MstepArgs& a, size_t lds, int write_sys, int sg,
                      hipStream_t s) {
@@ -857,7 +1070,10 @@ hipError_t launch_mstep_small(const Problem& pb, const MstepArgs& a, bool write_
         if (g_debug.small_stop == 1) return hipGetLastError();      // DIAGNOSTIC: build only
         switch (pb.NR) {
 #define SBCE_MS2S(nr) case nr: \
-    hipLaunchKernelGGL((mstep_small2_solve_kernel<nr>), dim3(pb.B), dim3(64), 0, s, a, pb.L, g_debug.small_stop); \
+    if (g_debug.small_col) \
+        hipLaunchKernelGGL((mstep_small2_solve_kernel<nr>), dim3(pb.B), dim3(64), 0, s, a, pb.L, g_debug.small_stop); \
+    else \
+        hipLaunchKernelGGL((mstep_small3_solve_kernel<nr>), dim3(pb.B), dim3(64), 0, s, a, pb.L, g_debug.small_stop); \
     break;
             SBCE_MS2S(1) SBCE_MS2S(2) SBCE_MS2S(3) SBCE_MS2S(4)
 #undef SBCE_MS2S

@@ -247,13 +247,15 @@ struct DebugConfig {
     int small_stop;      // SBCE_SMALL_STOP=1|2|3  DIAGNOSTIC: the one-workgroup M-step stops after its
                          //                        build (1) / factorisation (2) / symbol staging
                          //                        without the build's arithmetic (3); results invalid
+    bool small_col;      // SBCE_SMALL_SOLVE=col   n_tx <= 2 small M-step: the round-6 column-by-column
+                         //                        solve instead of the 4-column-panel MFMA one
     char pm_impl;        // SBCE_PM_IMPL=wave      ZF/MMSE (n_tx <= 2) and PM (n_tx = 2, |A| = 1) E-steps
                          //                        one wave per symbol too; =t / =q the PM one thread /
                          //                        one quad per symbol at any size (all bitwise the
                          //                        same results; not flagged)
 };
 inline constexpr DebugConfig kDebugDefault = {false, false, false, false, false, 128, false, false,
-                                              false, true, false, false, false, 0, 0};
+                                              false, true, false, false, false, 0, false, 0};
 #if SBCE_AB
 extern DebugConfig g_debug;
 #else

@@ -503,7 +503,8 @@ def test_small_mstep_matches_batched_path(sbce, shape, solve):
     """L <= 64 (n_tx not 4, 8): R and B^H of the one-workgroup kernel's VALU build (P > 16;
     SBCE_MSTEP_SMALL=v forces it at P <= 16 too) are bitwise the batched build's (same per-element
     operation order); its MFMA builds (P <= 16: the round-6 mstep_small2_kernel for n_tx <= 2,
-    n_rx <= 4 -- block-per-wave three-MFMA build, one-wave solve -- and the round-5 kernel,
+    n_rx <= 4 -- block-per-wave three-MFMA build, one-wave solve by 4-column panels with MFMA
+    trailing updates, or column by column with SBCE_SMALL_SOLVE=col -- and the round-5 kernel,
     SBCE_MSTEP_SMALL=1) agree to 1e-13; the solves agree with the batched panel Cholesky
     (SBCE_MSTEP_SMALL=0) and numpy.linalg.solve; the same trials are flagged."""
     n_tx, n_rx, N, T_p, T_d, M = shape
@@ -513,8 +514,8 @@ def test_small_mstep_matches_batched_path(sbce, shape, solve):
     args = (b["y_d"], b["y_p"], b["psi_d"], b["u_p"], b["cons"], x, S, 0.1)
     with sbce._lib.debug_env(SBCE_MSTEP_SMALL="0"):
         th0, R0, rhs0, st0 = sbce.mstep_batch(*args, solve=solve)
-    for arm, env in (("default", {}), ("v1", {"SBCE_MSTEP_SMALL": "1"}),
-                     ("valu", {"SBCE_MSTEP_SMALL": "v"})):
+    for arm, env in (("default", {}), ("col", {"SBCE_SMALL_SOLVE": "col"}),
+                     ("v1", {"SBCE_MSTEP_SMALL": "1"}), ("valu", {"SBCE_MSTEP_SMALL": "v"})):
         with sbce._lib.debug_env(**env):
             th, R, rhs, st = sbce.mstep_batch(*args, solve=solve)
         wave = arm != "valu" and N + 1 <= 16 and n_tx <= 3
@@ -553,6 +554,39 @@ def test_small_mstep_full_em_matches_batched_path(sbce):
             it0 = eng0.iters_done.cpu().numpy()
         assert np.array_equal(it, it0), mode
         assert rel(th, th0) < 1e-9, mode
+
+
+@pytest.mark.parametrize("case", ["cfg5_small_mstep", "cfg1_shape_two_streams"])
+def test_captured_graph_replay_is_bitwise_the_eager_run(sbce, case):
+    """EMEngine.capture: the whole sbce_em call as one HIP graph (bench.py's cfg5 grid replays
+    them).  Replays give the eager run's theta, iters_done and status bitwise -- twice (the graph
+    restarts from theta_0), after the buffers were overwritten by another run, and with the
+    stream sub-batches' fork/join captured too."""
+    import torch
+    if case == "cfg5_small_mstep":
+        varn = np.array([float(sbce.signal_model.snr_to_varn(s, 42.0)) for s in (0.0, 30.0)])
+        b = sbce.signal_model.synthetic_batch(4, 2, 2, 15, 20, 45, 64, 1.0, seed=44, pinv="scipy")
+        varn = np.repeat(varn, 2)
+        kw = dict(mode="soft", early_stop=True)
+        iters = 6
+    else:
+        varn = float(sbce.signal_model.snr_to_varn(20.0))
+        b = sbce.signal_model.synthetic_batch(8, 4, 4, 64, 16, 64, 16, varn, seed=45)
+        kw = dict(mode="soft", streams=2)
+        iters = 3
+    eng = sbce.EMEngine(b, varn, **kw)
+    th = eng.run(iters).cpu().numpy()
+    it, st = eng.iters_done.cpu().numpy(), eng.status.cpu().numpy()
+    g = eng.capture(iters)
+    for _ in range(2):
+        eng.theta.fill_(float("nan"))
+        eng.iters_done.fill_(-1)
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(eng.theta.cpu().numpy(), th), case
+        assert np.array_equal(eng.iters_done.cpu().numpy(), it), case
+        assert np.array_equal(eng.status.cpu().numpy(), st), case
+    assert np.isfinite(th).all()
 
 
 @pytest.mark.parametrize("shape", [

@@ -29,7 +29,7 @@ def main():
     batch["cons"] = pts[0]["cons"]
     vt = np.repeat(varn, 64)
     for arm, env in (("small", {}), ("small_v1", {"SBCE_MSTEP_SMALL": "1"}),
-                     ("small_build", {"SBCE_SMALL_STOP": "1"}), ("small_factor", {"SBCE_SMALL_STOP": "2"}),
+                     ("small_build", {"SBCE_SMALL_STOP": "1"}), ("small_col", {"SBCE_SMALL_SOLVE": "col"}),
                      ("batched", {"SBCE_MSTEP_SMALL": "0"})):
         with pkg._lib.debug_env(**env):
             eng = pkg.EMEngine(batch, vt, mode="soft")
