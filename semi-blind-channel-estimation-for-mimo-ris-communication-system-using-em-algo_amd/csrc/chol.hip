@@ -342,12 +342,15 @@ __device__ __forceinline__ void diag_inverse_rd(const cd* A, cd* Di, const doubl
         const int bi = lane >> (2 * ls), rem = lane & (s * s - 1);
         const int i = rem >> ls, j = rem & (s - 1);
         const int b0 = bi * 2 * s;
+        // every operand read unconditionally (the entries a guard skips are finite: zeros of Di's
+        // strict upper part, or P entries) and the guarded FMAs as selects, so the reads can issue
+        // ahead of the FMA chain instead of one LDS latency per product (same sums, same order)
         if (on) {                                            // P = L21 D11 (D11 lower: m >= j)
             const cd* Lr = A + (b0 + s + i) * NB + b0;
             cd acc = czero();
 #pragma unroll
             for (int m = 0; m < s; ++m)
-                if (m >= j) acc = cfma(acc, Lr[m], Di[(b0 + m) * NB + b0 + j]);
+                acc = csel(m >= j, cfma(acc, Lr[m], Di[(b0 + m) * NB + b0 + j]), acc);
             P[(lane >> 3) * NB + (lane & 7)] = acc;
         }
         wave_sync();
@@ -356,10 +359,8 @@ __device__ __forceinline__ void diag_inverse_rd(const cd* A, cd* Di, const doubl
             cd acc = czero();
 #pragma unroll
             for (int m = 0; m < s; ++m) {
-                if (m <= i) {
-                    const int pe = bi * s * s + m * s + j;
-                    acc = cfma(acc, Dr[m], P[(pe >> 3) * NB + (pe & 7)]);
-                }
+                const int pe = bi * s * s + m * s + j;
+                acc = csel(m <= i, cfma(acc, Dr[m], P[(pe >> 3) * NB + (pe & 7)]), acc);
             }
             Di[(b0 + s + i) * NB + b0 + j] = (b0 + s + i < w) ? cmk(-acc.x, -acc.y) : czero();
         }
