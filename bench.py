@@ -629,7 +629,9 @@ def grid_roofline(args, g, engines, k_last, torch):
 
 def grid_main(args, ranks, pkg):
     """--config cfg5: one step = the whole SNR x T_d grid, five detector EMs per point, `trials`
-    Monte-Carlo trials per point on every rank.  Calls are spread over 3 HIP streams (--streams), each a captured HIP graph (--graphs), longest first onto the least loaded stream (--schedule lpt).  value =
+    Monte-Carlo trials per point on every rank.  Calls are spread over 3 HIP streams (--streams),
+    each a captured HIP graph (--graphs), longest first onto the least loaded stream (--schedule
+    lpt).  value =
     trial-iterations EXECUTED (the oracle early stop ends a trial's EM; iters_done) / time."""
     import torch
     g = dict(GRID[args.config])

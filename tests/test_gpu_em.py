@@ -497,6 +497,9 @@ def test_mfma_and_valu_cholesky_agree(sbce, shape):
     (2, 8, 31, 20, 100, 16),            # L = 64, n_rx = 8
     (1, 1, 0, 3, 2, 4),                 # L = 1
     (2, 2, 15, 4, 5, 4),                # T_p + T_d n_tx < L: clamped / dropped pivots
+    (2, 4, 15, 8, 30, 4),               # L = 32, n_rx = 4: the panel solve's widest right-hand side
+    (2, 3, 7, 6, 20, 16),               # L = 16, n_rx = 3: one tile column only
+    (1, 4, 12, 5, 20, 4),               # L = 13, n_rx = 4: a ragged last panel (13 = 3 * 4 + 1)
 ])
 @pytest.mark.parametrize("solve", ["chol", "drop"])
 def test_small_mstep_matches_batched_path(sbce, shape, solve):
