@@ -416,6 +416,12 @@ def parse_args(argv=None):
     ap.add_argument("--graphs", type=int, default=1,
                     help="cfg5: each sbce_em call replayed as one captured HIP graph (1, default) "
                          "or launched eagerly (0)")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES for this process (HIP's default 4) when the "
+                         "environment does not set it; at most 32")
+    ap.add_argument("--enqueue", choices=("serial", "threads"), default="serial",
+                    help="cfg5: the grid's calls enqueued by this thread, interleaved over the "
+                         "streams (serial), or by one host thread per stream (threads)")
     ap.add_argument("--schedule", choices=("lpt", "rr"), default="lpt",
                     help="cfg5: calls onto streams longest-first to the least loaded (lpt, by each "
                          "call's measured time) or round robin in grid order (rr)")
@@ -702,11 +708,30 @@ def grid_main(args, ranks, pkg):
             order[s_min].append(i)
             load[s_min] += call_ms[i]
 
+    pool = None
+    if args.enqueue == "threads":
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(len(streams))
+
+    def enqueue(st, o):                  # one stream's calls (a host thread of its own)
+        for i in o:
+            if graphs is None:
+                engines[i][3].run(iters, stream=st)
+            else:
+                with torch.cuda.stream(st):
+                    graphs[i].replay()
+
     def step():
         ev = torch.cuda.Event()
         ev.record(cur)
         for st in streams:
             st.wait_event(ev)
+        if pool is not None:
+            for f in [pool.submit(enqueue, st, o) for st, o in zip(streams, order)]:
+                f.result()
+            for st in streams:
+                cur.wait_stream(st)
+            return
         # calls are issued interleaved over the streams (the host enqueue never starves one)
         for r in range(max(len(o) for o in order)):
             for st, o in zip(streams, order):
@@ -731,8 +756,11 @@ def grid_main(args, ranks, pkg):
         step()
     ranks.barrier()
     t0 = time.perf_counter()
+    host = 0.0                        # host time inside step(): the enqueue of the grid's launches
     for _ in range(args.steps):
+        th = time.perf_counter()
         step()
+        host += time.perf_counter() - th
     torch.cuda.synchronize()
     ranks.barrier()
     elapsed = ranks.max_time(time.perf_counter() - t0)
@@ -769,7 +797,7 @@ def grid_main(args, ranks, pkg):
                    "partition_r": g["partition_r"], "solve": "chol", "early_stop": "oracle (h)",
                    "grid_batch": args.grid_batch, "sbce_em_calls_per_step": len(engines),
                    "streams_per_gpu": len(streams), "hip_graphs": graphs is not None,
-                   "schedule": args.schedule,
+                   "schedule": args.schedule, "enqueue": args.enqueue,
                    "call_ms_sum": None if call_ms is None else float(sum(call_ms)),
                    "parallelism": f"trials-sharded x{world}"},
         "value_note": ("value counts the trial-iterations the EMs executed (each EM stops at the "
@@ -777,6 +805,7 @@ def grid_main(args, ranks, pkg):
                        f"nominal {nominal * world:.0f} per step (all {iters} iterations), executed "
                        f"{executed:.0f}"),
         "executed_iterations_per_step": executed,
+        "host_enqueue_ms_per_step": host / args.steps * 1e3,
         "nominal_iterations_per_step": nominal * world,
         "nmse_grid_mean": {det: float(np.mean(mean[di])) for di, det in enumerate(dets)},
         "nmse_at_max_td": {det: [float(v) for v in mean[di, -1]] for di, det in enumerate(dets)},
@@ -809,6 +838,9 @@ def main(argv=None):
     # the same schedule: the RCCL communicator (and its streams) is created lazily at the
     # accumulator all-reduce after the timed region.
     nstreams = args.streams if args.streams is not None else (3 if args.config == "cfg1" else 1)
+    if args.hw_queues and "GPU_MAX_HW_QUEUES" not in os.environ:
+        # hardware queues per process: read once by the HIP runtime, so before torch loads it
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     import torch
     import __graft_entry__ as ge
     pkg = ge.package()
