@@ -426,7 +426,7 @@ def parse_args(argv=None):
                     help="cfg5: calls onto streams longest-first to the least loaded (lpt, by each "
                          "call's measured time) or round robin in grid order (rr)")
     ap.add_argument("--streams", type=int, default=None,
-                    help="sub-batches on concurrent HIP streams per GPU (default: 3 at cfg1, else 1)")
+                    help="sub-batches on concurrent HIP streams per GPU (default: 3 at cfg1, 4 for the cfg5 grid's calls, else 1)")
     ap.add_argument("--rccl-init", choices=["lazy", "eager"], default="lazy",
                     help="multi-rank runs: create the RCCL communicator at its first collective "
                          "(after the timed region; default) or at process-group init")
@@ -635,7 +635,7 @@ def grid_roofline(args, g, engines, k_last, torch):
 
 def grid_main(args, ranks, pkg):
     """--config cfg5: one step = the whole SNR x T_d grid, five detector EMs per point, `trials`
-    Monte-Carlo trials per point on every rank.  Calls are spread over 3 HIP streams (--streams),
+    Monte-Carlo trials per point on every rank.  Calls are spread over 4 HIP streams (--streams),
     each a captured HIP graph (--graphs), longest first onto the least loaded stream (--schedule
     lpt).  value =
     trial-iterations EXECUTED (the oracle early stop ends a trial's EM; iters_done) / time."""
@@ -674,7 +674,7 @@ def grid_main(args, ranks, pkg):
                 engines.append((di, k, js, eng))
         del pts
     torch.cuda.synchronize()
-    streams = [torch.cuda.Stream() for _ in range(args.streams or 3)]
+    streams = [torch.cuda.Stream() for _ in range(args.streams or 4)]
     cur = torch.cuda.current_stream()
     graphs = None
     if args.graphs and not args.roofline_only:
@@ -838,6 +838,10 @@ def main(argv=None):
     # the same schedule: the RCCL communicator (and its streams) is created lazily at the
     # accumulator all-reduce after the timed region.
     nstreams = args.streams if args.streams is not None else (3 if args.config == "cfg1" else 1)
+    if args.hw_queues is None and args.config in GRID:
+        # the grid's latency-bound calls: 4 streams on 8 hardware queues measured best on one box
+        # (16.06 ms vs 17.07-17.42 with 3 on the default 4; profiles/r06/cfg5_streams/)
+        args.hw_queues = 8
     if args.hw_queues and "GPU_MAX_HW_QUEUES" not in os.environ:
         # hardware queues per process: read once by the HIP runtime, so before torch loads it
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
